@@ -1,0 +1,273 @@
+// Fp arithmetic for BLS12-381 on gfx950: 381-bit prime field, 12 x 32-bit limbs per element,
+// Montgomery form with R = 2^384.  One lane owns one element; every carry chain stays in VGPRs
+// (32x32->64 v_mad_u64_u32 + v_add_co/v_addc_co).  All values are kept fully reduced in [0, p),
+// so equality and zero tests are limb compares.
+//
+// This replaces the mcl Fp layer that herumi/bls-eth-go-binary v1.32.1 links into charon's
+// tbls.Herumi (/root/reference/tbls/herumi.go:12); see DESIGN.md for the roofline unit
+// (one fp_mul = one "Fp-mul-equivalent").
+#pragma once
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BLS_HD __host__ __device__
+#define BLS_INLINE static __forceinline__
+#else
+#define BLS_HD
+#define BLS_INLINE static inline
+#endif
+#define BLS_NOINLINE static __attribute__((noinline))
+
+namespace bls {
+
+struct fp {
+  uint32_t v[12];
+};
+struct fp2 {
+  fp c0, c1;
+};
+
+}  // namespace bls
+
+#include "bls_constants.h"
+
+#if defined(BLS_COUNT_OPS)
+namespace bls {
+// Host-only instrumentation (tests/native builds): counts the Fp multiplications an operation
+// performs -- the algorithmic unit behind bench.py's roofline.
+extern thread_local uint64_t g_fp_mul_count;
+extern thread_local uint64_t g_fp_sqr_count;
+}  // namespace bls
+#define BLS_COUNT_MUL() (++::bls::g_fp_mul_count)
+#define BLS_COUNT_SQR() (++::bls::g_fp_sqr_count)
+#else
+#define BLS_COUNT_MUL() ((void)0)
+#define BLS_COUNT_SQR() ((void)0)
+#endif
+
+namespace bls {
+
+BLS_HD BLS_INLINE void fp_set_zero(fp& r) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = 0;
+}
+
+BLS_HD BLS_INLINE void fp_set_one(fp& r) { r = FP_ONE; }
+
+BLS_HD BLS_INLINE bool fp_is_zero(const fp& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc |= a.v[i];
+  return acc == 0;
+}
+
+BLS_HD BLS_INLINE bool fp_eq(const fp& a, const fp& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc |= a.v[i] ^ b.v[i];
+  return acc == 0;
+}
+
+// r = a + b mod p
+BLS_HD BLS_INLINE void fp_add(fp& r, const fp& a, const fp& b) {
+  uint32_t s[12];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)a.v[i] + b.v[i];
+    s[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  // s < 2p < 2^384, no carry out; subtract p and keep if no borrow
+  uint32_t d[12];
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    br += (int64_t)s[i] - P_LIMBS[i];
+    d[i] = (uint32_t)br;
+    br >>= 32;
+  }
+  const bool keep_s = br < 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = keep_s ? s[i] : d[i];
+}
+
+// r = a - b mod p
+BLS_HD BLS_INLINE void fp_sub(fp& r, const fp& a, const fp& b) {
+  uint32_t d[12];
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    br += (int64_t)a.v[i] - b.v[i];
+    d[i] = (uint32_t)br;
+    br >>= 32;
+  }
+  const uint32_t mask = br < 0 ? 0xffffffffu : 0u;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)d[i] + (P_LIMBS[i] & mask);
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+
+BLS_HD BLS_INLINE void fp_neg(fp& r, const fp& a) {
+  fp z;
+  fp_set_zero(z);
+  fp_sub(r, z, a);
+}
+
+BLS_HD BLS_INLINE void fp_dbl(fp& r, const fp& a) { fp_add(r, a, a); }
+
+// Montgomery product r = a*b*R^-1 mod p.  CIOS with the "no-carry" shortcut: p's top limb
+// 0x1a0111ea < 2^31 - 1, so the running sum never needs a 14th word.
+BLS_HD BLS_INLINE void fp_mul_impl(fp& r, const fp& a, const fp& b) {
+  uint32_t t[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint32_t bi = b.v[i];
+    uint64_t A = (uint64_t)a.v[0] * bi + t[0];
+    t[0] = (uint32_t)A;
+    const uint32_t m = t[0] * P_INV32;
+    uint64_t C = (uint64_t)m * P_LIMBS[0] + t[0];
+#pragma unroll
+    for (int j = 1; j < 12; ++j) {
+      A = (uint64_t)a.v[j] * bi + t[j] + (A >> 32);
+      t[j] = (uint32_t)A;
+      C = (uint64_t)m * P_LIMBS[j] + t[j] + (C >> 32);
+      t[j - 1] = (uint32_t)C;
+    }
+    t[11] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+  }
+  // t < 2p: conditional subtraction
+  uint32_t d[12];
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    br += (int64_t)t[i] - P_LIMBS[i];
+    d[i] = (uint32_t)br;
+    br >>= 32;
+  }
+  const bool keep_t = br < 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = keep_t ? t[i] : d[i];
+}
+
+// The non-inlined, by-value entry points keep kernels' instruction footprint small (a fully
+// inlined Miller loop would not fit the instruction cache) while passing operands in VGPRs
+// rather than through the private stack.
+BLS_HD BLS_NOINLINE fp fp_mul_v(fp a, fp b) {
+  BLS_COUNT_MUL();
+  fp r;
+  fp_mul_impl(r, a, b);
+  return r;
+}
+BLS_HD BLS_NOINLINE fp fp_sqr_v(fp a) {
+  BLS_COUNT_SQR();
+  fp r;
+  fp_mul_impl(r, a, a);
+  return r;
+}
+BLS_HD BLS_INLINE void fp_mul(fp& r, const fp& a, const fp& b) { r = fp_mul_v(a, b); }
+BLS_HD BLS_INLINE void fp_sqr(fp& r, const fp& a) { r = fp_sqr_v(a); }
+
+// r = a^e for a fixed exponent given as little-endian 32-bit limbs whose top set bit is top_bit
+// (left-to-right binary; the exponent is the same for every lane, so the branch is uniform).
+BLS_HD BLS_INLINE void fp_pow(fp& r, const fp& a, const uint32_t* e, int top_bit) {
+  fp acc = a;
+  for (int i = top_bit - 1; i >= 0; --i) {
+    fp_sqr(acc, acc);
+    if ((e[i >> 5] >> (i & 31)) & 1u) fp_mul(acc, acc, a);
+  }
+  r = acc;
+}
+
+BLS_HD BLS_INLINE void fp_mul_small(fp& r, const fp& a, uint32_t k) {
+  // r = k*a mod p for tiny k by repeated doubling/adding (k <= 16)
+  fp acc;
+  fp_set_zero(acc);
+  fp base = a;
+  while (k) {
+    if (k & 1) fp_add(acc, acc, base);
+    fp_add(base, base, base);
+    k >>= 1;
+  }
+  r = acc;
+}
+
+BLS_HD BLS_INLINE void fp_inv(fp& r, const fp& a) { fp_pow(r, a, EXP_P_MINUS_2, 380); }
+
+// Returns true and r = sqrt(a) when a is a square (p = 3 mod 4: r = a^((p+1)/4)).
+BLS_HD BLS_INLINE bool fp_sqrt(fp& r, const fp& a) {
+  fp s, s2;
+  fp_pow(s, a, EXP_SQRT, 378);
+  fp_sqr(s2, s);
+  r = s;
+  return fp_eq(s2, a);
+}
+
+BLS_HD BLS_INLINE void fp_to_mont(fp& r, const fp& a) {
+  fp r2;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r2.v[i] = R2_LIMBS[i];
+  fp_mul(r, a, r2);
+}
+
+BLS_HD BLS_INLINE void fp_from_mont(fp& r, const fp& a) {
+  fp one;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) one.v[i] = i == 0 ? 1u : 0u;
+  fp_mul(r, a, one);
+}
+
+// Plain (non-Montgomery) value compare: is a > (p-1)/2 ?  'a' must be canonical (from_mont'd).
+BLS_HD BLS_INLINE bool fp_plain_gt_half(const fp& a) {
+  // (p-1)/2 limbs
+  constexpr uint32_t H[12] = {0xffffd555u, 0xdcff7fffu, 0x58a9ffffu, 0x0f55ffffu, 0x7b587b12u, 0xb3986950u,
+                              0x79c2895fu, 0xb23ba5c2u, 0x21a5d66bu, 0x258dd3dbu, 0x1cbff34du, 0x0d0088f5u};
+  // compute H - a; borrow => a > H
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    br += (int64_t)H[i] - a.v[i];
+    br >>= 32;
+  }
+  return br < 0;
+}
+
+// Is the plain value a < p ?
+BLS_HD BLS_INLINE bool fp_plain_lt_p(const fp& a) {
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    br += (int64_t)a.v[i] - P_LIMBS[i];
+    br >>= 32;
+  }
+  return br < 0;
+}
+
+// 48 big-endian bytes -> plain limbs
+BLS_HD BLS_INLINE void fp_plain_from_be48(fp& r, const uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint8_t* q = b + 44 - 4 * i;
+    r.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | (uint32_t)q[3];
+  }
+}
+
+BLS_HD BLS_INLINE void fp_plain_to_be48(uint8_t* b, const fp& a) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint8_t* q = b + 44 - 4 * i;
+    q[0] = (uint8_t)(a.v[i] >> 24);
+    q[1] = (uint8_t)(a.v[i] >> 16);
+    q[2] = (uint8_t)(a.v[i] >> 8);
+    q[3] = (uint8_t)a.v[i];
+  }
+}
+
+}  // namespace bls

@@ -1,0 +1,94 @@
+// Per-item operations of the tbls.Implementation hot path, written once and called by the HIP
+// kernels (one lane per item).  Status codes mirror the three error strings of
+// tbls.Herumi.Verify (/root/reference/tbls/herumi.go:285-301):
+//   HIPBLS_OK = 0, HIPBLS_ERR_PUBKEY = 1 ("cannot set compressed public key in Herumi format"),
+//   HIPBLS_ERR_SIGNATURE = 2 ("cannot unmarshal signature into Herumi signature"),
+//   HIPBLS_ERR_VERIFY = 3 ("signature not verified").
+#pragma once
+#include "../../include/hipbls.h"
+#include "fr.h"
+#include "h2c.h"
+#include "pairing.h"
+
+namespace bls {
+
+// Verify with pk and sig already decoded (affine, subgroup-checked) and H(m) already hashed.
+BLS_HD BLS_INLINE bool pairing_check_verify(const g1a& pk, const g2a& hm, const g2a& sig) {
+  // e(pk, H(m)) * e(-g1, sig) == 1
+  g1a P[2];
+  g2a Q[2];
+  bool skip[2] = {false, false};
+  P[0] = pk;
+  Q[0] = hm;
+  P[1].x = G1_GEN_X;
+  P[1].y = G1_NEG_GEN_Y;
+  Q[1] = sig;
+  fp12 f, e;
+  miller_loop_n(f, P, Q, skip, 2);
+  final_exponentiation(e, f);
+  return fp12_is_one(e);
+}
+
+// Full tbls.Verify for one item (used by the fused kernel and host-side instrumentation).
+
+// sigma = sk * H(msg); returns HIPBLS_OK or HIPBLS_ERR_SECRET
+
+// pk = sk * g1; zero secret is an error (GetSafePublicKey, herumi.go:74)
+
+// Lagrange coefficient at 0 for the i-th id of a set (ids small positive integers, distinct)
+BLS_HD BLS_INLINE void lagrange_at_zero(fr& out_plain, const uint32_t* ids, int n, int i) {
+  fr num, den, t, xi, xj;
+  fr_from_u32(num, 1);
+  fr_from_u32(den, 1);
+  fr_from_u32(xi, ids[i]);
+  for (int j = 0; j < n; ++j) {
+    if (j == i) continue;
+    fr_from_u32(xj, ids[j]);
+    fr_mul(num, num, xj);
+    fr_sub(t, xj, xi);
+    fr_mul(den, den, t);
+  }
+  fr_inv(den, den);
+  fr_mul(t, num, den);
+  fr_to_plain(out_plain, t);
+}
+
+BLS_HD BLS_INLINE int op_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96) {
+  g1a pk;
+  const int dp = g1_decompress(pk, pk48, true);
+  if (dp == DEC_BAD) return HIPBLS_ERR_PUBKEY;
+  g2a sig;
+  const int ds = g2_decompress(sig, sig96, true);
+  if (ds == DEC_BAD) return HIPBLS_ERR_SIGNATURE;
+  if (dp == DEC_INF || ds == DEC_INF) return HIPBLS_ERR_VERIFY;  // KeyValidate / e(pk,H) != 1
+  g2j hj;
+  hash_to_g2(hj, msg, msg_len, DST_POP, 43);
+  g2a hm;
+  jac_to_aff(hm, hj);
+  return pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+}
+
+BLS_HD BLS_INLINE int op_sign(uint8_t* out96, const uint8_t* sk32, const uint8_t* msg, uint32_t msg_len) {
+  fr sk;
+  if (!fr_plain_from_be32(sk, sk32)) return HIPBLS_ERR_SECRET;
+  g2j h, s;
+  hash_to_g2(h, msg, msg_len, DST_POP, 43);
+  jac_mul_limbs(s, h, sk.v, 8);
+  g2_compress(out96, s);
+  return HIPBLS_OK;
+}
+
+BLS_HD BLS_INLINE int op_sk_to_pk(uint8_t* out48, const uint8_t* sk32) {
+  fr sk;
+  if (!fr_plain_from_be32(sk, sk32)) return HIPBLS_ERR_SECRET;
+  if (fr_is_zero(sk)) return HIPBLS_ERR_SECRET;
+  g1j g, pk;
+  g.x = G1_GEN_X;
+  g.y = G1_GEN_Y;
+  fp_set_one(g.z);
+  jac_mul_limbs(pk, g, sk.v, 8);
+  g1_compress(out48, pk);
+  return HIPBLS_OK;
+}
+
+}  // namespace bls

@@ -1,0 +1,403 @@
+// Extension tower for BLS12-381:  Fp2 = Fp[u]/(u^2+1),  Fp6 = Fp2[v]/(v^3-xi),  Fp12 = Fp6[w]/(w^2-v),
+// xi = 1+u.  Same tower as the oracle (oracle/bls12381.py) so Fp12 values are comparable limb for
+// limb, but the formulas here are the lane-local Karatsuba / sparse forms the kernels run.
+#pragma once
+#include "field.h"
+
+namespace bls {
+
+struct fp6 {
+  fp2 c0, c1, c2;
+};
+struct fp12 {
+  fp6 c0, c1;
+};
+
+// ---------------------------------------------------------------------------------- Fp2
+BLS_HD BLS_INLINE void fp2_set_zero(fp2& r) {
+  fp_set_zero(r.c0);
+  fp_set_zero(r.c1);
+}
+BLS_HD BLS_INLINE void fp2_set_one(fp2& r) {
+  fp_set_one(r.c0);
+  fp_set_zero(r.c1);
+}
+BLS_HD BLS_INLINE bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+BLS_HD BLS_INLINE bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+BLS_HD BLS_INLINE void fp2_add(fp2& r, const fp2& a, const fp2& b) {
+  fp_add(r.c0, a.c0, b.c0);
+  fp_add(r.c1, a.c1, b.c1);
+}
+BLS_HD BLS_INLINE void fp2_sub(fp2& r, const fp2& a, const fp2& b) {
+  fp_sub(r.c0, a.c0, b.c0);
+  fp_sub(r.c1, a.c1, b.c1);
+}
+BLS_HD BLS_INLINE void fp2_neg(fp2& r, const fp2& a) {
+  fp_neg(r.c0, a.c0);
+  fp_neg(r.c1, a.c1);
+}
+BLS_HD BLS_INLINE void fp2_dbl(fp2& r, const fp2& a) { fp2_add(r, a, a); }
+BLS_HD BLS_INLINE void fp2_conj(fp2& r, const fp2& a) {
+  r.c0 = a.c0;
+  fp_neg(r.c1, a.c1);
+}
+BLS_HD BLS_INLINE void fp2_mul_fp(fp2& r, const fp2& a, const fp& b) {
+  fp_mul(r.c0, a.c0, b);
+  fp_mul(r.c1, a.c1, b);
+}
+// (a0 + a1 u)(1 + u) = (a0 - a1) + (a0 + a1) u
+BLS_HD BLS_INLINE void fp2_mul_xi(fp2& r, const fp2& a) {
+  fp t;
+  fp_sub(t, a.c0, a.c1);
+  fp_add(r.c1, a.c0, a.c1);
+  r.c0 = t;
+}
+BLS_HD BLS_INLINE void fp2_mul_small(fp2& r, const fp2& a, uint32_t k) {
+  fp_mul_small(r.c0, a.c0, k);
+  fp_mul_small(r.c1, a.c1, k);
+}
+
+
+// ---------------------------------------------------------------------------------- Fp6
+BLS_HD BLS_INLINE void fp6_set_zero(fp6& r) {
+  fp2_set_zero(r.c0);
+  fp2_set_zero(r.c1);
+  fp2_set_zero(r.c2);
+}
+BLS_HD BLS_INLINE void fp6_set_one(fp6& r) {
+  fp2_set_one(r.c0);
+  fp2_set_zero(r.c1);
+  fp2_set_zero(r.c2);
+}
+BLS_HD BLS_INLINE void fp6_add(fp6& r, const fp6& a, const fp6& b) {
+  fp2_add(r.c0, a.c0, b.c0);
+  fp2_add(r.c1, a.c1, b.c1);
+  fp2_add(r.c2, a.c2, b.c2);
+}
+BLS_HD BLS_INLINE void fp6_sub(fp6& r, const fp6& a, const fp6& b) {
+  fp2_sub(r.c0, a.c0, b.c0);
+  fp2_sub(r.c1, a.c1, b.c1);
+  fp2_sub(r.c2, a.c2, b.c2);
+}
+BLS_HD BLS_INLINE void fp6_neg(fp6& r, const fp6& a) {
+  fp2_neg(r.c0, a.c0);
+  fp2_neg(r.c1, a.c1);
+  fp2_neg(r.c2, a.c2);
+}
+// r = a * v
+BLS_HD BLS_INLINE void fp6_mul_v(fp6& r, const fp6& a) {
+  fp2 t;
+  fp2_mul_xi(t, a.c2);
+  r.c2 = a.c1;
+  r.c1 = a.c0;
+  r.c0 = t;
+}
+// r = a * (b0 + b1 v)
+// r = a * (b1 v)
+
+// ---------------------------------------------------------------------------------- Fp12
+BLS_HD BLS_INLINE void fp12_set_one(fp12& r) {
+  fp6_set_one(r.c0);
+  fp6_set_zero(r.c1);
+}
+BLS_HD BLS_INLINE bool fp12_is_one(const fp12& a) {
+  fp12 one;
+  fp12_set_one(one);
+  bool eq = true;
+  const fp* x = &a.c0.c0.c0;
+  const fp* y = &one.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) eq = eq && fp_eq(x[i], y[i]);
+  return eq;
+}
+BLS_HD BLS_INLINE void fp12_conj(fp12& r, const fp12& a) {
+  r.c0 = a.c0;
+  fp6_neg(r.c1, a.c1);
+}
+// f *= line with the M-twist sparse shape (g0 + g1 v) + (h1 v) w
+// Frobenius x -> x^(p^j), j in {1,2,3}
+// Granger-Scott squaring for elements of the cyclotomic subgroup
+
+BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
+  // Karatsuba: 3 Fp products
+  fp t0, t1, t2, s0, s1;
+  fp_mul(t0, a.c0, b.c0);
+  fp_mul(t1, a.c1, b.c1);
+  fp_add(s0, a.c0, a.c1);
+  fp_add(s1, b.c0, b.c1);
+  fp_mul(t2, s0, s1);
+  fp_sub(r.c0, t0, t1);
+  fp_sub(t2, t2, t0);
+  fp_sub(r.c1, t2, t1);
+}
+BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
+  // (a0+a1)(a0-a1) + 2 a0 a1 u
+  fp s, d, m;
+  fp_add(s, a.c0, a.c1);
+  fp_sub(d, a.c0, a.c1);
+  fp_mul(m, a.c0, a.c1);
+  fp_mul(r.c0, s, d);
+  fp_add(r.c1, m, m);
+}
+BLS_HD BLS_INLINE void fp2_inv(fp2& r, const fp2& a) {
+  fp t0, t1;
+  fp_sqr(t0, a.c0);
+  fp_sqr(t1, a.c1);
+  fp_add(t0, t0, t1);
+  fp_inv(t1, t0);
+  fp_mul(r.c0, a.c0, t1);
+  fp_mul(t0, a.c1, t1);
+  fp_neg(r.c1, t0);
+}
+
+BLS_HD BLS_INLINE void fp6_mul(fp6& r, const fp6& a, const fp6& b) {
+  // Karatsuba over Fp2 (6 Fp2 products)
+  fp2 t0, t1, t2, s0, s1, u0, u1, u2;
+  fp2_mul(t0, a.c0, b.c0);
+  fp2_mul(t1, a.c1, b.c1);
+  fp2_mul(t2, a.c2, b.c2);
+  // c0 = t0 + xi((a1+a2)(b1+b2) - t1 - t2)
+  fp2_add(s0, a.c1, a.c2);
+  fp2_add(s1, b.c1, b.c2);
+  fp2_mul(u0, s0, s1);
+  fp2_sub(u0, u0, t1);
+  fp2_sub(u0, u0, t2);
+  fp2_mul_xi(u0, u0);
+  fp2_add(u0, u0, t0);
+  // c1 = (a0+a1)(b0+b1) - t0 - t1 + xi t2
+  fp2_add(s0, a.c0, a.c1);
+  fp2_add(s1, b.c0, b.c1);
+  fp2_mul(u1, s0, s1);
+  fp2_sub(u1, u1, t0);
+  fp2_sub(u1, u1, t1);
+  fp2 x2;
+  fp2_mul_xi(x2, t2);
+  fp2_add(u1, u1, x2);
+  // c2 = (a0+a2)(b0+b2) - t0 - t2 + t1
+  fp2_add(s0, a.c0, a.c2);
+  fp2_add(s1, b.c0, b.c2);
+  fp2_mul(u2, s0, s1);
+  fp2_sub(u2, u2, t0);
+  fp2_sub(u2, u2, t2);
+  fp2_add(u2, u2, t1);
+  r.c0 = u0;
+  r.c1 = u1;
+  r.c2 = u2;
+}
+BLS_HD BLS_INLINE void fp6_sqr(fp6& r, const fp6& a) {
+  // Chung-Hasan SQR2
+  fp2 s0, s1, s2, s3, s4, t;
+  fp2_sqr(s0, a.c0);
+  fp2_mul(s1, a.c0, a.c1);
+  fp2_dbl(s1, s1);
+  fp2_sub(t, a.c0, a.c1);
+  fp2_add(t, t, a.c2);
+  fp2_sqr(s2, t);
+  fp2_mul(s3, a.c1, a.c2);
+  fp2_dbl(s3, s3);
+  fp2_sqr(s4, a.c2);
+  fp2 c0, c1, c2;
+  fp2_mul_xi(c0, s3);
+  fp2_add(c0, c0, s0);
+  fp2_mul_xi(c1, s4);
+  fp2_add(c1, c1, s1);
+  fp2_add(c2, s1, s2);
+  fp2_add(c2, c2, s3);
+  fp2_sub(c2, c2, s0);
+  fp2_sub(c2, c2, s4);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+BLS_HD BLS_INLINE void fp6_inv(fp6& r, const fp6& a) {
+  fp2 c0, c1, c2, t, s;
+  fp2_sqr(c0, a.c0);
+  fp2_mul(t, a.c1, a.c2);
+  fp2_mul_xi(t, t);
+  fp2_sub(c0, c0, t);
+  fp2_sqr(c1, a.c2);
+  fp2_mul_xi(c1, c1);
+  fp2_mul(t, a.c0, a.c1);
+  fp2_sub(c1, c1, t);
+  fp2_sqr(c2, a.c1);
+  fp2_mul(t, a.c0, a.c2);
+  fp2_sub(c2, c2, t);
+  fp2_mul(t, a.c2, c1);
+  fp2_mul(s, a.c1, c2);
+  fp2_add(t, t, s);
+  fp2_mul_xi(t, t);
+  fp2_mul(s, a.c0, c0);
+  fp2_add(t, t, s);
+  fp2_inv(t, t);
+  fp2_mul(r.c0, c0, t);
+  fp2_mul(r.c1, c1, t);
+  fp2_mul(r.c2, c2, t);
+}
+BLS_HD BLS_INLINE void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& b1) {
+  // (a0 + a1 v + a2 v^2)(b0 + b1 v): 5 Fp2 products
+  fp2 t0, t1, s0, s1, u;
+  fp2_mul(t0, a.c0, b0);
+  fp2_mul(t1, a.c1, b1);
+  fp2 c0, c1, c2;
+  // c0 = t0 + xi * a2 b1
+  fp2_mul(u, a.c2, b1);
+  fp2_mul_xi(u, u);
+  fp2_add(c0, u, t0);
+  // c1 = (a0+a1)(b0+b1) - t0 - t1
+  fp2_add(s0, a.c0, a.c1);
+  fp2_add(s1, b0, b1);
+  fp2_mul(c1, s0, s1);
+  fp2_sub(c1, c1, t0);
+  fp2_sub(c1, c1, t1);
+  // c2 = a2 b0 + t1
+  fp2_mul(c2, a.c2, b0);
+  fp2_add(c2, c2, t1);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+BLS_HD BLS_INLINE void fp6_mul_1(fp6& r, const fp6& a, const fp2& b1) {
+  // (a0 + a1 v + a2 v^2) b1 v = xi a2 b1 + a0 b1 v + a1 b1 v^2
+  fp2 c0, c1, c2;
+  fp2_mul(c0, a.c2, b1);
+  fp2_mul_xi(c0, c0);
+  fp2_mul(c1, a.c0, b1);
+  fp2_mul(c2, a.c1, b1);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+
+BLS_HD BLS_INLINE void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
+  fp6 t0, t1, s0, s1;
+  fp6_mul(t0, a.c0, b.c0);
+  fp6_mul(t1, a.c1, b.c1);
+  fp6_add(s0, a.c0, a.c1);
+  fp6_add(s1, b.c0, b.c1);
+  fp6 c1;
+  fp6_mul(c1, s0, s1);
+  fp6_sub(c1, c1, t0);
+  fp6_sub(c1, c1, t1);
+  fp6_mul_v(t1, t1);
+  fp6_add(r.c0, t0, t1);
+  r.c1 = c1;
+}
+BLS_HD BLS_INLINE void fp12_sqr(fp12& r, const fp12& a) {
+  // complex squaring: c0 = (a0+a1)(a0+v a1) - t - v t, c1 = 2t, t = a0 a1
+  fp6 t, s0, s1, vt;
+  fp6_mul(t, a.c0, a.c1);
+  fp6_add(s0, a.c0, a.c1);
+  fp6_mul_v(s1, a.c1);
+  fp6_add(s1, s1, a.c0);
+  fp6_mul(s0, s0, s1);
+  fp6_sub(s0, s0, t);
+  fp6_mul_v(vt, t);
+  fp6_sub(r.c0, s0, vt);
+  fp6_add(r.c1, t, t);
+}
+BLS_HD BLS_INLINE void fp12_inv(fp12& r, const fp12& a) {
+  fp6 t0, t1;
+  fp6_sqr(t0, a.c0);
+  fp6_sqr(t1, a.c1);
+  fp6_mul_v(t1, t1);
+  fp6_sub(t0, t0, t1);
+  fp6_inv(t0, t0);
+  fp6_mul(r.c0, a.c0, t0);
+  fp6_mul(t1, a.c1, t0);
+  fp6_neg(r.c1, t1);
+}
+BLS_HD BLS_INLINE void fp12_mul_line(fp12& f, const fp2& g0, const fp2& g1, const fp2& h1) {
+  // f = (a0 + a1 w)(G + H w), G = g0 + g1 v, H = h1 v:
+  //   c0 = a0 G + v (a1 H),  c1 = (a0 + a1)(G + H) - a0 G - a1 H
+  fp6 t0, t1, s;
+  fp6_mul_01(t0, f.c0, g0, g1);
+  fp6_mul_1(t1, f.c1, h1);
+  fp6_add(s, f.c0, f.c1);
+  fp2 gh1;
+  fp2_add(gh1, g1, h1);
+  fp6_mul_01(s, s, g0, gh1);
+  fp6_sub(s, s, t0);
+  fp6_sub(f.c1, s, t1);
+  fp6_mul_v(t1, t1);
+  fp6_add(f.c0, t0, t1);
+}
+BLS_HD BLS_INLINE void fp12_frobenius(fp12& r, const fp12& a, int j) {
+  // coefficient of w^k (k = 2i + h for a.c_h.c_i) is conj^j(c) * gamma_{j,k}
+  const fp2* g = j == 1 ? FROB1 : (j == 2 ? FROB2 : FROB3);
+  const fp2* src[6] = {&a.c0.c0, &a.c1.c0, &a.c0.c1, &a.c1.c1, &a.c0.c2, &a.c1.c2};
+  fp2* dst[6] = {&r.c0.c0, &r.c1.c0, &r.c0.c1, &r.c1.c1, &r.c0.c2, &r.c1.c2};
+  fp2 tmp[6];
+  for (int k = 0; k < 6; ++k) {
+    fp2 c = *src[k];
+    if (j & 1) fp2_conj(c, c);
+    if (k == 0)
+      tmp[k] = c;
+    else
+      fp2_mul(tmp[k], c, g[k]);
+  }
+  for (int k = 0; k < 6; ++k) *dst[k] = tmp[k];
+}
+BLS_HD BLS_INLINE void fp12_cyclotomic_sqr(fp12& r, const fp12& a) {
+  // Granger-Scott: view a in Fp4^3 with Fp4 = Fp2[s]/(s^2 - xi), s = w^3... pairs
+  // (g0,g1) := (c0.c0, c1.c1), (g2,g3) := (c1.c0, c0.c2), (g4,g5) := (c0.c1, c1.c2)
+  fp2 z0 = a.c0.c0, z4 = a.c0.c1, z3 = a.c0.c2;
+  fp2 z2 = a.c1.c0, z1 = a.c1.c1, z5 = a.c1.c2;
+  fp2 t0, t1, t2, t3, tmp, tmp2;
+  // fp4_sqr(z0, z1) -> (t0, t1)
+  fp2_sqr(tmp, z0);
+  fp2_sqr(tmp2, z1);
+  fp2_mul_xi(t0, tmp2);
+  fp2_add(t0, t0, tmp);
+  fp2_add(t1, z0, z1);
+  fp2_sqr(t1, t1);
+  fp2_sub(t1, t1, tmp);
+  fp2_sub(t1, t1, tmp2);
+  // fp4_sqr(z2, z3) -> (t2, t3)
+  fp2_sqr(tmp, z2);
+  fp2_sqr(tmp2, z3);
+  fp2_mul_xi(t2, tmp2);
+  fp2_add(t2, t2, tmp);
+  fp2_add(t3, z2, z3);
+  fp2_sqr(t3, t3);
+  fp2_sub(t3, t3, tmp);
+  fp2_sub(t3, t3, tmp2);
+  // fp4_sqr(z4, z5) -> (t4, t5)
+  fp2 t4, t5;
+  fp2_sqr(tmp, z4);
+  fp2_sqr(tmp2, z5);
+  fp2_mul_xi(t4, tmp2);
+  fp2_add(t4, t4, tmp);
+  fp2_add(t5, z4, z5);
+  fp2_sqr(t5, t5);
+  fp2_sub(t5, t5, tmp);
+  fp2_sub(t5, t5, tmp2);
+  // z0 = 3 t0 - 2 z0 ; z1 = 3 t1 + 2 z1
+  fp2_sub(z0, t0, z0);
+  fp2_dbl(z0, z0);
+  fp2_add(z0, z0, t0);
+  fp2_add(z1, t1, z1);
+  fp2_dbl(z1, z1);
+  fp2_add(z1, z1, t1);
+  // z2 = 3 xi t5 + 2 z2 ; z3 = 3 t4 - 2 z3
+  fp2_mul_xi(tmp, t5);
+  fp2_add(z2, tmp, z2);
+  fp2_dbl(z2, z2);
+  fp2_add(z2, z2, tmp);
+  fp2_sub(z3, t4, z3);
+  fp2_dbl(z3, z3);
+  fp2_add(z3, z3, t4);
+  // z4 = 3 t2 - 2 z4 ; z5 = 3 t3 + 2 z5
+  fp2_sub(z4, t2, z4);
+  fp2_dbl(z4, z4);
+  fp2_add(z4, z4, t2);
+  fp2_add(z5, t3, z5);
+  fp2_dbl(z5, z5);
+  fp2_add(z5, z5, t3);
+  r.c0.c0 = z0;
+  r.c0.c1 = z4;
+  r.c0.c2 = z3;
+  r.c1.c0 = z2;
+  r.c1.c1 = z1;
+  r.c1.c2 = z5;
+}
+
+}  // namespace bls

@@ -1,0 +1,121 @@
+/*
+ * hipbls — MI355X (gfx950) BLS12-381 engine behind charon's tbls.Implementation.
+ *
+ * C-ABI only: plain pointers and sizes, no HIP or torch types.  All buffers are owned by the
+ * caller; the library never keeps a caller pointer after a call returns (cgo pointer rules).
+ * Every entry point is thread-safe (one internal lock per device context).  A HIP failure is
+ * reported as HIPBLS_ERR_DEVICE for the whole call and NEVER as a per-item "verified".
+ *
+ * Reference interface each entry point replaces (paths relative to the charon repository):
+ *   hipbls_verify_batch                tbls.Implementation.Verify            tbls/tbls.go:53-55, tbls/herumi.go:285-301
+ *   hipbls_threshold_aggregate_batch   tbls.Implementation.ThresholdAggregate tbls/tbls.go:50-51, tbls/herumi.go:244-283
+ *   hipbls_sign_batch                  tbls.Implementation.Sign              tbls/tbls.go:57-59, tbls/herumi.go:303-313
+ *   hipbls_secret_to_public_key_batch  tbls.Implementation.SecretToPublicKey tbls/tbls.go:36-38, tbls/herumi.go:67-80
+ *   hipbls_verify_aggregate            tbls.Implementation.VerifyAggregate   tbls/tbls.go:61-63, tbls/herumi.go:315-339
+ *   hipbls_aggregate                   tbls.Implementation.Aggregate         tbls/tbls.go:65-67, tbls/herumi.go:220-242
+ *   hipbls_threshold_split             tbls.Implementation.ThresholdSplit[Insecure] tbls/tbls.go:40-47, tbls/herumi.go:84-181
+ *   hipbls_recover_secret              tbls.Implementation.RecoverSecret     tbls/tbls.go:49, tbls/herumi.go:183-218
+ * Underneath, these replace herumi's cgo entry points blsVerify / blsSignatureRecover /
+ * blsSign / blsGetPublicKey / blsFastAggregateVerify / blsAggregateSignature
+ * (github.com/herumi/bls-eth-go-binary v1.32.1, imported at tbls/herumi.go:12).
+ *
+ * Wire formats (herumi ETH mode): secret key 32 bytes big-endian; public key 48-byte compressed G1;
+ * signature 96-byte compressed G2 (x = c1 || c0), ZCash flag bits.
+ */
+#ifndef HIPBLS_H
+#define HIPBLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Per-item and per-call status codes.  1..5 map onto the reference's error strings. */
+enum {
+  HIPBLS_OK = 0,
+  HIPBLS_ERR_PUBKEY = 1,    /* "cannot set compressed public key in Herumi format" */
+  HIPBLS_ERR_SIGNATURE = 2, /* "cannot unmarshal signature into Herumi signature" */
+  HIPBLS_ERR_VERIFY = 3,    /* "signature not verified" (Verify) / "signature verification failed" (VerifyAggregate) */
+  HIPBLS_ERR_SECRET = 4,    /* "cannot unmarshal secret into Herumi secret key" / "cannot obtain public key from secret" */
+  HIPBLS_ERR_COMBINE = 5,   /* "cannot combine signatures" (empty set, id 0, duplicate id) */
+  HIPBLS_ERR_ARG = 16,      /* bad arguments (null pointer, size overflow) */
+  HIPBLS_ERR_DEVICE = 17    /* HIP runtime failure; see hipbls_last_error() */
+};
+
+/* Library/ABI version (bumped on any signature change). */
+#define HIPBLS_ABI_VERSION 1
+int hipbls_abi_version(void);
+
+/* Select the HIP device used by the calling process (one process per GPU); idempotent.
+ * Returns HIPBLS_OK or HIPBLS_ERR_DEVICE. */
+int hipbls_init(int device);
+/* Number of visible HIP devices (0 when none). */
+int hipbls_device_count(void);
+/* Thread-local text of the last HIPBLS_ERR_DEVICE / HIPBLS_ERR_ARG. */
+const char* hipbls_last_error(void);
+
+/* ---------------------------------------------------------------- batched, host buffers ---- */
+
+/* Verify n items: item i is (pks[48 i..], msgs[msg_offsets[i] .. msg_offsets[i+1]), sigs[96 i..]).
+ * status[i] = HIPBLS_OK | HIPBLS_ERR_PUBKEY | HIPBLS_ERR_SIGNATURE | HIPBLS_ERR_VERIFY,
+ * exactly the outcome tbls.Herumi.Verify returns for that item. */
+int hipbls_verify_batch(const uint8_t* pks, const uint8_t* msgs, const uint64_t* msg_offsets,
+                        const uint8_t* sigs, uint64_t n, int32_t* status);
+
+/* ThresholdAggregate for n_groups sets: group g holds partials
+ * sigs[96 k ..], share_idx[k] for k in [group_offsets[g], group_offsets[g+1]).
+ * out_sigs[96 g ..] = sum_k lambda_k(0) * sig_k (Lagrange at 0 over the 1-based share indices).
+ * status[g] = HIPBLS_OK | HIPBLS_ERR_SIGNATURE | HIPBLS_ERR_COMBINE. */
+int hipbls_threshold_aggregate_batch(const uint8_t* sigs, const uint32_t* share_idx,
+                                     const uint64_t* group_offsets, uint64_t n_groups,
+                                     uint8_t* out_sigs, int32_t* status);
+
+/* Sign n messages: out_sigs[96 i ..] = sks[32 i ..] * H(msg_i).  status[i] = OK | ERR_SECRET. */
+int hipbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n,
+                      uint8_t* out_sigs, int32_t* status);
+
+/* out_pks[48 i ..] = sks[32 i ..] * g1.  status[i] = OK | ERR_SECRET (zero or >= r). */
+int hipbls_secret_to_public_key_batch(const uint8_t* sks, uint64_t n, uint8_t* out_pks, int32_t* status);
+
+/* FastAggregateVerify(pks[0..n), sig, msg).  *status = OK | ERR_PUBKEY | ERR_SIGNATURE | ERR_VERIFY. */
+int hipbls_verify_aggregate(const uint8_t* pks, uint64_t n, const uint8_t* sig, const uint8_t* msg,
+                            uint64_t msg_len, int32_t* status);
+
+/* Plain G2 sum of n signatures.  *status = OK | ERR_SIGNATURE | ERR_COMBINE (n == 0). */
+int hipbls_aggregate(const uint8_t* sigs, uint64_t n, uint8_t* out_sig, int32_t* status);
+
+/* Shamir split: share_i = secret + sum_j poly_tail[j] * i^(j+1) mod r, i = 1..total.
+ * poly_tail holds threshold-1 secrets of 32 bytes (the reference draws them from a CSPRNG or an
+ * insecure reader; the caller supplies them).  *status = OK | ERR_SECRET. */
+int hipbls_threshold_split(const uint8_t* secret, const uint8_t* poly_tail, uint32_t total, uint32_t threshold,
+                           uint8_t* out_shares, int32_t* status);
+
+/* Lagrange recovery of the secret at 0 from n (id, share) pairs.  *status = OK | ERR_SECRET | ERR_COMBINE. */
+int hipbls_recover_secret(const uint8_t* shares, const uint32_t* ids, uint32_t n, uint8_t* out_secret,
+                          int32_t* status);
+
+/* ------------------------------------------- device-resident variants (inputs already in HBM) ---- */
+/* Same semantics; every pointer is a device pointer; work is enqueued on `stream` (a hipStream_t,
+ * NULL = the library's stream) and the call returns without synchronizing. */
+int hipbls_verify_batch_device(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
+                               const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream);
+int hipbls_threshold_aggregate_batch_device(const uint8_t* d_sigs, const uint32_t* d_share_idx,
+                                            const uint64_t* d_group_offsets, uint64_t n_groups,
+                                            uint8_t* d_out_sigs, int32_t* d_status, void* stream);
+int hipbls_sign_batch_device(const uint8_t* d_sks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
+                             uint64_t n, uint8_t* d_out_sigs, int32_t* d_status, void* stream);
+int hipbls_secret_to_public_key_batch_device(const uint8_t* d_sks, uint64_t n, uint8_t* d_out_pks,
+                                             int32_t* d_status, void* stream);
+
+/* Average duration (ms) of the dominant verify kernel over the calls since the last reset,
+ * measured with HIP events on the stream it runs on (bench.py roofline). */
+int hipbls_kernel_timing(const char* name, double* avg_ms, uint64_t* launches);
+int hipbls_kernel_timing_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HIPBLS_H */

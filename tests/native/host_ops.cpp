@@ -1,0 +1,234 @@
+// Host (x86) build of the HIP engine's per-lane arithmetic (charon_amd/csrc/*.h), exported for
+// ctypes so tests/test_host_arith.py can diff every layer against oracle/bls12381.py without a GPU.
+// TEST INFRASTRUCTURE ONLY: the product library (charon_amd/libhipbls.so) never calls this code;
+// it is the same source compiled for the CPU so kernel bugs show up in the CPU test suite.
+#define BLS_COUNT_OPS 1
+#include "../../charon_amd/csrc/ops.h"
+
+namespace bls {
+thread_local uint64_t g_fp_mul_count = 0;
+thread_local uint64_t g_fp_sqr_count = 0;
+}  // namespace bls
+
+using namespace bls;
+
+static void fp_out(uint8_t* o, const fp& a) {
+  fp t;
+  fp_from_mont(t, a);
+  fp_plain_to_be48(o, t);
+}
+static void fp_in(fp& a, const uint8_t* b) {
+  fp_plain_from_be48(a, b);
+  fp_to_mont(a, a);
+}
+
+extern "C" {
+
+int ht_sign(const uint8_t* sk, const uint8_t* msg, uint32_t len, uint8_t* out) { return op_sign(out, sk, msg, len); }
+int ht_sk_to_pk(const uint8_t* sk, uint8_t* out) { return op_sk_to_pk(out, sk); }
+int ht_verify(const uint8_t* pk, const uint8_t* msg, uint32_t len, const uint8_t* sig) {
+  return op_verify(pk, msg, len, sig);
+}
+
+void ht_hash_to_g2(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dst_len, uint8_t* out_aff192) {
+  g2j h;
+  hash_to_g2(h, msg, len, dst, dst_len);
+  g2a a;
+  jac_to_aff(a, h);
+  fp_out(out_aff192, a.x.c0);
+  fp_out(out_aff192 + 48, a.x.c1);
+  fp_out(out_aff192 + 96, a.y.c0);
+  fp_out(out_aff192 + 144, a.y.c1);
+}
+
+void ht_expand_message(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dst_len, uint8_t* out256) {
+  uint32_t w[64];
+  expand_message_xmd_256(w, msg, len, dst, dst_len);
+  for (int i = 0; i < 64; ++i) {
+    out256[4 * i] = (uint8_t)(w[i] >> 24);
+    out256[4 * i + 1] = (uint8_t)(w[i] >> 16);
+    out256[4 * i + 2] = (uint8_t)(w[i] >> 8);
+    out256[4 * i + 3] = (uint8_t)w[i];
+  }
+}
+
+// u (plain c0||c1) -> SSWU point on E2' (plain x0,x1,y0,y1)
+void ht_map_to_curve(const uint8_t* u96, uint8_t* out192) {
+  fp2 u;
+  fp_in(u.c0, u96);
+  fp_in(u.c1, u96 + 48);
+  g2a p;
+  map_to_curve_sswu(p, u);
+  fp_out(out192, p.x.c0);
+  fp_out(out192 + 48, p.x.c1);
+  fp_out(out192 + 96, p.y.c0);
+  fp_out(out192 + 144, p.y.c1);
+}
+
+int ht_g1_decompress(const uint8_t* in, int check, uint8_t* out96) {
+  g1a a;
+  int st = g1_decompress(a, in, check != 0);
+  if (st == DEC_OK) {
+    fp_out(out96, a.x);
+    fp_out(out96 + 48, a.y);
+  }
+  return st;
+}
+int ht_g2_decompress(const uint8_t* in, int check, uint8_t* out192) {
+  g2a a;
+  int st = g2_decompress(a, in, check != 0);
+  if (st == DEC_OK) {
+    fp_out(out192, a.x.c0);
+    fp_out(out192 + 48, a.x.c1);
+    fp_out(out192 + 96, a.y.c0);
+    fp_out(out192 + 144, a.y.c1);
+  }
+  return st;
+}
+int ht_g1_in_subgroup(const uint8_t* xy96) {
+  g1j p;
+  fp_in(p.x, xy96);
+  fp_in(p.y, xy96 + 48);
+  fp_set_one(p.z);
+  return g1_in_subgroup(p) ? 1 : 0;
+}
+int ht_g2_in_subgroup(const uint8_t* xy192) {
+  g2j p;
+  fp_in(p.x.c0, xy192);
+  fp_in(p.x.c1, xy192 + 48);
+  fp_in(p.y.c0, xy192 + 96);
+  fp_in(p.y.c1, xy192 + 144);
+  fp2_set_one(p.z);
+  return g2_in_subgroup(p) ? 1 : 0;
+}
+void ht_g2_clear_cofactor(const uint8_t* xy192, uint8_t* out192) {
+  g2j p, q;
+  fp_in(p.x.c0, xy192);
+  fp_in(p.x.c1, xy192 + 48);
+  fp_in(p.y.c0, xy192 + 96);
+  fp_in(p.y.c1, xy192 + 144);
+  fp2_set_one(p.z);
+  g2_clear_cofactor(q, p);
+  g2a a;
+  jac_to_aff(a, q);
+  fp_out(out192, a.x.c0);
+  fp_out(out192 + 48, a.x.c1);
+  fp_out(out192 + 96, a.y.c0);
+  fp_out(out192 + 144, a.y.c1);
+}
+
+// e(P, Q) for affine plain inputs; out = 12 plain Fp coefficients in tower order
+// (c0.c0.c0, c0.c0.c1, c0.c1.c0, ..., c1.c2.c1), each 48 bytes.  Computes f^(3 (p^12-1)/r).
+void ht_pairing(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
+  g1a P[1];
+  g2a Q[1];
+  bool skip[1] = {false};
+  fp_in(P[0].x, p96);
+  fp_in(P[0].y, p96 + 48);
+  fp_in(Q[0].x.c0, q192);
+  fp_in(Q[0].x.c1, q192 + 48);
+  fp_in(Q[0].y.c0, q192 + 96);
+  fp_in(Q[0].y.c1, q192 + 144);
+  fp12 f, e;
+  miller_loop_n(f, P, Q, skip, 1);
+  final_exponentiation(e, f);
+  const fp* c = &e.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) fp_out(out576 + 48 * i, c[i]);
+}
+
+// Miller loop only (no final exponentiation), same output layout
+void ht_miller(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
+  g1a P[1];
+  g2a Q[1];
+  bool skip[1] = {false};
+  fp_in(P[0].x, p96);
+  fp_in(P[0].y, p96 + 48);
+  fp_in(Q[0].x.c0, q192);
+  fp_in(Q[0].x.c1, q192 + 48);
+  fp_in(Q[0].y.c0, q192 + 96);
+  fp_in(Q[0].y.c1, q192 + 144);
+  fp12 f;
+  miller_loop_n(f, P, Q, skip, 1);
+  const fp* c = &f.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) fp_out(out576 + 48 * i, c[i]);
+}
+
+// Fp12 product / final exponentiation on raw coefficient arrays (plain, tower order)
+void ht_final_exp(const uint8_t* in576, uint8_t* out576) {
+  fp12 f, e;
+  fp* c = &f.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) fp_in(c[i], in576 + 48 * i);
+  final_exponentiation(e, f);
+  const fp* d = &e.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) fp_out(out576 + 48 * i, d[i]);
+}
+
+void ht_fp12_op(int op, const uint8_t* a576, const uint8_t* b576, uint8_t* out576) {
+  fp12 a, b, r;
+  fp* ca = &a.c0.c0.c0;
+  fp* cb = &b.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) {
+    fp_in(ca[i], a576 + 48 * i);
+    fp_in(cb[i], b576 + 48 * i);
+  }
+  switch (op) {
+    case 0: fp12_mul(r, a, b); break;
+    case 1: fp12_sqr(r, a); break;
+    case 2: fp12_inv(r, a); break;
+    case 3: fp12_frobenius(r, a, 1); break;
+    case 4: fp12_frobenius(r, a, 2); break;
+    case 5: fp12_frobenius(r, a, 3); break;
+    case 6: fp12_cyclotomic_sqr(r, a); break;
+    case 7: fp12_mul_line(a, b.c0.c0, b.c0.c1, b.c1.c1); r = a; break;
+    default: r = a;
+  }
+  const fp* d = &r.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) fp_out(out576 + 48 * i, d[i]);
+}
+
+int ht_threshold_aggregate(const uint8_t* sigs, const uint32_t* ids, int n, uint8_t* out96) {
+  g2j acc;
+  jac_set_inf(acc);
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < n; ++j)
+      if (j != i && ids[j] == ids[i]) return HIPBLS_ERR_COMBINE;
+    if (ids[i] == 0) return HIPBLS_ERR_COMBINE;
+  }
+  for (int i = 0; i < n; ++i) {
+    g2a s;
+    int st = g2_decompress(s, sigs + 96 * i, true);
+    if (st == DEC_BAD) return HIPBLS_ERR_SIGNATURE;
+    g2j sj;
+    if (st == DEC_INF)
+      jac_set_inf(sj);
+    else
+      jac_from_aff(sj, s);
+    fr lam;
+    lagrange_at_zero(lam, ids, n, i);
+    g2j t;
+    jac_mul_limbs(t, sj, lam.v, 8);
+    jac_add(acc, acc, t);
+  }
+  g2_compress(out96, acc);
+  return HIPBLS_OK;
+}
+
+// Fp-multiplication counts of one op_verify call (mul, sqr)
+void ht_count_verify(const uint8_t* pk, const uint8_t* msg, uint32_t len, const uint8_t* sig, uint64_t* out2) {
+  g_fp_mul_count = 0;
+  g_fp_sqr_count = 0;
+  op_verify(pk, msg, len, sig);
+  out2[0] = g_fp_mul_count;
+  out2[1] = g_fp_sqr_count;
+}
+
+void ht_reset_counts(void) {
+  g_fp_mul_count = 0;
+  g_fp_sqr_count = 0;
+}
+void ht_get_counts(uint64_t* out2) {
+  out2[0] = g_fp_mul_count;
+  out2[1] = g_fp_sqr_count;
+}
+
+}  // extern "C"

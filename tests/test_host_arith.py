@@ -1,0 +1,206 @@
+"""Layer-by-layer parity of the kernel arithmetic (host build, tests/native) against the oracle.
+
+The kernels' per-lane code in charon_amd/csrc is compiled for x86 here, so every field/tower/curve/
+hash/pairing layer is diffed against oracle/bls12381.py on the CPU.  The GPU tests then only have to
+show the device build computes the same thing (tests/test_gpu_parity.py).
+"""
+import random
+
+import pytest
+
+from oracle import bls12381 as bls
+from tests.hostlib import buf, lib
+
+P = bls.P
+
+
+def be48(v):
+    return v.to_bytes(48, "big")
+
+
+def fp_from(b):
+    return int.from_bytes(b, "big")
+
+
+def g1_bytes(pt):
+    return be48(pt[0]) + be48(pt[1])
+
+
+def g2_bytes(pt):
+    (x0, x1), (y0, y1) = pt
+    return be48(x0) + be48(x1) + be48(y0) + be48(y1)
+
+
+def g2_from(b):
+    v = [fp_from(b[48 * i:48 * i + 48]) for i in range(4)]
+    return ((v[0], v[1]), (v[2], v[3]))
+
+
+def f12_from(b):
+    c = [fp_from(b[48 * i:48 * i + 48]) for i in range(12)]
+    f2 = [(c[2 * i], c[2 * i + 1]) for i in range(6)]
+    return ((f2[0], f2[1], f2[2]), (f2[3], f2[4], f2[5]))
+
+
+def f12_bytes(f):
+    out = b""
+    for f6 in f:
+        for f2 in f6:
+            out += be48(f2[0]) + be48(f2[1])
+    return out
+
+
+def rand_f12(rng):
+    return tuple(tuple((rng.randrange(P), rng.randrange(P)) for _ in range(3)) for _ in range(2))
+
+
+@pytest.fixture(scope="module")
+def L():
+    return lib()
+
+
+def test_expand_message(L):
+    out = buf(256)
+    dst = b"QUUX-V01-CS02-with-expander-SHA256-128"
+    for msg in [b"", b"abc", b"a" * 200]:
+        L.ht_expand_message(msg, len(msg), dst, len(dst), out)
+        assert out.raw == bls.expand_message_xmd(msg, dst, 256)
+
+
+def test_map_to_curve(L):
+    rng = random.Random(7)
+    out = buf(192)
+    for _ in range(6):
+        u = (rng.randrange(P), rng.randrange(P))
+        L.ht_map_to_curve(be48(u[0]) + be48(u[1]), out)
+        assert g2_from(out.raw) == bls.map_to_curve_sswu(u)
+
+
+def test_hash_to_g2(L):
+    out = buf(192)
+    for msg, dst in [(b"", b"QUUX-V01-CS02-with-BLS12381G2_XMD:SHA-256_SSWU_RO_"),
+                     (b"abc", b"QUUX-V01-CS02-with-BLS12381G2_XMD:SHA-256_SSWU_RO_"),
+                     (b"hello obol!", bls.DST_POP), (bytes(range(32)), bls.DST_POP)]:
+        L.ht_hash_to_g2(msg, len(msg), dst, len(dst), out)
+        assert g2_from(out.raw) == bls.hash_to_g2(msg, dst)
+
+
+def test_clear_cofactor_matches_h_eff(L):
+    rng = random.Random(3)
+    out = buf(192)
+    for _ in range(3):
+        pt = bls.iso_map_g2(bls.map_to_curve_sswu((rng.randrange(P), rng.randrange(P))))
+        L.ht_g2_clear_cofactor(g2_bytes(pt), out)
+        assert g2_from(out.raw) == bls.g2_mul(pt, bls.H_EFF_G2)
+
+
+def _random_g1_point(rng):
+    while True:
+        x = rng.randrange(P)
+        y = bls.fp_sqrt((x ** 3 + 4) % P)
+        if y is not None:
+            return (x, y)
+
+
+def _random_g2_point(rng):
+    while True:
+        x = (rng.randrange(P), rng.randrange(P))
+        y = bls.f2_sqrt(bls.f2_add(bls.f2_mul(bls.f2_sqr(x), x), bls.B2))
+        if y is not None:
+            return (x, y)
+
+
+def test_g1_subgroup_check_vs_order(L):
+    rng = random.Random(11)
+    for _ in range(4):
+        pt = _random_g1_point(rng)  # almost surely not in G1
+        assert L.ht_g1_in_subgroup(g1_bytes(pt)) == int(bls.g1_mul(pt, bls.R) is None)
+        pt_in = bls.g1_mul(pt, 0x396C8C005555E1568C00AAAB0000AAAB)  # cofactor h1 -> lands in G1
+        assert L.ht_g1_in_subgroup(g1_bytes(pt_in)) == 1
+
+
+def test_g2_subgroup_check_vs_order(L):
+    rng = random.Random(12)
+    for _ in range(3):
+        pt = _random_g2_point(rng)
+        assert L.ht_g2_in_subgroup(g2_bytes(pt)) == int(bls.g2_mul(pt, bls.R) is None) == 0
+        pt_in = bls.g2_mul(pt, bls.H_EFF_G2)
+        assert L.ht_g2_in_subgroup(g2_bytes(pt_in)) == 1
+
+
+def test_decompress_roundtrip(L):
+    rng = random.Random(5)
+    out1, out2 = buf(96), buf(192)
+    for _ in range(3):
+        k = rng.randrange(1, bls.R)
+        p1 = bls.g1_mul(bls.G1_GEN, k)
+        assert L.ht_g1_decompress(bls.g1_compress(p1), 1, out1) == 0
+        assert out1.raw == g1_bytes(p1)
+        p2 = bls.g2_mul(bls.G2_GEN, k)
+        assert L.ht_g2_decompress(bls.g2_compress(p2), 1, out2) == 0
+        assert g2_from(out2.raw) == p2
+
+
+def test_fp12_ops(L):
+    rng = random.Random(9)
+    out = buf(576)
+    a, b = rand_f12(rng), rand_f12(rng)
+    L.ht_fp12_op(0, f12_bytes(a), f12_bytes(b), out)
+    assert f12_from(out.raw) == bls.f12_mul(a, b)
+    L.ht_fp12_op(1, f12_bytes(a), f12_bytes(b), out)
+    assert f12_from(out.raw) == bls.f12_mul(a, a)
+    L.ht_fp12_op(2, f12_bytes(a), f12_bytes(b), out)
+    assert f12_from(out.raw) == bls.f12_inv(a)
+    for op, j in ((3, 1), (4, 2), (5, 3)):
+        L.ht_fp12_op(op, f12_bytes(a), f12_bytes(b), out)
+        assert f12_from(out.raw) == bls.f12_pow(a, P ** j)
+    # cyclotomic squaring on an element of the cyclotomic subgroup: a^((p^6-1)(p^2+1))
+    c = bls.f12_mul(bls.f12_conj(a), bls.f12_inv(a))
+    c = bls.f12_mul(bls.f12_pow(c, P * P), c)
+    L.ht_fp12_op(6, f12_bytes(c), f12_bytes(b), out)
+    assert f12_from(out.raw) == bls.f12_mul(c, c)
+    # sparse line multiplication vs dense
+    z = (0, 0)
+    line = ((b[0][0], b[0][1], z), (z, b[1][1], z))
+    L.ht_fp12_op(7, f12_bytes(a), f12_bytes(line), out)
+    assert f12_from(out.raw) == bls.f12_mul(a, line)
+
+
+def test_pairing_matches_oracle_cubed(L):
+    out = buf(576)
+    k1, k2 = 0x1234567, 0x89ABCDEF
+    P1 = bls.g1_mul(bls.G1_GEN, k1)
+    Q1 = bls.g2_mul(bls.G2_GEN, k2)
+    L.ht_pairing(g1_bytes(P1), g2_bytes(Q1), out)
+    e = bls.pairing(P1, Q1)
+    assert f12_from(out.raw) == bls.f12_mul(bls.f12_mul(e, e), e)
+
+
+def test_sign_and_verify_kats(L, kat):
+    k = kat["prysm"]
+    out = buf(96)
+    assert L.ht_sign(bytes.fromhex(k["sk"]), bytes.fromhex(k["signing_root"]), 32, out) == 0
+    assert out.raw.hex() == k["sig"]
+    pk = buf(48)
+    assert L.ht_sk_to_pk(bytes.fromhex(k["sk"]), pk) == 0
+    assert pk.raw == bls.secret_to_public_key(bytes.fromhex(k["sk"]))
+    root = bytes.fromhex(k["signing_root"])
+    assert L.ht_verify(pk.raw, root, 32, out.raw) == 0
+    assert L.ht_verify(pk.raw, root[:-1] + b"\x00", 32, out.raw) == 3
+    bad = bytearray(out.raw)
+    bad[5] ^= 1
+    assert L.ht_verify(pk.raw, root, 32, bytes(bad)) in (2, 3)
+    assert L.ht_verify(bytes(48), root, 32, out.raw) == 1
+
+
+def test_threshold_aggregate_host(L):
+    msg = b"hello obol!"
+    secret = 0xABCDEF0123456789
+    shares = bls.threshold_split_poly(secret, [11, 22, 33], 7)
+    ids = [2, 3, 5, 7]
+    sigs = b"".join(bls.sign(shares[i], msg) for i in ids)
+    import ctypes
+    arr = (ctypes.c_uint32 * 4)(*ids)
+    out = buf(96)
+    assert L.ht_threshold_aggregate(sigs, arr, 4, out) == 0
+    assert out.raw == bls.sign(bls.sk_serialize(secret), msg)
