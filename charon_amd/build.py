@@ -1,0 +1,39 @@
+"""Build the HIP engine for gfx950 in-tree: charon_amd/libhipbls.so (C-ABI, include/hipbls.h)."""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libhipbls.so")
+ARCH = os.environ.get("HIPBLS_ARCH", "gfx950")
+
+
+def _sources():
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hip"))]
+    return hdrs + [os.path.join(ROOT, "include", "hipbls.h")]
+
+
+def stale(lib=LIB):
+    if not os.path.exists(lib):
+        return True
+    t = os.path.getmtime(lib)
+    return any(os.path.getmtime(s) > t for s in _sources())
+
+
+def build(force=False, verbose=True, extra=()):
+    if not force and not stale():
+        return LIB
+    cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I" + CSRC, "-I" + os.path.join(ROOT, "include"),
+           "-o", LIB + ".tmp", os.path.join(CSRC, "hipbls.hip")] + list(extra)
+    if verbose:
+        print("[hipbls] " + " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

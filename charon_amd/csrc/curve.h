@@ -70,7 +70,7 @@ BLS_HD BLS_INLINE void jac_neg(jac<F>& r, const jac<F>& a) {
 
 // dbl-2009-l (a = 0)
 template <class F>
-BLS_HD BLS_INLINE void jac_dbl(jac<F>& r, const jac<F>& p) {
+BLS_HD BLS_CALL void jac_dbl(jac<F>& r, const jac<F>& p) {
   F A, B, C, D, E, Fv, t;
   f_sqr(A, p.x);
   f_sqr(B, p.y);
@@ -100,7 +100,7 @@ BLS_HD BLS_INLINE void jac_dbl(jac<F>& r, const jac<F>& p) {
 
 // add-2007-bl with the exceptional cases handled (P = Q doubles, P = -Q gives infinity)
 template <class F>
-BLS_HD BLS_INLINE void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
+BLS_HD BLS_CALL void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
   if (jac_is_inf(p)) {
     r = q;
     return;
@@ -155,7 +155,7 @@ BLS_HD BLS_INLINE void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
 
 // mixed addition r = p + q with q affine (madd-2007-bl), exceptional cases handled
 template <class F>
-BLS_HD BLS_INLINE void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) {
+BLS_HD BLS_CALL void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) {
   if (jac_is_inf(p)) {
     jac_from_aff(r, q);
     return;
@@ -202,7 +202,7 @@ BLS_HD BLS_INLINE void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) 
 
 // r = [k] p for a 64-bit scalar k (uniform across lanes when k is a constant)
 template <class F>
-BLS_HD BLS_INLINE void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
+BLS_HD BLS_CALL void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
   jac<F> acc;
   jac_set_inf(acc);
   for (int i = 63; i >= 0; --i) {
@@ -214,7 +214,7 @@ BLS_HD BLS_INLINE void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
 
 // r = [k] p for a scalar given as nlimbs little-endian 32-bit limbs
 template <class F>
-BLS_HD BLS_INLINE void jac_mul_limbs(jac<F>& r, const jac<F>& p, const uint32_t* k, int nlimbs) {
+BLS_HD BLS_CALL void jac_mul_limbs(jac<F>& r, const jac<F>& p, const uint32_t* k, int nlimbs) {
   jac<F> acc;
   jac_set_inf(acc);
   for (int i = nlimbs * 32 - 1; i >= 0; --i) {
@@ -226,7 +226,7 @@ BLS_HD BLS_INLINE void jac_mul_limbs(jac<F>& r, const jac<F>& p, const uint32_t*
 
 // Jacobian equality without normalization
 template <class F>
-BLS_HD BLS_INLINE bool jac_eq(const jac<F>& p, const jac<F>& q) {
+BLS_HD BLS_CALL bool jac_eq(const jac<F>& p, const jac<F>& q) {
   const bool pi = jac_is_inf(p), qi = jac_is_inf(q);
   if (pi || qi) return pi && qi;
   F z1z1, z2z2, a, b;
@@ -243,7 +243,7 @@ BLS_HD BLS_INLINE bool jac_eq(const jac<F>& p, const jac<F>& q) {
 }
 
 template <class F>
-BLS_HD BLS_INLINE void jac_to_aff(aff<F>& r, const jac<F>& p) {
+BLS_HD BLS_CALL void jac_to_aff(aff<F>& r, const jac<F>& p) {
   F zi, zi2;
   f_inv(zi, p.z);
   f_sqr(zi2, zi);
@@ -312,7 +312,7 @@ BLS_HD BLS_INLINE bool fp2_is_lex_largest(const fp2& y) {
 
 // 48-byte compressed G1 -> affine; returns DEC_OK / DEC_BAD / DEC_INF.  Subgroup test included.
 
-BLS_HD BLS_INLINE bool g1_in_subgroup(const g1j& p) {
+BLS_HD BLS_CALL bool g1_in_subgroup(const g1j& p) {
   if (jac_is_inf(p)) return true;
   g1j q;
   jac_mul_u64(q, p, X_ABS);
@@ -323,7 +323,7 @@ BLS_HD BLS_INLINE bool g1_in_subgroup(const g1j& p) {
   phi.z = p.z;
   return jac_eq(q, phi);
 }
-BLS_HD BLS_INLINE bool g2_in_subgroup(const g2j& p) {
+BLS_HD BLS_CALL bool g2_in_subgroup(const g2j& p) {
   if (jac_is_inf(p)) return true;
   g2j q, ps;
   jac_mul_u64(q, p, X_ABS);
@@ -331,7 +331,7 @@ BLS_HD BLS_INLINE bool g2_in_subgroup(const g2j& p) {
   g2_psi(ps, p);
   return jac_eq(q, ps);
 }
-BLS_HD BLS_INLINE void g2_clear_cofactor(g2j& r, const g2j& p) {
+BLS_HD BLS_CALL void g2_clear_cofactor(g2j& r, const g2j& p) {
   g2j t1, t2, t3, np;
   jac_mul_u64(t1, p, X_ABS);
   jac_neg(t1, t1);  // t1 = [x] P
@@ -352,7 +352,7 @@ BLS_HD BLS_INLINE void g2_clear_cofactor(g2j& r, const g2j& p) {
   jac_add(r, t3, np);
 }
 
-BLS_HD BLS_INLINE bool fp2_sqrt(fp2& r, const fp2& a) {
+BLS_HD BLS_CALL bool fp2_sqrt(fp2& r, const fp2& a) {
   fp n, s, t, x0, inv2x0, t2;
   fp_sqr(n, a.c0);
   fp_sqr(t, a.c1);
@@ -383,7 +383,7 @@ BLS_HD BLS_INLINE bool fp2_sqrt(fp2& r, const fp2& a) {
   return fp2_eq(chk, a);
 }
 
-BLS_HD BLS_INLINE int g1_decompress(g1a& out, const uint8_t* b, bool subgroup_check) {
+BLS_HD BLS_CALL int g1_decompress(g1a& out, const uint8_t* b, bool subgroup_check) {
   const uint8_t flags = b[0];
   if (!(flags & 0x80)) return DEC_BAD;
   uint8_t buf[48];
@@ -414,7 +414,7 @@ BLS_HD BLS_INLINE int g1_decompress(g1a& out, const uint8_t* b, bool subgroup_ch
   return DEC_OK;
 }
 
-BLS_HD BLS_INLINE int g2_decompress(g2a& out, const uint8_t* b, bool subgroup_check) {
+BLS_HD BLS_CALL int g2_decompress(g2a& out, const uint8_t* b, bool subgroup_check) {
   const uint8_t flags = b[0];
   if (!(flags & 0x80)) return DEC_BAD;
   uint8_t buf[96];
@@ -447,7 +447,7 @@ BLS_HD BLS_INLINE int g2_decompress(g2a& out, const uint8_t* b, bool subgroup_ch
   return DEC_OK;
 }
 
-BLS_HD BLS_INLINE void g1_compress(uint8_t* b, const g1j& p) {
+BLS_HD BLS_CALL void g1_compress(uint8_t* b, const g1j& p) {
   if (jac_is_inf(p)) {
     b[0] = 0xc0;
     for (int i = 1; i < 48; ++i) b[i] = 0;
@@ -462,7 +462,7 @@ BLS_HD BLS_INLINE void g1_compress(uint8_t* b, const g1j& p) {
   if (fp_is_lex_largest(a.y)) b[0] |= 0x20;
 }
 
-BLS_HD BLS_INLINE void g2_compress(uint8_t* b, const g2j& p) {
+BLS_HD BLS_CALL void g2_compress(uint8_t* b, const g2j& p) {
   if (jac_is_inf(p)) {
     b[0] = 0xc0;
     for (int i = 1; i < 96; ++i) b[i] = 0;

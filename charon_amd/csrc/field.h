@@ -18,6 +18,10 @@
 #define BLS_INLINE static inline
 #endif
 #define BLS_NOINLINE static __attribute__((noinline))
+// Mid-level building blocks (Fp6/Fp12 products, curve steps, hash stages) are real calls: their
+// bodies are emitted once, so a kernel's instruction footprint stays within the instruction cache
+// and compile time stays linear.  Fp and Fp2 arithmetic is inlined into them.
+#define BLS_CALL static __attribute__((noinline))
 
 namespace bls {
 
@@ -177,7 +181,7 @@ BLS_HD BLS_INLINE void fp_sqr(fp& r, const fp& a) { r = fp_sqr_v(a); }
 
 // r = a^e for a fixed exponent given as little-endian 32-bit limbs whose top set bit is top_bit
 // (left-to-right binary; the exponent is the same for every lane, so the branch is uniform).
-BLS_HD BLS_INLINE void fp_pow(fp& r, const fp& a, const uint32_t* e, int top_bit) {
+BLS_HD BLS_CALL void fp_pow(fp& r, const fp& a, const uint32_t* e, int top_bit) {
   fp acc = a;
   for (int i = top_bit - 1; i >= 0; --i) {
     fp_sqr(acc, acc);

@@ -53,7 +53,7 @@ BLS_HD BLS_INLINE void fr_sub(fr& r, const fr& a, const fr& b) {
 
 // CIOS Montgomery product (r's top limb 0x73eda753 < 2^31 - 1: no-carry variant applies)
 
-BLS_HD BLS_INLINE void fr_mul(fr& r, const fr& a, const fr& b) {
+BLS_HD BLS_CALL void fr_mul(fr& r, const fr& a, const fr& b) {
   uint32_t t[8];
   for (int i = 0; i < 8; ++i) t[i] = 0;
 #pragma unroll
@@ -119,7 +119,7 @@ BLS_HD BLS_INLINE bool fr_plain_from_be32(fr& r, const uint8_t* b) {
   return br < 0;
 }
 
-BLS_HD BLS_INLINE void fr_inv(fr& r, const fr& a) {
+BLS_HD BLS_CALL void fr_inv(fr& r, const fr& a) {
   fr acc = a;
   for (int i = 253; i >= 0; --i) {  // r - 2 has its top bit at 254
     fr_mul(acc, acc, acc);

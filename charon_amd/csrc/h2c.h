@@ -66,7 +66,7 @@ BLS_HD BLS_INLINE int fp2_sgn0(const fp2& a) {
 // 3-isogeny E2' -> E2, returning Jacobian coordinates (no inversion)
 // full hash_to_curve; result in Jacobian coordinates on E2 (in G2)
 
-BLS_HD BLS_INLINE void sha256_compress(sha256_state& s, const uint32_t w_in[16]) {
+BLS_HD BLS_CALL void sha256_compress(sha256_state& s, const uint32_t w_in[16]) {
   constexpr uint32_t K[64] = {
       0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
       0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
@@ -117,7 +117,7 @@ BLS_HD BLS_INLINE void sha256_compress(sha256_state& s, const uint32_t w_in[16])
   s.h[7] += h;
 }
 
-BLS_HD BLS_INLINE void sha256_segs(uint32_t out[8], const byte_segs& m) {
+BLS_HD BLS_CALL void sha256_segs(uint32_t out[8], const byte_segs& m) {
   const uint32_t len = m.n[0] + m.n[1] + m.n[2] + m.n[3];
   const uint32_t nblocks = (len + 9 + 63) / 64;
   sha256_state s;
@@ -148,7 +148,7 @@ BLS_HD BLS_INLINE void sha256_segs(uint32_t out[8], const byte_segs& m) {
   for (int i = 0; i < 8; ++i) out[i] = s.h[i];
 }
 
-BLS_HD BLS_INLINE void expand_message_xmd_256(uint32_t out[64], const uint8_t* msg, uint32_t msg_len,
+BLS_HD BLS_CALL void expand_message_xmd_256(uint32_t out[64], const uint8_t* msg, uint32_t msg_len,
                                                 const uint8_t* dst, uint32_t dst_len) {
   // msg_prime = Z_pad(64) || msg || I2OSP(256, 2) || I2OSP(0, 1) || DST || I2OSP(len(DST), 1)
   uint8_t mid[3] = {0x01, 0x00, 0x00};  // l_i_b_str = 0x0100, then 0x00
@@ -204,7 +204,7 @@ BLS_HD BLS_INLINE void expand_message_xmd_256(uint32_t out[64], const uint8_t* m
   }
 }
 
-BLS_HD BLS_INLINE void fp_from_be64_words(fp& r, const uint32_t* w) {
+BLS_HD BLS_CALL void fp_from_be64_words(fp& r, const uint32_t* w) {
   // X = X_hi * 2^256 + X_lo with X_hi, X_lo < 2^256 < p;  mont(X) = mont_mul(X_lo, R^2) + mont_mul(X_hi, 2^256 R^2)
   fp hi, lo, c;
   for (int i = 0; i < 12; ++i) {
@@ -222,7 +222,7 @@ BLS_HD BLS_INLINE void fp_from_be64_words(fp& r, const uint32_t* w) {
   fp_add(r, lo, hi);
 }
 
-BLS_HD BLS_INLINE void map_to_curve_sswu(g2a& out, const fp2& u) {
+BLS_HD BLS_CALL void map_to_curve_sswu(g2a& out, const fp2& u) {
   fp2 u2, zu2, den, tv1, x1, gx1, t, y, x;
   fp2_sqr(u2, u);
   fp2_mul(zu2, SSWU_Z, u2);
@@ -260,7 +260,7 @@ BLS_HD BLS_INLINE void map_to_curve_sswu(g2a& out, const fp2& u) {
   out.y = y;
 }
 
-BLS_HD BLS_INLINE void iso_map_g2(g2j& out, const g2a& p) {
+BLS_HD BLS_CALL void iso_map_g2(g2j& out, const g2a& p) {
   // x = xn/xd, y = y * yn/yd  ->  Jacobian (xn xd yd^2, y yn xd^3 yd^2, xd yd)
   const fp2& x = p.x;
   fp2 xn, xd, yn, yd, t;
@@ -293,7 +293,7 @@ BLS_HD BLS_INLINE void iso_map_g2(g2j& out, const g2a& p) {
   out.z = z;
 }
 
-BLS_HD BLS_INLINE void hash_to_g2(g2j& out, const uint8_t* msg, uint32_t msg_len, const uint8_t* dst,
+BLS_HD BLS_CALL void hash_to_g2(g2j& out, const uint8_t* msg, uint32_t msg_len, const uint8_t* dst,
                                     uint32_t dst_len) {
   uint32_t uni[64];
   expand_message_xmd_256(uni, msg, msg_len, dst, dst_len);

@@ -13,7 +13,7 @@
 namespace bls {
 
 // Verify with pk and sig already decoded (affine, subgroup-checked) and H(m) already hashed.
-BLS_HD BLS_INLINE bool pairing_check_verify(const g1a& pk, const g2a& hm, const g2a& sig) {
+BLS_HD BLS_CALL bool pairing_check_verify(const g1a& pk, const g2a& hm, const g2a& sig) {
   // e(pk, H(m)) * e(-g1, sig) == 1
   g1a P[2];
   g2a Q[2];
@@ -36,7 +36,7 @@ BLS_HD BLS_INLINE bool pairing_check_verify(const g1a& pk, const g2a& hm, const 
 // pk = sk * g1; zero secret is an error (GetSafePublicKey, herumi.go:74)
 
 // Lagrange coefficient at 0 for the i-th id of a set (ids small positive integers, distinct)
-BLS_HD BLS_INLINE void lagrange_at_zero(fr& out_plain, const uint32_t* ids, int n, int i) {
+BLS_HD BLS_CALL void lagrange_at_zero(fr& out_plain, const uint32_t* ids, int n, int i) {
   fr num, den, t, xi, xj;
   fr_from_u32(num, 1);
   fr_from_u32(den, 1);
@@ -53,7 +53,7 @@ BLS_HD BLS_INLINE void lagrange_at_zero(fr& out_plain, const uint32_t* ids, int 
   fr_to_plain(out_plain, t);
 }
 
-BLS_HD BLS_INLINE int op_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96) {
+BLS_HD BLS_CALL int op_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96) {
   g1a pk;
   const int dp = g1_decompress(pk, pk48, true);
   if (dp == DEC_BAD) return HIPBLS_ERR_PUBKEY;
@@ -68,7 +68,7 @@ BLS_HD BLS_INLINE int op_verify(const uint8_t* pk48, const uint8_t* msg, uint32_
   return pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }
 
-BLS_HD BLS_INLINE int op_sign(uint8_t* out96, const uint8_t* sk32, const uint8_t* msg, uint32_t msg_len) {
+BLS_HD BLS_CALL int op_sign(uint8_t* out96, const uint8_t* sk32, const uint8_t* msg, uint32_t msg_len) {
   fr sk;
   if (!fr_plain_from_be32(sk, sk32)) return HIPBLS_ERR_SECRET;
   g2j h, s;
@@ -78,7 +78,7 @@ BLS_HD BLS_INLINE int op_sign(uint8_t* out96, const uint8_t* sk32, const uint8_t
   return HIPBLS_OK;
 }
 
-BLS_HD BLS_INLINE int op_sk_to_pk(uint8_t* out48, const uint8_t* sk32) {
+BLS_HD BLS_CALL int op_sk_to_pk(uint8_t* out48, const uint8_t* sk32) {
   fr sk;
   if (!fr_plain_from_be32(sk, sk32)) return HIPBLS_ERR_SECRET;
   if (fr_is_zero(sk)) return HIPBLS_ERR_SECRET;

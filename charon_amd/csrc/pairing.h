@@ -23,7 +23,7 @@ struct g1_pair_in {  // P in affine coordinates, or is_inf
 
 // r = f^((p^12-1)/r * 3)
 
-BLS_HD BLS_INLINE void miller_dbl_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const fp& xp, const fp& yp) {
+BLS_HD BLS_CALL void miller_dbl_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const fp& xp, const fp& yp) {
   // Homogeneous coordinates (x = X/Z, y = Y/Z).  Note: T.z here is the projective Z, not Jacobian.
   fp2 A, B, C, E, F, G, H, J, t;
   fp2_mul(A, T.x, T.y);
@@ -62,7 +62,7 @@ BLS_HD BLS_INLINE void miller_dbl_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const 
   T.z = Z3;
 }
 
-BLS_HD BLS_INLINE void miller_add_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const g2a& Q, const fp& xp,
+BLS_HD BLS_CALL void miller_add_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const g2a& Q, const fp& xp,
                                          const fp& yp) {
   fp2 theta, lambda, C, D, E, F, G, H, t;
   fp2_mul(t, Q.y, T.z);
@@ -98,7 +98,7 @@ BLS_HD BLS_INLINE void miller_add_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const 
   T.z = Z3;
 }
 
-BLS_HD BLS_INLINE void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bool* skip, int n) {
+BLS_HD BLS_CALL void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bool* skip, int n) {
   constexpr int MAXN = 2;
   g2j T[MAXN];
   for (int i = 0; i < n; ++i) {
@@ -127,7 +127,7 @@ BLS_HD BLS_INLINE void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const 
 }
 
 // r = a^|x| for a in the cyclotomic subgroup
-BLS_HD BLS_INLINE void fp12_cyc_exp_xabs(fp12& r, const fp12& a) {
+BLS_HD BLS_CALL void fp12_cyc_exp_xabs(fp12& r, const fp12& a) {
   fp12 acc = a;
   for (int bit = 62; bit >= 0; --bit) {
     fp12_cyclotomic_sqr(acc, acc);
@@ -136,7 +136,7 @@ BLS_HD BLS_INLINE void fp12_cyc_exp_xabs(fp12& r, const fp12& a) {
   r = acc;
 }
 
-BLS_HD BLS_INLINE void final_exponentiation(fp12& r, const fp12& f) {
+BLS_HD BLS_CALL void final_exponentiation(fp12& r, const fp12& f) {
   // easy part: f^((p^6-1)(p^2+1))
   fp12 t, fi, m;
   fp12_conj(t, f);

@@ -138,7 +138,7 @@ BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
   fp_mul(r.c0, s, d);
   fp_add(r.c1, m, m);
 }
-BLS_HD BLS_INLINE void fp2_inv(fp2& r, const fp2& a) {
+BLS_HD BLS_CALL void fp2_inv(fp2& r, const fp2& a) {
   fp t0, t1;
   fp_sqr(t0, a.c0);
   fp_sqr(t1, a.c1);
@@ -149,7 +149,7 @@ BLS_HD BLS_INLINE void fp2_inv(fp2& r, const fp2& a) {
   fp_neg(r.c1, t0);
 }
 
-BLS_HD BLS_INLINE void fp6_mul(fp6& r, const fp6& a, const fp6& b) {
+BLS_HD BLS_CALL void fp6_mul(fp6& r, const fp6& a, const fp6& b) {
   // Karatsuba over Fp2 (6 Fp2 products)
   fp2 t0, t1, t2, s0, s1, u0, u1, u2;
   fp2_mul(t0, a.c0, b.c0);
@@ -183,7 +183,7 @@ BLS_HD BLS_INLINE void fp6_mul(fp6& r, const fp6& a, const fp6& b) {
   r.c1 = u1;
   r.c2 = u2;
 }
-BLS_HD BLS_INLINE void fp6_sqr(fp6& r, const fp6& a) {
+BLS_HD BLS_CALL void fp6_sqr(fp6& r, const fp6& a) {
   // Chung-Hasan SQR2
   fp2 s0, s1, s2, s3, s4, t;
   fp2_sqr(s0, a.c0);
@@ -208,7 +208,7 @@ BLS_HD BLS_INLINE void fp6_sqr(fp6& r, const fp6& a) {
   r.c1 = c1;
   r.c2 = c2;
 }
-BLS_HD BLS_INLINE void fp6_inv(fp6& r, const fp6& a) {
+BLS_HD BLS_CALL void fp6_inv(fp6& r, const fp6& a) {
   fp2 c0, c1, c2, t, s;
   fp2_sqr(c0, a.c0);
   fp2_mul(t, a.c1, a.c2);
@@ -232,7 +232,7 @@ BLS_HD BLS_INLINE void fp6_inv(fp6& r, const fp6& a) {
   fp2_mul(r.c1, c1, t);
   fp2_mul(r.c2, c2, t);
 }
-BLS_HD BLS_INLINE void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& b1) {
+BLS_HD BLS_CALL void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& b1) {
   // (a0 + a1 v + a2 v^2)(b0 + b1 v): 5 Fp2 products
   fp2 t0, t1, s0, s1, u;
   fp2_mul(t0, a.c0, b0);
@@ -255,7 +255,7 @@ BLS_HD BLS_INLINE void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2
   r.c1 = c1;
   r.c2 = c2;
 }
-BLS_HD BLS_INLINE void fp6_mul_1(fp6& r, const fp6& a, const fp2& b1) {
+BLS_HD BLS_CALL void fp6_mul_1(fp6& r, const fp6& a, const fp2& b1) {
   // (a0 + a1 v + a2 v^2) b1 v = xi a2 b1 + a0 b1 v + a1 b1 v^2
   fp2 c0, c1, c2;
   fp2_mul(c0, a.c2, b1);
@@ -267,7 +267,7 @@ BLS_HD BLS_INLINE void fp6_mul_1(fp6& r, const fp6& a, const fp2& b1) {
   r.c2 = c2;
 }
 
-BLS_HD BLS_INLINE void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
+BLS_HD BLS_CALL void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
   fp6 t0, t1, s0, s1;
   fp6_mul(t0, a.c0, b.c0);
   fp6_mul(t1, a.c1, b.c1);
@@ -281,7 +281,7 @@ BLS_HD BLS_INLINE void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
   fp6_add(r.c0, t0, t1);
   r.c1 = c1;
 }
-BLS_HD BLS_INLINE void fp12_sqr(fp12& r, const fp12& a) {
+BLS_HD BLS_CALL void fp12_sqr(fp12& r, const fp12& a) {
   // complex squaring: c0 = (a0+a1)(a0+v a1) - t - v t, c1 = 2t, t = a0 a1
   fp6 t, s0, s1, vt;
   fp6_mul(t, a.c0, a.c1);
@@ -294,7 +294,7 @@ BLS_HD BLS_INLINE void fp12_sqr(fp12& r, const fp12& a) {
   fp6_sub(r.c0, s0, vt);
   fp6_add(r.c1, t, t);
 }
-BLS_HD BLS_INLINE void fp12_inv(fp12& r, const fp12& a) {
+BLS_HD BLS_CALL void fp12_inv(fp12& r, const fp12& a) {
   fp6 t0, t1;
   fp6_sqr(t0, a.c0);
   fp6_sqr(t1, a.c1);
@@ -305,7 +305,7 @@ BLS_HD BLS_INLINE void fp12_inv(fp12& r, const fp12& a) {
   fp6_mul(t1, a.c1, t0);
   fp6_neg(r.c1, t1);
 }
-BLS_HD BLS_INLINE void fp12_mul_line(fp12& f, const fp2& g0, const fp2& g1, const fp2& h1) {
+BLS_HD BLS_CALL void fp12_mul_line(fp12& f, const fp2& g0, const fp2& g1, const fp2& h1) {
   // f = (a0 + a1 w)(G + H w), G = g0 + g1 v, H = h1 v:
   //   c0 = a0 G + v (a1 H),  c1 = (a0 + a1)(G + H) - a0 G - a1 H
   fp6 t0, t1, s;
@@ -320,7 +320,7 @@ BLS_HD BLS_INLINE void fp12_mul_line(fp12& f, const fp2& g0, const fp2& g1, cons
   fp6_mul_v(t1, t1);
   fp6_add(f.c0, t0, t1);
 }
-BLS_HD BLS_INLINE void fp12_frobenius(fp12& r, const fp12& a, int j) {
+BLS_HD BLS_CALL void fp12_frobenius(fp12& r, const fp12& a, int j) {
   // coefficient of w^k (k = 2i + h for a.c_h.c_i) is conj^j(c) * gamma_{j,k}
   const fp2* g = j == 1 ? FROB1 : (j == 2 ? FROB2 : FROB3);
   const fp2* src[6] = {&a.c0.c0, &a.c1.c0, &a.c0.c1, &a.c1.c1, &a.c0.c2, &a.c1.c2};
@@ -336,7 +336,7 @@ BLS_HD BLS_INLINE void fp12_frobenius(fp12& r, const fp12& a, int j) {
   }
   for (int k = 0; k < 6; ++k) *dst[k] = tmp[k];
 }
-BLS_HD BLS_INLINE void fp12_cyclotomic_sqr(fp12& r, const fp12& a) {
+BLS_HD BLS_CALL void fp12_cyclotomic_sqr(fp12& r, const fp12& a) {
   // Granger-Scott: view a in Fp4^3 with Fp4 = Fp2[s]/(s^2 - xi), s = w^3... pairs
   // (g0,g1) := (c0.c0, c1.c1), (g2,g3) := (c1.c0, c0.c2), (g4,g5) := (c0.c1, c1.c2)
   fp2 z0 = a.c0.c0, z4 = a.c0.c1, z3 = a.c0.c2;

@@ -1,0 +1,287 @@
+"""Host-side mirror of charon's tbls.Implementation backed by the HIP engine (libhipbls.so).
+
+charon's Go interface (/root/reference/tbls/tbls.go:28-69) has 11 methods; `HipBLS` exposes the
+same methods with the same argument meaning and the same error strings as tbls.Herumi
+(/root/reference/tbls/herumi.go), plus the batched entry points the north star adds
+(`batch_verify`, `batch_threshold_aggregate`).  Every curve operation runs on the GPU through the
+C-ABI in include/hipbls.h; there is no CPU fallback: constructing `HipBLS` without the built
+library or without a GPU raises.
+
+The Go binding a charon maintainer would add (tbls/hipbls, cgo) is in INTEGRATION.md; this module
+is the same boundary seen from Python, used by the parity tests and bench.py.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import secrets
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+OK, ERR_PUBKEY, ERR_SIGNATURE, ERR_VERIFY, ERR_SECRET, ERR_COMBINE = 0, 1, 2, 3, 4, 5
+ERR_ARG, ERR_DEVICE = 16, 17
+
+# tbls/herumi.go error strings by status code
+VERIFY_ERRORS = {
+    ERR_PUBKEY: "cannot set compressed public key in Herumi format",
+    ERR_SIGNATURE: "cannot unmarshal signature into Herumi signature",
+    ERR_VERIFY: "signature not verified",
+}
+
+
+class TBLSError(Exception):
+    """A tbls error: message is the string tbls.Herumi returns for the same input."""
+
+
+class DeviceError(RuntimeError):
+    """HIP runtime failure.  Never converted into a 'verified' result."""
+
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhipbls.so")
+_lib = None
+
+
+def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
+    """Load libhipbls.so and declare the C-ABI; raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError("hipbls native library not built: %s (run __graft_entry__.build())" % path)
+    lib = ctypes.CDLL(path)
+    u8p = ctypes.c_char_p
+    u64 = ctypes.c_uint64
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    vp = ctypes.c_void_p
+    sig = {
+        "hipbls_abi_version": ([], ctypes.c_int),
+        "hipbls_init": ([ctypes.c_int], ctypes.c_int),
+        "hipbls_device_count": ([], ctypes.c_int),
+        "hipbls_last_error": ([], ctypes.c_char_p),
+        "hipbls_verify_batch": ([u8p, u8p, u64p, u8p, u64, i32p], ctypes.c_int),
+        "hipbls_threshold_aggregate_batch": ([u8p, u32p, u64p, u64, u8p, i32p], ctypes.c_int),
+        "hipbls_sign_batch": ([u8p, u8p, u64p, u64, u8p, i32p], ctypes.c_int),
+        "hipbls_secret_to_public_key_batch": ([u8p, u64, u8p, i32p], ctypes.c_int),
+        "hipbls_verify_aggregate": ([u8p, u64, u8p, u8p, u64, i32p], ctypes.c_int),
+        "hipbls_aggregate": ([u8p, u64, u8p, i32p], ctypes.c_int),
+        "hipbls_threshold_split": ([u8p, u8p, ctypes.c_uint32, ctypes.c_uint32, u8p, i32p], ctypes.c_int),
+        "hipbls_recover_secret": ([u8p, u32p, ctypes.c_uint32, u8p, i32p], ctypes.c_int),
+        "hipbls_verify_batch_device": ([vp, vp, vp, vp, u64, vp, vp], ctypes.c_int),
+        "hipbls_threshold_aggregate_batch_device": ([vp, vp, vp, u64, vp, vp, vp], ctypes.c_int),
+        "hipbls_sign_batch_device": ([vp, vp, vp, u64, vp, vp, vp], ctypes.c_int),
+        "hipbls_secret_to_public_key_batch_device": ([vp, u64, vp, vp, vp], ctypes.c_int),
+        "hipbls_kernel_timing": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), u64p], ctypes.c_int),
+        "hipbls_kernel_timing_reset": ([], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> List[str]:
+    return [
+        "hipbls_abi_version", "hipbls_init", "hipbls_device_count", "hipbls_last_error",
+        "hipbls_verify_batch", "hipbls_threshold_aggregate_batch", "hipbls_sign_batch",
+        "hipbls_secret_to_public_key_batch", "hipbls_verify_aggregate", "hipbls_aggregate",
+        "hipbls_threshold_split", "hipbls_recover_secret", "hipbls_verify_batch_device",
+        "hipbls_threshold_aggregate_batch_device", "hipbls_sign_batch_device",
+        "hipbls_secret_to_public_key_batch_device", "hipbls_kernel_timing", "hipbls_kernel_timing_reset",
+    ]
+
+
+def _check(rc: int, lib) -> None:
+    if rc == OK:
+        return
+    msg = lib.hipbls_last_error()
+    msg = msg.decode() if msg else ""
+    if rc == ERR_DEVICE:
+        raise DeviceError("hipbls device error: " + msg)
+    raise ValueError("hipbls invalid argument (rc=%d) %s" % (rc, msg))
+
+
+def _offsets(msgs: Sequence[bytes]):
+    offs = (ctypes.c_uint64 * (len(msgs) + 1))()
+    acc = 0
+    for i, m in enumerate(msgs):
+        offs[i] = acc
+        acc += len(m)
+    offs[len(msgs)] = acc
+    return b"".join(msgs), offs
+
+
+def _status_array(n: int):
+    return (ctypes.c_int32 * max(n, 1))()
+
+
+class HipBLS:
+    """tbls.Implementation on MI355X.  Method names follow tbls.go:28-69 (snake_case)."""
+
+    def __init__(self, device: Optional[int] = None):
+        self.lib = load_library()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        _check(self.lib.hipbls_init(device), self.lib)
+
+    # ---------------------------------------------------------------- key tooling
+    def generate_secret_key(self) -> bytes:
+        """herumi.go:59-69 (SetByCSPRNG): uniform secret in [0, r)."""
+        while True:
+            v = int.from_bytes(secrets.token_bytes(32), "big") & ((1 << 255) - 1)
+            if v < R:
+                return v.to_bytes(32, "big")
+
+    def generate_insecure_key(self, random) -> bytes:
+        """herumi.go:343-360: up to 100 reads of 32 bytes until one deserializes (< r)."""
+        for _ in range(100):
+            b = random.read(32)
+            if int.from_bytes(b, "big") < R:
+                return bytes(b)
+        raise TBLSError("cannot generate insecure key")
+
+    def secret_to_public_key(self, secret: bytes) -> bytes:
+        pk, st = self.secret_to_public_key_batch([secret])
+        if st[0] != OK:
+            v = int.from_bytes(secret, "big")
+            if v >= R:
+                raise TBLSError("cannot unmarshal secret into Herumi secret key")
+            raise TBLSError("cannot obtain public key from secret")
+        return pk[0]
+
+    def secret_to_public_key_batch(self, secrets_: Sequence[bytes]) -> Tuple[List[bytes], List[int]]:
+        n = len(secrets_)
+        out = ctypes.create_string_buffer(48 * max(n, 1))
+        st = _status_array(n)
+        _check(self.lib.hipbls_secret_to_public_key_batch(b"".join(secrets_), n, out, st), self.lib)
+        return [out.raw[48 * i:48 * i + 48] for i in range(n)], [st[i] for i in range(n)]
+
+    def _split(self, secret: bytes, total: int, threshold: int, tail: Sequence[bytes]) -> Dict[int, bytes]:
+        if int.from_bytes(secret, "big") >= R:
+            raise TBLSError("cannot unmarshal bytes into Herumi secret key")
+        out = ctypes.create_string_buffer(32 * total)
+        st = _status_array(1)
+        _check(self.lib.hipbls_threshold_split(secret, b"".join(tail), total, threshold, out, st), self.lib)
+        if st[0] != OK:
+            raise TBLSError("cannot unmarshal bytes into Herumi secret key")
+        return {i + 1: out.raw[32 * i:32 * i + 32] for i in range(total)}
+
+    def threshold_split(self, secret: bytes, total: int, threshold: int) -> Dict[int, bytes]:
+        """herumi.go:134-181: polynomial tail from the CSPRNG."""
+        tail = [self.generate_secret_key() for _ in range(threshold - 1)]
+        return self._split(secret, total, threshold, tail)
+
+    def threshold_split_insecure(self, secret: bytes, total: int, threshold: int, random) -> Dict[int, bytes]:
+        """herumi.go:84-132: polynomial tail from an insecure reader."""
+        tail = [self.generate_insecure_key(random) for _ in range(threshold - 1)]
+        return self._split(secret, total, threshold, tail)
+
+    def recover_secret(self, shares: Mapping[int, bytes], total: int = 0, threshold: int = 0) -> bytes:
+        """herumi.go:183-218."""
+        ids = list(shares.keys())
+        for i in ids:
+            if int.from_bytes(shares[i], "big") >= R:
+                raise TBLSError("cannot unmarshal key with into Herumi secret key")
+        arr = (ctypes.c_uint32 * max(len(ids), 1))(*[int(i) & 0xFFFFFFFF for i in ids])
+        out = ctypes.create_string_buffer(32)
+        st = _status_array(1)
+        _check(self.lib.hipbls_recover_secret(b"".join(shares[i] for i in ids), arr, len(ids), out, st), self.lib)
+        if st[0] != OK:
+            raise TBLSError("cannot recover full private key from partial keys")
+        return out.raw
+
+    # ---------------------------------------------------------------- hot path
+    def sign(self, private_key: bytes, data: bytes) -> bytes:
+        sigs, st = self.sign_batch([private_key], [data])
+        if st[0] != OK:
+            raise TBLSError("cannot unmarshal secret into Herumi secret key")
+        return sigs[0]
+
+    def sign_batch(self, sks: Sequence[bytes], msgs: Sequence[bytes]) -> Tuple[List[bytes], List[int]]:
+        n = len(sks)
+        blob, offs = _offsets(msgs)
+        out = ctypes.create_string_buffer(96 * max(n, 1))
+        st = _status_array(n)
+        _check(self.lib.hipbls_sign_batch(b"".join(sks), blob, offs, n, out, st), self.lib)
+        return [out.raw[96 * i:96 * i + 96] for i in range(n)], [st[i] for i in range(n)]
+
+    def verify(self, compressed_public_key: bytes, data: bytes, signature: bytes) -> None:
+        """herumi.go:285-301: raises TBLSError with the reference's message on failure."""
+        st = self.batch_verify_status([compressed_public_key], [data], [signature])[0]
+        if st != OK:
+            raise TBLSError(VERIFY_ERRORS[st])
+
+    def batch_verify_status(self, pks: Sequence[bytes], msgs: Sequence[bytes], sigs: Sequence[bytes]) -> List[int]:
+        n = len(pks)
+        if not (len(msgs) == n == len(sigs)):
+            raise ValueError("mismatching lengths")
+        if any(len(p) != 48 for p in pks) or any(len(s) != 96 for s in sigs):
+            raise ValueError("bad key/signature length")
+        blob, offs = _offsets(msgs)
+        st = _status_array(n)
+        _check(self.lib.hipbls_verify_batch(b"".join(pks), blob, offs, b"".join(sigs), n, st), self.lib)
+        return [st[i] for i in range(n)]
+
+    def batch_verify(self, pks, msgs, sigs) -> List[Optional[TBLSError]]:
+        """Per-item outcome of Verify: None when valid, else the TBLSError Verify would raise."""
+        return [None if s == OK else TBLSError(VERIFY_ERRORS[s]) for s in self.batch_verify_status(pks, msgs, sigs)]
+
+    def threshold_aggregate(self, partial_signatures_by_index: Mapping[int, bytes]) -> bytes:
+        """herumi.go:244-283."""
+        res = self.batch_threshold_aggregate([partial_signatures_by_index])[0]
+        if isinstance(res, TBLSError):
+            raise res
+        return res
+
+    def batch_threshold_aggregate(self, groups: Sequence[Mapping[int, bytes]]):
+        """One ThresholdAggregate per group; returns the 96-byte signature or the TBLSError."""
+        n_groups = len(groups)
+        offs = (ctypes.c_uint64 * (n_groups + 1))()
+        ids, sigs = [], []
+        for g, grp in enumerate(groups):
+            offs[g] = len(ids)
+            for idx, s in grp.items():
+                ids.append(int(idx) & 0xFFFFFFFF if int(idx) >= 0 else 0)
+                sigs.append(bytes(s))
+        offs[n_groups] = len(ids)
+        arr = (ctypes.c_uint32 * max(len(ids), 1))(*ids)
+        out = ctypes.create_string_buffer(96 * max(n_groups, 1))
+        st = _status_array(n_groups)
+        _check(self.lib.hipbls_threshold_aggregate_batch(b"".join(sigs), arr, offs, n_groups, out, st), self.lib)
+        res = []
+        for g in range(n_groups):
+            if st[g] == OK:
+                res.append(out.raw[96 * g:96 * g + 96])
+            elif st[g] == ERR_SIGNATURE:
+                res.append(TBLSError("cannot unmarshal signature into Herumi signature"))
+            else:
+                res.append(TBLSError("cannot combine signatures"))
+        return res
+
+    def verify_aggregate(self, shares: Sequence[bytes], signature: bytes, data: bytes) -> None:
+        """herumi.go:315-339 (FastAggregateVerify)."""
+        st = _status_array(1)
+        _check(self.lib.hipbls_verify_aggregate(b"".join(shares), len(shares), signature, data, len(data), st),
+               self.lib)
+        if st[0] == ERR_SIGNATURE:
+            raise TBLSError("cannot unmarshal signature into Herumi signature")
+        if st[0] == ERR_PUBKEY:
+            raise TBLSError("cannot set compressed public key in Herumi format")
+        if st[0] != OK:
+            raise TBLSError("signature verification failed")
+
+    def aggregate(self, signs: Sequence[bytes]) -> bytes:
+        """herumi.go:220-242."""
+        out = ctypes.create_string_buffer(96)
+        st = _status_array(1)
+        _check(self.lib.hipbls_aggregate(b"".join(signs), len(signs), out, st), self.lib)
+        if st[0] == ERR_SIGNATURE:
+            raise TBLSError("cannot unmarshal signature into Herumi signature")
+        if st[0] != OK:
+            raise TBLSError("cannot aggregate zero signatures")
+        return out.raw

@@ -204,3 +204,14 @@ def test_threshold_aggregate_host(L):
     out = buf(96)
     assert L.ht_threshold_aggregate(sigs, arr, 4, out) == 0
     assert out.raw == bls.sign(bls.sk_serialize(secret), msg)
+
+
+def test_fixtures_verify_host(L):
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fixtures.json")) as f:
+        fx = json.load(f)
+    for c in fx["verify"]:
+        msg = bytes.fromhex(c["msg"])
+        st = L.ht_verify(bytes.fromhex(c["pk"]), msg, len(msg), bytes.fromhex(c["sig"]))
+        assert st == c["status"], c["note"]
