@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""Benchmark: charon's BLS hot path on MI355X (BASELINE.json metric).
+
+  python bench.py --gpus N --steps K --warmup W
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Step = one pass of the hot path over one batch: tbls.Verify of the configs[1] workload (C2:
+65,536 partial signatures over distinct 32-byte signing roots, 1% corrupted) through the C-ABI
+device entry point, inputs already resident in HBM.  Multi-GPU is weak scaling: every rank owns its
+own validator-index shard of the same size (no data-path collective).  Threshold aggregation (C3:
+10,000 validators x 7-of-10 + Verify of each aggregate) is timed after the main loop and reported as
+an extra field.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import ctypes
+import json
+import os
+import random
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SEED = 0x636861726F6E
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+METRIC = "verified BLS partial sigs/sec (node) + threshold aggregates/sec, 1/2/4/8 GPU"
+
+# Algorithmic work per honest Verify of a 32-byte root, in Fp-multiplication equivalents
+# (one 381-bit Montgomery product, fp_mul or fp_sqr, = 12x12 CIOS = 300 32x32->64 multiply-adds).
+# Counted by the instrumented host build of the same kernels (tests/test_work_counts.py keeps
+# this in sync).  See DESIGN.md "Roofline".
+FPMUL_PER_VERIFY = 37122
+MADS_PER_FPMUL = 300
+# gfx950 32x32->64 integer multiply-add peak (v_mad_u64_u32): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+# at half rate (measured: profiles/r01_mad_probe.txt) = 39.3e12 MAD/s.
+MAD_PEAK_T = 39.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=65536, help="verifies per GPU per step (C2: 65,536)")
+    ap.add_argument("--tagg-groups", type=int, default=10000, help="C3 validators per GPU (0 = skip)")
+    ap.add_argument("--tagg-steps", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=16, help="oracle verifies for cpu_baseline (0 = skip)")
+    return ap.parse_args()
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def make_c2(impl, n, rng):
+    """n partial signatures by 4,096 share keys over distinct roots; 1% corrupted at seeded spots."""
+    nkeys = min(4096, n)
+    sks = [rng.randrange(1, R_ORDER).to_bytes(32, "big") for _ in range(nkeys)]
+    pks, st = impl.secret_to_public_key_batch(sks)
+    assert set(st) == {0}
+    roots = [rng.randbytes(32) for _ in range(n)]
+    owner = [i % nkeys for i in range(n)]
+    sigs, st = impl.sign_batch([sks[o] for o in owner], roots)
+    assert set(st) == {0}
+    pk_list = [pks[o] for o in owner]
+    bad = sorted(rng.sample(range(n), max(1, n // 100)))
+    for j, i in enumerate(bad):
+        kind = j % 3
+        if kind == 0:    # wrong root
+            roots[i] = bytes(32 - len(roots[i][:1])) + roots[i][:1]
+        elif kind == 1:  # swapped share (another validator's pubshare)
+            pk_list[i] = pks[(owner[i] + 1) % nkeys]
+        else:            # flipped bit in the signature
+            s = bytearray(sigs[i])
+            s[40] ^= 0x04
+            sigs[i] = bytes(s)
+    return pk_list, roots, sigs, set(bad)
+
+
+def make_c3(impl, groups, rng, t=7, n=10):
+    """groups DVs, each split t-of-n; a random t-subset of partials per DV; DV pubkeys + one root each."""
+    secrets_ = [rng.randrange(1, R_ORDER) for _ in range(groups)]
+    roots = [rng.randbytes(32) for _ in range(groups)]
+    part_sks, part_msgs, part_ids, offs = [], [], [], [0]
+    for g in range(groups):
+        poly = [secrets_[g]] + [rng.randrange(R_ORDER) for _ in range(t - 1)]
+        ids = sorted(rng.sample(range(1, n + 1), t))
+        for i in ids:
+            acc = 0
+            for c in reversed(poly):
+                acc = (acc * i + c) % R_ORDER
+            part_sks.append(acc.to_bytes(32, "big"))
+            part_msgs.append(roots[g])
+            part_ids.append(i)
+        offs.append(len(part_ids))
+    psigs, st = impl.sign_batch(part_sks, part_msgs)
+    assert set(st) == {0}
+    dv_pks, st = impl.secret_to_public_key_batch([s.to_bytes(32, "big") for s in secrets_])
+    assert set(st) == {0}
+    return psigs, part_ids, offs, dv_pks, roots
+
+
+def cpu_baseline(n_sample, rng):
+    """Oracle (oracle/bls12381.py, pure Python, 1 core) timed on this host: kind 'port'."""
+    from oracle import bls12381 as bls
+    sks = [rng.randrange(1, R_ORDER).to_bytes(32, "big") for _ in range(4)]
+    items = []
+    for i in range(n_sample):
+        sk = sks[i % 4]
+        m = rng.randbytes(32)
+        items.append((bls.secret_to_public_key(sk), m, bls.sign(sk, m)))
+    t0 = time.perf_counter()
+    ok = sum(bls.verify_status(pk, m, s) == 0 for pk, m, s in items)
+    dt = time.perf_counter() - t0
+    assert ok == n_sample
+    return {"value": round(n_sample / dt, 3), "unit": "verifies/s", "cores": 1, "kind": "port",
+            "sample": "%d tbls.Verify calls of C2 items (32-byte roots) through oracle/bls12381.py, "
+                      "single-threaded CPython; not herumi (no Go toolchain / herumi module on the box)" % n_sample}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        dist.init_process_group(backend=backend)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from charon_amd.tbls import HipBLS, load_library
+    impl = HipBLS(device=local)
+    lib = load_library()
+
+    rng = random.Random(SEED * 1000003 + rank)  # validator-index shard of this rank
+    t0 = time.time()
+    pks, roots, sigs, bad = make_c2(impl, args.n, rng)
+    log("rank %d: C2 data (%d items) in %.1fs" % (rank, args.n, time.time() - t0))
+
+    n = args.n
+    d_pk = torch.frombuffer(bytearray(b"".join(pks)), dtype=torch.uint8).to(dev)
+    d_sig = torch.frombuffer(bytearray(b"".join(sigs)), dtype=torch.uint8).to(dev)
+    d_msg = torch.frombuffer(bytearray(b"".join(roots)), dtype=torch.uint8).to(dev)
+    d_off = torch.arange(0, 32 * (n + 1), 32, dtype=torch.int64).to(dev)
+    d_st = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        rc = lib.hipbls_verify_batch_device(d_pk.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(), d_sig.data_ptr(),
+                                            n, d_st.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError("hipbls_verify_batch_device rc=%d %s" % (rc, lib.hipbls_last_error()))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    lib.hipbls_kernel_timing_reset()
+    barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+
+    st = d_st.cpu().tolist()
+    fails = {i for i, s in enumerate(st) if s != 0}
+    assert fails == bad, "verify bitmap mismatch: %d unexpected, %d missed" % (len(fails - bad), len(bad - fails))
+    avg_ms = ctypes.c_double()
+    launches = ctypes.c_uint64()
+    lib.hipbls_kernel_timing(b"verify", ctypes.byref(avg_ms), ctypes.byref(launches))
+
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    elapsed = float(t_max.item())
+    total = n * args.steps * world
+    value = total / elapsed
+
+    # ---- C3: threshold aggregation + Verify of the aggregate (extra field)
+    tagg = None
+    if args.tagg_groups > 0:
+        t0 = time.time()
+        psigs, pids, poffs, dv_pks, droots = make_c3(impl, args.tagg_groups, rng)
+        log("rank %d: C3 data (%d groups) in %.1fs" % (rank, args.tagg_groups, time.time() - t0))
+        G = args.tagg_groups
+        d_psig = torch.frombuffer(bytearray(b"".join(psigs)), dtype=torch.uint8).to(dev)
+        d_pid = torch.tensor(pids, dtype=torch.int32).to(dev)
+        d_poff = torch.tensor(poffs, dtype=torch.int64).to(dev)
+        d_agg = torch.zeros(G * 96, dtype=torch.uint8, device=dev)
+        d_gst = torch.full((G,), -1, dtype=torch.int32, device=dev)
+        d_dpk = torch.frombuffer(bytearray(b"".join(dv_pks)), dtype=torch.uint8).to(dev)
+        d_dmsg = torch.frombuffer(bytearray(b"".join(droots)), dtype=torch.uint8).to(dev)
+        d_doff = torch.arange(0, 32 * (G + 1), 32, dtype=torch.int64).to(dev)
+        d_vst = torch.full((G,), -1, dtype=torch.int32, device=dev)
+
+        def tstep():
+            rc = lib.hipbls_threshold_aggregate_batch_device(d_psig.data_ptr(), d_pid.data_ptr(), d_poff.data_ptr(), G,
+                                                             d_agg.data_ptr(), d_gst.data_ptr(),
+                                                             ctypes.c_void_p(stream.cuda_stream))
+            assert rc == 0
+            rc = lib.hipbls_verify_batch_device(d_dpk.data_ptr(), d_dmsg.data_ptr(), d_doff.data_ptr(),
+                                                d_agg.data_ptr(), G, d_vst.data_ptr(),
+                                                ctypes.c_void_p(stream.cuda_stream))
+            assert rc == 0
+
+        tstep()
+        torch.cuda.synchronize(dev)
+        barrier()
+        ts = time.perf_counter()
+        for _ in range(args.tagg_steps):
+            tstep()
+        torch.cuda.synchronize(dev)
+        barrier()
+        tel = time.perf_counter() - ts
+        assert set(d_gst.cpu().tolist()) == {0} and set(d_vst.cpu().tolist()) == {0}, "aggregate mismatch"
+        tt = torch.tensor([tel], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tagg = G * args.tagg_steps * world / float(tt.item())
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "verified partial sigs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: seeded share keys, distinct 32-byte roots, 1% corrupted (wrong root / swapped "
+                    "share / flipped sig bit); signatures made by the engine's own sign kernel",
+            "config": {"workload": "C2 (BASELINE.json configs[1]): individual tbls.Verify of %d partial sigs per GPU, "
+                                   "distinct messages" % n,
+                       "items_per_gpu": n, "parallelism": "shard-by-validator-index x %d" % world},
+            "pairings_per_s": round(2 * value, 1),
+            "threshold_aggregates_per_s": round(tagg, 1) if tagg else None,
+            "threshold_aggregate_workload": "C3: %d validators x 7-of-10 Lagrange in G2 + Verify of each aggregate per GPU"
+                                            % args.tagg_groups if tagg else None,
+        }
+        k_ms = avg_ms.value
+        if k_ms > 0:
+            achieved = FPMUL_PER_VERIFY * MADS_PER_FPMUL * n / (k_ms * 1e-3) / 1e12
+            out["roofline"] = {
+                "bound": "valu-int (32x32->64 v_mad_u64_u32; no HBM or MFMA bound: ~190 B in per verify)",
+                "kernel": "k_verify_fused",
+                "achieved": round(achieved, 3),
+                "peak": MAD_PEAK_T,
+                "unit": "Tmad/s",
+                "frac": round(achieved / MAD_PEAK_T, 4),
+                "traffic": None,
+                "algorithmic_unit": "%d Fp-mul-equivalents x %d MADs per verify" % (FPMUL_PER_VERIFY, MADS_PER_FPMUL),
+                "kernel_avg_ms": round(k_ms, 3),
+                "kernel_launches": int(launches.value),
+            }
+        if world == 1 and args.cpu_sample > 0:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_sample, random.Random(SEED))
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
