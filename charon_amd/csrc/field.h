@@ -164,6 +164,34 @@ BLS_HD BLS_INLINE void fp_mul_impl(fp& r, const fp& a, const fp& b) {
 // The non-inlined, by-value entry points keep kernels' instruction footprint small (a fully
 // inlined Miller loop would not fit the instruction cache) while passing operands in VGPRs
 // rather than through the private stack.
+#if defined(__HIP_DEVICE_COMPILE__)
+// gfx950: the product is one inline-asm block (tools/gen_fp_asm.py) inside a non-inlined function
+// whose 12-dword vector arguments arrive in v[0:11] / v[12:23] and whose result leaves in v[0:11]
+// per the AMDGPU calling convention -- the asm operands are pinned to exactly those registers.
+typedef uint32_t u32x12 __attribute__((ext_vector_type(12)));
+}  // namespace bls
+#include "fp_asm_gfx950.h"
+namespace bls {
+__device__ __attribute__((noinline)) static u32x12 fp_mul_dev(u32x12 a, u32x12 b) {
+  asm volatile(BLS_FP_MUL_ASM_BODY : "+{v[0:11]}"(a), "+{v[12:23]}"(b) : : BLS_FP_MUL_ASM_CLOBBERS);
+  return a;
+}
+BLS_HD BLS_INLINE u32x12 fp_to_vec(const fp& a) {
+  u32x12 v;
+  v.s0 = a.v[0]; v.s1 = a.v[1]; v.s2 = a.v[2]; v.s3 = a.v[3]; v.s4 = a.v[4]; v.s5 = a.v[5];
+  v.s6 = a.v[6]; v.s7 = a.v[7]; v.s8 = a.v[8]; v.s9 = a.v[9]; v.sA = a.v[10]; v.sB = a.v[11];
+  return v;
+}
+BLS_HD BLS_INLINE void fp_from_vec(fp& r, const u32x12& v) {
+  r.v[0] = v.s0; r.v[1] = v.s1; r.v[2] = v.s2; r.v[3] = v.s3; r.v[4] = v.s4; r.v[5] = v.s5;
+  r.v[6] = v.s6; r.v[7] = v.s7; r.v[8] = v.s8; r.v[9] = v.s9; r.v[10] = v.sA; r.v[11] = v.sB;
+}
+BLS_HD BLS_INLINE void fp_mul(fp& r, const fp& a, const fp& b) { fp_from_vec(r, fp_mul_dev(fp_to_vec(a), fp_to_vec(b))); }
+BLS_HD BLS_INLINE void fp_sqr(fp& r, const fp& a) {
+  const u32x12 v = fp_to_vec(a);
+  fp_from_vec(r, fp_mul_dev(v, v));
+}
+#else
 BLS_HD BLS_NOINLINE fp fp_mul_v(fp a, fp b) {
   BLS_COUNT_MUL();
   fp r;
@@ -178,6 +206,7 @@ BLS_HD BLS_NOINLINE fp fp_sqr_v(fp a) {
 }
 BLS_HD BLS_INLINE void fp_mul(fp& r, const fp& a, const fp& b) { r = fp_mul_v(a, b); }
 BLS_HD BLS_INLINE void fp_sqr(fp& r, const fp& a) { r = fp_sqr_v(a); }
+#endif
 
 // r = a^e for a fixed exponent given as little-endian 32-bit limbs whose top set bit is top_bit
 // (left-to-right binary; the exponent is the same for every lane, so the branch is uniform).
