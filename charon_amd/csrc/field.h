@@ -21,7 +21,9 @@
 // Mid-level building blocks (Fp6/Fp12 products, curve steps, hash stages) are real calls: their
 // bodies are emitted once, so a kernel's instruction footprint stays within the instruction cache
 // and compile time stays linear.  Fp and Fp2 arithmetic is inlined into them.
+#ifndef BLS_CALL
 #define BLS_CALL static __attribute__((noinline))
+#endif
 
 namespace bls {
 
@@ -73,6 +75,30 @@ BLS_HD BLS_INLINE bool fp_eq(const fp& a, const fp& b) {
   return acc == 0;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// Device: explicit 32-bit carry chains (__builtin_addc/__builtin_subc lower to v_add_co/v_addc_co and
+// v_sub_co/v_subb_co), ~43 VALU per add or sub; the generic 64-bit form below compiles to ~110.
+// r = a + b mod p
+BLS_HD BLS_INLINE void fp_add(fp& r, const fp& a, const fp& b) {
+  uint32_t s[12], d[12], c = 0, br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) s[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  // s < 2p < 2^384: subtract p, keep s on borrow
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d[i] = __builtin_subc(s[i], P_LIMBS[i], br, &br);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = br ? s[i] : d[i];
+}
+// r = a - b mod p
+BLS_HD BLS_INLINE void fp_sub(fp& r, const fp& a, const fp& b) {
+  uint32_t d[12], c = 0, br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+  const uint32_t m = 0u - br;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = __builtin_addc(d[i], P_LIMBS[i] & m, c, &c);
+}
+#else
 // r = a + b mod p
 BLS_HD BLS_INLINE void fp_add(fp& r, const fp& a, const fp& b) {
   uint32_t s[12];
@@ -116,6 +142,8 @@ BLS_HD BLS_INLINE void fp_sub(fp& r, const fp& a, const fp& b) {
     c >>= 32;
   }
 }
+
+#endif
 
 BLS_HD BLS_INLINE void fp_neg(fp& r, const fp& a) {
   fp z;
@@ -161,19 +189,28 @@ BLS_HD BLS_INLINE void fp_mul_impl(fp& r, const fp& a, const fp& b) {
   for (int i = 0; i < 12; ++i) r.v[i] = keep_t ? t[i] : d[i];
 }
 
-// The non-inlined, by-value entry points keep kernels' instruction footprint small (a fully
-// inlined Miller loop would not fit the instruction cache) while passing operands in VGPRs
-// rather than through the private stack.
+// gfx950: the product is one hand-scheduled routine (tools/gen_fp_asm.py) emitted ONCE into the
+// code object and reached by an s_swappc from inline asm.  Because the compiler sees an asm block
+// rather than a call, the only registers it must treat as clobbered are the ones the routine really
+// touches (v24-v39, s16-s31, vcc) -- not the ABI's whole caller-saved set -- so values live across
+// a product stay in registers instead of being saved to scratch around every multiplication.
+// Operands are pinned: a in v[0:11] (result out), b in v[12:23].
 #if defined(__HIP_DEVICE_COMPILE__)
-// gfx950: the product is one inline-asm block (tools/gen_fp_asm.py) inside a non-inlined function
-// whose 12-dword vector arguments arrive in v[0:11] / v[12:23] and whose result leaves in v[0:11]
-// per the AMDGPU calling convention -- the asm operands are pinned to exactly those registers.
 typedef uint32_t u32x12 __attribute__((ext_vector_type(12)));
 }  // namespace bls
 #include "fp_asm_gfx950.h"
 namespace bls {
-__device__ __attribute__((noinline)) static u32x12 fp_mul_dev(u32x12 a, u32x12 b) {
-  asm volatile(BLS_FP_MUL_ASM_BODY : "+{v[0:11]}"(a), "+{v[12:23]}"(b) : : BLS_FP_MUL_ASM_CLOBBERS);
+// Never called: hosts the routine's code (entered only at the local label).
+__device__ __attribute__((used, noinline)) static void bls_fp_asm_routines() {
+  asm volatile("s_endpgm\n.p2align 6\n.type bls_fp_mul_rt,@function\nbls_fp_mul_rt:\n\t" BLS_FP_MUL_ASM_BODY
+               "\n\ts_setpc_b64 s[30:31]\n");
+}
+#define BLS_ASM_CALL(fn)                                                                           \
+  "s_getpc_b64 s[16:17]\n\ts_add_u32 s16, s16, " fn "@rel32@lo+4\n\ts_addc_u32 s17, s17, " fn \
+  "@rel32@hi+12\n\ts_swappc_b64 s[30:31], s[16:17]\n\t"
+__device__ __forceinline__ static u32x12 fp_mul_dev(u32x12 a, u32x12 b) {
+  asm volatile(BLS_ASM_CALL("bls_fp_mul_rt") : "+{v[0:11]}"(a), "+{v[12:23]}"(b) : : BLS_FP_MUL_ASM_CLOBBERS,
+               "s30", "s31", "scc");
   return a;
 }
 BLS_HD BLS_INLINE u32x12 fp_to_vec(const fp& a) {
