@@ -30,7 +30,7 @@ METRIC = "verified BLS partial sigs/sec (node) + threshold aggregates/sec, 1/2/4
 # (one 381-bit Montgomery product, fp_mul or fp_sqr, = 12x12 CIOS = 300 32x32->64 multiply-adds).
 # Counted by the instrumented host build of the same kernels (tests/test_work_counts.py keeps
 # this in sync).  See DESIGN.md "Roofline".
-FPMUL_PER_VERIFY = 37122
+FPMUL_PER_VERIFY = 35091
 MADS_PER_FPMUL = 300
 # gfx950 32x32->64 integer multiply-add peak (v_mad_u64_u32): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 # at half rate (measured: profiles/r01_mad_probe.txt) = 39.3e12 MAD/s.
