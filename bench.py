@@ -127,12 +127,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        dist.init_process_group(backend=backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:  # "nccl" is RCCL on ROCm
+        dist.init_process_group(backend="nccl", device_id=dev)
 
+    from charon_amd.shard import gather_bitmaps, pack_bitmap, unpack_bitmap
     from charon_amd.tbls import HipBLS, load_library
     impl = HipBLS(device=local)
     lib = load_library()
@@ -149,12 +149,15 @@ def main():
     d_off = torch.arange(0, 32 * (n + 1), 32, dtype=torch.int64).to(dev)
     d_st = torch.full((n,), -1, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    gathered = [None]
 
     def step():
         rc = lib.hipbls_verify_batch_device(d_pk.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(), d_sig.data_ptr(),
                                             n, d_st.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
         if rc != 0:
             raise RuntimeError("hipbls_verify_batch_device rc=%d %s" % (rc, lib.hipbls_last_error()))
+        if world > 1:  # the only collective: all-gather of the per-rank verify bitmaps (RCCL/xGMI)
+            gathered[0] = gather_bitmaps(pack_bitmap(d_st))
 
     def barrier():
         if world > 1:
@@ -176,6 +179,9 @@ def main():
     st = d_st.cpu().tolist()
     fails = {i for i, s in enumerate(st) if s != 0}
     assert fails == bad, "verify bitmap mismatch: %d unexpected, %d missed" % (len(fails - bad), len(bad - fails))
+    if world > 1:  # my row of the gathered node bitmap equals my local result
+        mine = unpack_bitmap(gathered[0][rank], n).cpu()
+        assert {i for i in range(n) if not mine[i]} == bad, "gathered bitmap mismatch"
     avg_ms = ctypes.c_double()
     launches = ctypes.c_uint64()
     lib.hipbls_kernel_timing(b"verify", ctypes.byref(avg_ms), ctypes.byref(launches))
