@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(kBlock) k_g1_decode(const uint8_t* __restrict_
 }
 
 // FastAggregateVerify tail: one lane sums the decoded keys, hashes, pairs.
-__global__ void k_fast_aggregate_verify_tail(const uint32_t* __restrict__ pts, const int32_t* __restrict__ code,
+__global__ void __launch_bounds__(kBlock) k_fast_aggregate_verify_tail(const uint32_t* __restrict__ pts, const int32_t* __restrict__ code,
                                              uint64_t n, const uint8_t* __restrict__ sig,
                                              const uint8_t* __restrict__ msg, uint64_t msg_len,
                                              int32_t* __restrict__ status) {
@@ -190,7 +190,7 @@ __global__ void k_fast_aggregate_verify_tail(const uint32_t* __restrict__ pts, c
   *status = pairing_check_verify(pk, hm, s) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }
 
-__global__ void k_aggregate(const uint8_t* __restrict__ sigs, uint64_t n, uint8_t* __restrict__ out,
+__global__ void __launch_bounds__(kBlock) k_aggregate(const uint8_t* __restrict__ sigs, uint64_t n, uint8_t* __restrict__ out,
                             int32_t* __restrict__ status) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   if (n == 0) {
@@ -213,7 +213,7 @@ __global__ void k_aggregate(const uint8_t* __restrict__ sigs, uint64_t n, uint8_
 }
 
 // Shamir shares: lane i-1 evaluates share_i = sum_j poly_j i^j (Horner over Fr)
-__global__ void k_threshold_split(const uint8_t* __restrict__ secret, const uint8_t* __restrict__ tail,
+__global__ void __launch_bounds__(kBlock) k_threshold_split(const uint8_t* __restrict__ secret, const uint8_t* __restrict__ tail,
                                   uint32_t total, uint32_t threshold, uint8_t* __restrict__ out,
                                   int32_t* __restrict__ status) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -237,7 +237,7 @@ __global__ void k_threshold_split(const uint8_t* __restrict__ secret, const uint
   if (i == 0) *status = ok ? HIPBLS_OK : HIPBLS_ERR_SECRET;
 }
 
-__global__ void k_recover_secret(const uint8_t* __restrict__ shares, const uint32_t* __restrict__ ids, uint32_t n,
+__global__ void __launch_bounds__(kBlock) k_recover_secret(const uint8_t* __restrict__ shares, const uint32_t* __restrict__ ids, uint32_t n,
                                  uint8_t* __restrict__ out, int32_t* __restrict__ status) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   int st = n > 0 ? HIPBLS_OK : HIPBLS_ERR_COMBINE;
