@@ -46,6 +46,11 @@ def parse():
     ap.add_argument("--tagg-groups", type=int, default=10000, help="C3 validators per GPU (0 = skip)")
     ap.add_argument("--tagg-steps", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=16, help="oracle verifies for cpu_baseline (0 = skip)")
+    ap.add_argument("--rlc-validators", type=int, default=32768,
+                    help="C4 validators per GPU (x4 partials; 32,768 = the 1M-partial node batch / 8 GPUs; 0 = skip)")
+    ap.add_argument("--rlc-steps", type=int, default=3)
+    ap.add_argument("--rlc-big-validators", type=int, default=262144,
+                    help="also time one GPU on the whole C4 node batch (262,144 x 4 = 1M partials; 0 = skip)")
     return ap.parse_args()
 
 
@@ -99,6 +104,35 @@ def make_c3(impl, groups, rng, t=7, n=10):
     dv_pks, st = impl.secret_to_public_key_batch([s.to_bytes(32, "big") for s in secrets_])
     assert set(st) == {0}
     return psigs, part_ids, offs, dv_pks, roots
+
+
+def make_c4(impl, n_dv, rng, shared_roots=0, shares=4, nkeys=4096):
+    """C4 shard: n_dv validators x `shares` partials, items grouped by validator.  One root per
+    validator (variant i) or `shared_roots` committee roots (variant ii).  1% corrupted."""
+    n = n_dv * shares
+    sks = [rng.randrange(1, R_ORDER).to_bytes(32, "big") for _ in range(nkeys)]
+    keys, st = impl.secret_to_public_key_batch(sks)
+    assert set(st) == {0}
+    if shared_roots:
+        roots = [rng.randbytes(32) for _ in range(shared_roots)]
+        dv_root = [d * shared_roots // n_dv for d in range(n_dv)]  # contiguous committees
+    else:
+        roots = [rng.randbytes(32) for _ in range(n_dv)]
+        dv_root = list(range(n_dv))
+    owner = [rng.randrange(nkeys) for _ in range(n)]
+    midx = [dv_root[i // shares] for i in range(n)]
+    sigs, st = impl.sign_batch([sks[o] for o in owner], [roots[m] for m in midx])
+    assert set(st) == {0}
+    pks = [keys[o] for o in owner]
+    bad = sorted(rng.sample(range(n), max(1, n // 100)))
+    for j, i in enumerate(bad):
+        if j % 2 == 0:  # swapped share
+            pks[i] = keys[(owner[i] + 1) % nkeys]
+        else:           # flipped bit in the signature
+            s = bytearray(sigs[i])
+            s[40] ^= 0x04
+            sigs[i] = bytes(s)
+    return pks, sigs, midx, roots, set(bad)
 
 
 def cpu_baseline(n_sample, rng):
@@ -235,6 +269,66 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         tagg = G * args.tagg_steps * world / float(tt.item())
 
+    # ---- C4: random-linear-combination BatchVerify of this rank's shard (extra fields)
+    rlc = {}
+    if args.rlc_validators > 0:
+        variants = [("i_root_per_validator", args.rlc_validators, 0),
+                    ("ii_committee_roots", args.rlc_validators, max(1, args.rlc_validators // 128))]
+        if args.rlc_big_validators > 0:
+            variants.append(("i_node_batch_on_each_gpu", args.rlc_big_validators, 0))
+        for variant, n_dv, shared in variants:
+            t0 = time.time()
+            pks4, sigs4, midx4, roots4, bad4 = make_c4(impl, n_dv, rng, shared_roots=shared)
+            n4 = len(pks4)
+            log("rank %d: C4(%s) data (%d items, %d roots) in %.1fs" % (rank, variant, n4, len(roots4), time.time() - t0))
+            d_pk4 = torch.frombuffer(bytearray(b"".join(pks4)), dtype=torch.uint8).to(dev)
+            d_sig4 = torch.frombuffer(bytearray(b"".join(sigs4)), dtype=torch.uint8).to(dev)
+            d_midx4 = torch.tensor(midx4, dtype=torch.int32).to(dev)
+            d_msg4 = torch.frombuffer(bytearray(b"".join(roots4)), dtype=torch.uint8).to(dev)
+            d_off4 = torch.arange(0, 32 * (len(roots4) + 1), 32, dtype=torch.int64).to(dev)
+            d_st4 = torch.full((n4,), -7, dtype=torch.int32, device=dev)
+            seed = os.urandom(32)
+
+            def rstep():
+                rc = lib.hipbls_batch_verify_rlc_device(d_pk4.data_ptr(), d_sig4.data_ptr(), d_midx4.data_ptr(), n4,
+                                                        d_msg4.data_ptr(), d_off4.data_ptr(), len(roots4), seed,
+                                                        d_st4.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+                if rc != 0:
+                    raise RuntimeError("hipbls_batch_verify_rlc_device rc=%d" % rc)
+
+            rstep()
+            torch.cuda.synchronize(dev)
+            lib.hipbls_kernel_timing_reset()
+            barrier()
+            torch.cuda.synchronize(dev)
+            ts = time.perf_counter()
+            for _ in range(args.rlc_steps):
+                rstep()
+            torch.cuda.synchronize(dev)
+            barrier()
+            tel = time.perf_counter() - ts
+            st4 = d_st4.cpu().tolist()
+            assert {i for i, x in enumerate(st4) if x != 0} == bad4, "RLC bitmap mismatch"
+            w = ctypes.c_uint64()
+            wf = ctypes.c_uint64()
+            fb = ctypes.c_uint64()
+            lib.hipbls_rlc_stats(ctypes.byref(w), ctypes.byref(wf), ctypes.byref(fb))
+            kms = {}
+            for k in ("rlc_items", "rlc_hash", "rlc_window", "rlc_fallback"):
+                a = ctypes.c_double()
+                c = ctypes.c_uint64()
+                lib.hipbls_kernel_timing(k.encode(), ctypes.byref(a), ctypes.byref(c))
+                kms[k] = round(a.value, 3)
+            tt = torch.tensor([tel], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            rlc[variant] = {"verified_partial_sigs_per_s": round(n4 * args.rlc_steps * world / float(tt.item()), 1),
+                            "items_per_gpu": n4, "distinct_roots_per_gpu": len(roots4),
+                            "ms_per_batch": round(1000 * float(tt.item()) / args.rlc_steps, 3),
+                            "windows": w.value, "windows_failed": wf.value, "items_fallback": fb.value,
+                            "kernel_avg_ms": kms}
+            del d_pk4, d_sig4, d_midx4, d_msg4, d_off4, d_st4
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -258,6 +352,13 @@ def main():
             "threshold_aggregate_workload": "C3: %d validators x 7-of-10 Lagrange in G2 + Verify of each aggregate per GPU"
                                             % args.tagg_groups if tagg else None,
         }
+        if rlc:
+            out["rlc_batch_verify"] = dict(rlc, workload="C4 (BASELINE configs[3]): validators x 4 partials per GPU, "
+                                                        "items grouped by validator, 1%% corrupted (swapped share / "
+                                                        "flipped sig bit), windows of 8 items, per-item bitmap == "
+                                                        "tbls.Verify; i/ii = the 1M-partial node batch sharded over 8 "
+                                                        "GPUs (%d validators per GPU), node_batch = all 1M on every GPU"
+                                                        % args.rlc_validators)
         k_ms = avg_ms.value
         if k_ms > 0:
             achieved = FPMUL_PER_VERIFY * MADS_PER_FPMUL * n / (k_ms * 1e-3) / 1e12

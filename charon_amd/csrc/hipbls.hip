@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <map>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -14,6 +15,7 @@
 #include <vector>
 
 #include "ops.h"
+#include "rlc.h"
 
 using namespace bls;
 
@@ -271,6 +273,60 @@ __global__ void __launch_bounds__(kBlock) k_recover_secret(const uint8_t* __rest
   *status = st;
 }
 
+
+// ---------------------------------------------------------------- RLC BatchVerify (rlc.h)
+// The four stages run per sub-batch (a contiguous, window-aligned item range) so that several
+// sub-batches' stages overlap on separate streams (launch_rlc).
+// Stage 1: one lane per item -> status (final or RLC_PENDING), [r_i] pk_i and [r_i] sig_i in SoA.
+__global__ void __launch_bounds__(kBlock) k_rlc_items(uint64_t i0, uint64_t i1, const uint8_t* __restrict__ pks,
+                                                      const uint8_t* __restrict__ sigs,
+                                                      const uint32_t* __restrict__ msg_idx, uint64_t n,
+                                                      uint64_t n_msgs, rlc_seed seed, uint32_t* __restrict__ rpk,
+                                                      uint32_t* __restrict__ rsig, int32_t* __restrict__ status) {
+  const uint64_t i = i0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < i1) rlc_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk, rsig, status);
+}
+
+// Stage 2: one lane per distinct message -> H(m) in affine SoA (48 words).
+__global__ void __launch_bounds__(kBlock) k_rlc_hash(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offs,
+                                                     uint64_t n_msgs, uint32_t* __restrict__ H) {
+  const uint64_t m = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (m < n_msgs) rlc_hash_lane(m, msgs, offs, n_msgs, H);
+}
+
+// Stage 3: one lane per window of RLC_W items -> one multi-pairing check.  The items a failed window
+// leaves pending are appended to this sub-batch's fallback list (one atomic per failed window), so
+// stage 4 runs on a dense list instead of waking a wave for every scattered pending item.
+__global__ void __launch_bounds__(kBlock) k_rlc_window(uint64_t w0, uint64_t w1, uint64_t n,
+                                                       const uint32_t* __restrict__ msg_idx,
+                                                       const uint32_t* __restrict__ rpk,
+                                                       const uint32_t* __restrict__ rsig,
+                                                       const uint32_t* __restrict__ H, uint64_t n_msgs,
+                                                       int32_t* __restrict__ status, int32_t* __restrict__ win_fail,
+                                                       uint32_t* __restrict__ list, uint32_t* __restrict__ list_len) {
+  const uint64_t w = w0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (w >= w1) return;
+  const int left = rlc_window_lane(w, n, msg_idx, rpk, rsig, H, n_msgs, status, win_fail);
+  if (left == 0) return;
+  uint32_t at = atomicAdd(list_len, (uint32_t)left);
+  const uint64_t i1 = w * RLC_W + RLC_W < n ? w * RLC_W + RLC_W : n;
+  for (uint64_t i = w * RLC_W; i < i1; ++i)
+    if (status[i] == RLC_PENDING) list[at++] = (uint32_t)i;
+}
+
+// Stage 4: items of failed windows (dense list) are checked one by one (rlc_fallback_lane).
+__global__ void __launch_bounds__(kBlock) k_rlc_fallback(const uint32_t* __restrict__ list,
+                                                         const uint32_t* __restrict__ list_len, uint64_t cap,
+                                                         const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
+                                                         const uint32_t* __restrict__ msg_idx,
+                                                         const uint32_t* __restrict__ H, uint64_t n_msgs,
+                                                         int32_t* __restrict__ status) {
+  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t len = *list_len;
+  if (j >= len || j >= cap) return;
+  rlc_fallback_lane(list[j], pks, sigs, msg_idx, H, n_msgs, status);
+}
+
 // ============================================================================ host runtime
 thread_local std::string g_last_error;
 
@@ -300,7 +356,14 @@ struct Context {
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevBuf b_pk, b_msg, b_off, b_sig, b_st, b_out, b_ids, b_pts, b_pst, b_aux;
-  TimingSlot verify_timing;
+  DevBuf r_pk, r_sig, r_h, r_win, r_midx, r_list, r_cnt;  // RLC BatchVerify workspaces
+  // RLC sub-batches in flight.  The process gets GPU_MAX_HW_QUEUES = 4 hardware queues: the caller's
+  // stream (which also hashes the messages) + 3 sub-batch streams, so no two streams share a queue.
+  static constexpr int kSub = 3;
+  hipStream_t sub[kSub] = {};
+  hipEvent_t ev_fork = nullptr, ev_hash = nullptr, ev_join[kSub] = {};
+  uint64_t r_windows = 0;                  // window count of the last RLC call (hipbls_rlc_stats)
+  std::map<std::string, TimingSlot> timing;  // per kernel name: HIP events on the launch stream
   bool timing_enabled = true;
 };
 
@@ -347,23 +410,122 @@ void drain_timing(TimingSlot& t) {
   t.pending.clear();
 }
 
-int launch_verify(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_offs, const uint8_t* d_sigs,
-                  uint64_t n, int32_t* d_status, hipStream_t s) {
-  if (n == 0) return HIPBLS_OK;
+// Brackets one kernel launch with HIP events on its stream (bench.py roofline: the average
+// duration per launch is read back through hipbls_kernel_timing).
+template <class Launch>
+int timed(const char* name, hipStream_t s, Launch launch) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (g_ctx.timing_enabled) {
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, s));
   }
-  hipLaunchKernelGGL(k_verify_fused, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs,
-                     n, d_status);
+  launch();
   HIP_TRY(hipGetLastError());
   if (g_ctx.timing_enabled) {
     HIP_TRY(hipEventRecord(e1, s));
-    g_ctx.verify_timing.pending.emplace_back(e0, e1);
-    if (g_ctx.verify_timing.pending.size() > 256) drain_timing(g_ctx.verify_timing);
+    TimingSlot& t = g_ctx.timing[name];
+    t.pending.emplace_back(e0, e1);
+    if (t.pending.size() > 256) drain_timing(t);
   }
+  return HIPBLS_OK;
+}
+
+int launch_verify(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_offs, const uint8_t* d_sigs,
+                  uint64_t n, int32_t* d_status, hipStream_t s) {
+  if (n == 0) return HIPBLS_OK;
+  return timed("verify", s, [&] {
+    hipLaunchKernelGGL(k_verify_fused, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs,
+                       n, d_status);
+  });
+}
+
+int ensure_rlc_streams() {
+  Context& c = g_ctx;
+  if (c.ev_fork) return HIPBLS_OK;
+  for (int k = 0; k < Context::kSub; ++k) HIP_TRY(hipStreamCreateWithFlags(&c.sub[k], hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&c.ev_hash, hipEventDisableTiming));
+  for (int k = 0; k < Context::kSub; ++k) HIP_TRY(hipEventCreateWithFlags(&c.ev_join[k], hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
+  return HIPBLS_OK;
+}
+
+// RLC BatchVerify: the batch is cut into up to kSub window-aligned sub-batches, each running
+// items -> window -> fallback on its own stream, while the distinct messages are hashed on the
+// caller's stream; windows wait only for the hash.  Every stage is latency-bound on its own (one lane per item
+// at one wave per SIMD), so overlapping the sub-batches' stages is what fills the CUs.  The caller's
+// stream `s` forks into the sub-streams and joins back, so the call stays stream-ordered.
+int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n, const uint8_t* d_msgs,
+               const uint64_t* d_offs, uint64_t n_msgs, const uint8_t* seed32, int32_t* d_status, hipStream_t s) {
+  Context& c = g_ctx;
+  c.r_windows = 0;
+  if (n == 0) return HIPBLS_OK;
+  if (n > 0xffffffffull) return HIPBLS_ERR_ARG;  // fallback list holds 32-bit item indices
+  int rc = ensure_rlc_streams();
+  if (rc) return rc;
+  rlc_seed seed;
+  for (int k = 0; k < 8; ++k)
+    seed.w[k] = (uint32_t)seed32[4 * k] << 24 | (uint32_t)seed32[4 * k + 1] << 16 | (uint32_t)seed32[4 * k + 2] << 8 |
+                (uint32_t)seed32[4 * k + 3];
+  const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
+  HIP_TRY(c.r_pk.ensure(n * 36 * 4));
+  HIP_TRY(c.r_sig.ensure(n * 72 * 4));
+  HIP_TRY(c.r_h.ensure((n_msgs ? n_msgs : 1) * 48 * 4));
+  HIP_TRY(c.r_win.ensure(n_win * 4));
+  HIP_TRY(c.r_list.ensure(n * 4));
+  HIP_TRY(c.r_cnt.ensure(Context::kSub * 4));
+  uint32_t* rpk = (uint32_t*)c.r_pk.p;
+  uint32_t* rsig = (uint32_t*)c.r_sig.p;
+  uint32_t* H = (uint32_t*)c.r_h.p;
+  int32_t* win = (int32_t*)c.r_win.p;
+  uint32_t* list = (uint32_t*)c.r_list.p;
+  uint32_t* cnt = (uint32_t*)c.r_cnt.p;
+  // sub-batches of whole windows; small batches stay in one
+  const uint64_t min_win = 2048;
+  int nsub = (int)((n_win + min_win - 1) / min_win);
+  if (nsub > Context::kSub) nsub = Context::kSub;
+  if (nsub < 1) nsub = 1;
+  const uint64_t win_per = (n_win + nsub - 1) / nsub;
+
+  HIP_TRY(hipMemsetAsync(cnt, 0, Context::kSub * 4, s));
+  HIP_TRY(hipEventRecord(c.ev_fork, s));
+  hipStream_t hs = s;
+  if (n_msgs) {
+    rc = timed("rlc_hash", hs, [&] {
+      hipLaunchKernelGGL(k_rlc_hash, dim3((unsigned)grid_for(n_msgs)), dim3(kBlock), 0, hs, d_msgs, d_offs, n_msgs, H);
+    });
+    if (rc) return rc;
+  }
+  HIP_TRY(hipEventRecord(c.ev_hash, hs));
+  for (int k = 0; k < nsub; ++k) {
+    hipStream_t ss = c.sub[k];
+    const uint64_t w0 = win_per * k, w1 = w0 + win_per < n_win ? w0 + win_per : n_win;
+    if (w0 >= w1) continue;
+    const uint64_t i0 = w0 * RLC_W, i1 = w1 * RLC_W < n ? w1 * RLC_W : n;
+    HIP_TRY(hipStreamWaitEvent(ss, c.ev_fork, 0));
+    rc = timed("rlc_items", ss, [&] {
+      hipLaunchKernelGGL(k_rlc_items, dim3((unsigned)grid_for(i1 - i0)), dim3(kBlock), 0, ss, i0, i1, d_pks, d_sigs,
+                         d_midx, n, n_msgs, seed, rpk, rsig, d_status);
+    });
+    if (rc) return rc;
+    HIP_TRY(hipStreamWaitEvent(ss, c.ev_hash, 0));
+    rc = timed("rlc_window", ss, [&] {
+      hipLaunchKernelGGL(k_rlc_window, dim3((unsigned)grid_for(w1 - w0)), dim3(kBlock), 0, ss, w0, w1, n, d_midx,
+                         (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)H, n_msgs, d_status, win,
+                         list + i0, cnt + k);
+    });
+    if (rc) return rc;
+    // the list length is only known on the device: launch for the worst case, idle lanes exit
+    rc = timed("rlc_fallback", ss, [&] {
+      hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(i1 - i0)), dim3(kBlock), 0, ss,
+                         (const uint32_t*)(list + i0), (const uint32_t*)(cnt + k), i1 - i0, d_pks, d_sigs, d_midx,
+                         (const uint32_t*)H, n_msgs, d_status);
+    });
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c.ev_join[k], ss));
+    HIP_TRY(hipStreamWaitEvent(s, c.ev_join[k], 0));
+  }
+  c.r_windows = n_win;
   return HIPBLS_OK;
 }
 
@@ -674,18 +836,95 @@ int hipbls_recover_secret(const uint8_t* shares, const uint32_t* ids, uint32_t n
 int hipbls_kernel_timing(const char* name, double* avg_ms, uint64_t* launches) {
   if (!name || !avg_ms || !launches) return HIPBLS_ERR_ARG;
   std::lock_guard<std::mutex> lk(g_ctx.mu);
-  if (std::strcmp(name, "verify") != 0) return HIPBLS_ERR_ARG;
-  drain_timing(g_ctx.verify_timing);
-  *launches = g_ctx.verify_timing.launches;
-  *avg_ms = g_ctx.verify_timing.launches ? g_ctx.verify_timing.total_ms / g_ctx.verify_timing.launches : 0.0;
+  auto it = g_ctx.timing.find(name);
+  if (it == g_ctx.timing.end()) {
+    *launches = 0;
+    *avg_ms = 0.0;
+    return HIPBLS_OK;
+  }
+  TimingSlot& t = it->second;
+  drain_timing(t);
+  *launches = t.launches;
+  *avg_ms = t.launches ? t.total_ms / t.launches : 0.0;
   return HIPBLS_OK;
 }
 
 int hipbls_kernel_timing_reset(void) {
   std::lock_guard<std::mutex> lk(g_ctx.mu);
-  drain_timing(g_ctx.verify_timing);
-  g_ctx.verify_timing.total_ms = 0;
-  g_ctx.verify_timing.launches = 0;
+  for (auto& kv : g_ctx.timing) {
+    drain_timing(kv.second);
+    kv.second.total_ms = 0;
+    kv.second.launches = 0;
+  }
+  return HIPBLS_OK;
+}
+
+int hipbls_batch_verify_rlc(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
+                            const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs, const uint8_t* seed32,
+                            int32_t* status) {
+  if (n == 0) return HIPBLS_OK;
+  if (!pks || !sigs || !msg_idx || !msg_offsets || !seed32 || !status || mul_overflows(n, 288)) return HIPBLS_ERR_ARG;
+  for (uint64_t i = 0; i < n; ++i)
+    if (msg_idx[i] >= n_msgs) {
+      g_last_error = "message index out of range";
+      return HIPBLS_ERR_ARG;
+    }
+  for (uint64_t m = 0; m < n_msgs; ++m)
+    if (msg_offsets[m + 1] < msg_offsets[m] || msg_offsets[m + 1] - msg_offsets[m] > 0xffffffffull)
+      return HIPBLS_ERR_ARG;
+  const uint64_t msg_total = msg_offsets[n_msgs];
+  if (msg_total && !msgs) return HIPBLS_ERR_ARG;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  Context& c = g_ctx;
+  HIP_TRY(c.b_pk.ensure(n * 48));
+  HIP_TRY(c.b_sig.ensure(n * 96));
+  HIP_TRY(c.r_midx.ensure(n * 4));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_off.ensure((n_msgs + 1) * 8));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.r_midx.p, msg_idx, n * 4, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n_msgs + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  rc = launch_rlc((const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_sig.p, (const uint32_t*)c.r_midx.p, n,
+                  (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p, n_msgs, seed32, (int32_t*)c.b_st.p, c.stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int hipbls_batch_verify_rlc_device(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_msg_idx, uint64_t n,
+                                   const uint8_t* d_msgs, const uint64_t* d_msg_offsets, uint64_t n_msgs,
+                                   const uint8_t* seed32, int32_t* d_status, void* stream) {
+  if (n == 0) return HIPBLS_OK;
+  if (!seed32 || mul_overflows(n, 288)) return HIPBLS_ERR_ARG;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  return launch_rlc(d_pks, d_sigs, d_msg_idx, n, d_msgs, d_msg_offsets, n_msgs, seed32, d_status,
+                    stream ? (hipStream_t)stream : g_ctx.stream);
+}
+
+int hipbls_rlc_stats(uint64_t* windows, uint64_t* windows_failed, uint64_t* items_fallback) {
+  if (!windows || !windows_failed || !items_fallback) return HIPBLS_ERR_ARG;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  Context& c = g_ctx;
+  *windows = c.r_windows;
+  *windows_failed = 0;
+  *items_fallback = 0;
+  if (c.r_windows == 0) return HIPBLS_OK;
+  std::vector<int32_t> v(c.r_windows);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(v.data(), c.r_win.p, v.size() * 4, hipMemcpyDeviceToHost));
+  for (int32_t x : v)
+    if (x > 0) {
+      *windows_failed += 1;
+      *items_fallback += (uint64_t)x;
+    }
   return HIPBLS_OK;
 }
 

@@ -1,0 +1,285 @@
+// Random-linear-combination BatchVerify (BASELINE configs[3]): the per-lane
+// stages behind hipbls_batch_verify_rlc, written once for the HIP kernels and the host test build.
+//
+// Semantics: status[i] is exactly what tbls.Herumi.Verify (/root/reference/tbls/herumi.go:285-301)
+// returns for item i.  Items are checked in windows of RLC_W consecutive items; a window passes
+// when, with per-item 64-bit random scalars r_i,
+//     prod_m e( sum_{i in window, msg i = m} r_i pk_i , H(m) ) * e( -g1 , sum_{i in window} r_i sig_i ) == 1
+// (one multi-Miller loop, one final exponentiation per window).  Every sig and pk is decoded and
+// subgroup-checked individually first, so a window that passes is valid item by item except with
+// probability <= 2^-64 (standard small-exponent batch verification).  Items of a window that fails
+// are re-verified individually (op_verify), so the bitmap never depends on the random scalars.
+//
+// Scalars: r_i = a_i + b_i * x  (x the BLS parameter, a_i, b_i uniform 32-bit) taken from
+// SHA-256(seed || i).  The 2^64 values are distinct mod r, which is all the soundness argument
+// needs, and both sides get the multiplication at half length through the endomorphisms:
+//   G2: [r] sig = [a] sig + [b] psi(sig)       (psi = [x] on G2, curve.h g2_in_subgroup)
+//   G1: [r] pk  = [a] pk  + [b] ([x] pk)       ([x] pk is the first half of the G1 subgroup test)
+#pragma once
+#include "ops.h"
+
+namespace bls {
+
+#ifndef RLC_W
+#define RLC_W 8  // items per verdict window
+#endif
+constexpr int RLC_PENDING = -1;  // internal status: decoded fine, verdict not yet known
+
+struct rlc_seed {
+  uint32_t w[8];  // 32 seed bytes as big-endian words
+};
+
+// (a, b) = first 8 bytes of SHA-256(seed || be64(i))
+BLS_HD BLS_INLINE void rlc_scalars(uint32_t& a, uint32_t& b, const rlc_seed& seed, uint64_t i) {
+  uint32_t w[16];
+  for (int k = 0; k < 8; ++k) w[k] = seed.w[k];
+  w[8] = (uint32_t)(i >> 32);
+  w[9] = (uint32_t)i;
+  w[10] = 0x80000000u;
+  for (int k = 11; k < 15; ++k) w[k] = 0;
+  w[15] = 40 * 8;
+  sha256_state s;
+  sha256_init(s);
+  sha256_compress(s, w);
+  a = s.h[0];
+  b = s.h[1];
+}
+
+// ---- SoA (limb-major) point storage: word k of element i at base[k * stride + i] -----------
+template <int WORDS>
+BLS_HD BLS_INLINE void soa_store(uint32_t* base, uint64_t stride, uint64_t i, const uint32_t* src) {
+  for (int k = 0; k < WORDS; ++k) base[(uint64_t)k * stride + i] = src[k];
+}
+template <int WORDS>
+BLS_HD BLS_INLINE void soa_load(uint32_t* dst, const uint32_t* base, uint64_t stride, uint64_t i) {
+  for (int k = 0; k < WORDS; ++k) dst[k] = base[(uint64_t)k * stride + i];
+}
+
+// [a] P + [b] Q with one shared doubling chain (Shamir's trick), 32-bit a, b
+template <class F>
+BLS_HD BLS_CALL void jac_mul2_u32(jac<F>& r, const jac<F>& P, const jac<F>& Q, uint32_t a, uint32_t b) {
+  jac<F> PQ, acc, addend;
+  jac_add(PQ, P, Q);
+  jac_set_inf(acc);
+  for (int bit = 31; bit >= 0; --bit) {
+    jac_dbl(acc, acc);
+    const uint32_t d = ((a >> bit) & 1u) | (((b >> bit) & 1u) << 1);
+    addend = d == 1 ? P : (d == 2 ? Q : PQ);
+    if (d) jac_add(acc, acc, addend);
+  }
+  r = acc;
+}
+
+// G1 decode with the subgroup test (phi(P) = [-x^2] P, as g1_in_subgroup) that also hands back
+// [x] P, the half-way point of that test.
+BLS_HD BLS_CALL int g1_decompress_keep_x(g1a& out, g1j& xP, const uint8_t* b) {
+  const int st = g1_decompress(out, b, false);
+  if (st != DEC_OK) return st;
+  g1j p, q, q2, phi;
+  jac_from_aff(p, out);
+  jac_mul_u64(q, p, X_ABS);   // [|x|] P
+  jac_mul_u64(q2, q, X_ABS);  // [x^2] P
+  fp_mul(phi.x, p.x, FP_BETA);
+  fp_neg(phi.y, p.y);
+  phi.z = p.z;
+  if (!jac_eq(q2, phi)) return DEC_BAD;
+  jac_neg(xP, q);  // x < 0
+  return DEC_OK;
+}
+
+// Stage 1, one lane per item: decode + subgroup-check pk and sig in herumi's order, then store
+// [r_i] pk_i (G1 Jacobian, 36 words) and [r_i] sig_i (G2 Jacobian, 72 words).  Items that already
+// have their final status (bad encoding, infinity) store the point at infinity.
+BLS_HD BLS_CALL int rlc_item(const uint8_t* pk48, const uint8_t* sig96, const rlc_seed& seed, uint64_t i,
+                             uint32_t* rpk36, uint32_t* rsig72) {
+  g1j rp;
+  g2j rs;
+  jac_set_inf(rp);
+  jac_set_inf(rs);
+  g1a pk;
+  g1j xpk;
+  int st = RLC_PENDING;
+  const int dp = g1_decompress_keep_x(pk, xpk, pk48);
+  if (dp == DEC_BAD) st = HIPBLS_ERR_PUBKEY;
+  g2a sig;
+  if (st == RLC_PENDING) {
+    const int ds = g2_decompress(sig, sig96, true);
+    if (ds == DEC_BAD)
+      st = HIPBLS_ERR_SIGNATURE;
+    else if (dp == DEC_INF || ds == DEC_INF)
+      st = HIPBLS_ERR_VERIFY;  // KeyValidate rejects the identity key; e(pk, H) != e(g1, O)
+  }
+  if (st == RLC_PENDING) {
+    uint32_t a, b;
+    rlc_scalars(a, b, seed, i);
+    g1j pj;
+    jac_from_aff(pj, pk);
+    jac_mul2_u32(rp, pj, xpk, a, b);
+    g2j sj, psj;
+    jac_from_aff(sj, sig);
+    g2_psi(psj, sj);  // = [x] sig for sig in G2 (checked above)
+    jac_mul2_u32(rs, sj, psj, a, b);
+  }
+  const uint32_t* p = &rp.x.v[0];
+  for (int k = 0; k < 36; ++k) rpk36[k] = p[k];
+  const uint32_t* s = &rs.x.c0.v[0];
+  for (int k = 0; k < 72; ++k) rsig72[k] = s[k];
+  return st;
+}
+
+// Multi-Miller loop over up to MAXN pairs with one shared Fp12 squaring chain (pairing.h steps).
+template <int MAXN>
+BLS_HD BLS_CALL void miller_loop_multi(fp12& f, const g1a* P, const g2a* Q, int n) {
+  g2j T[MAXN];
+  for (int k = 0; k < n; ++k) {
+    T[k].x = Q[k].x;
+    T[k].y = Q[k].y;
+    fp2_set_one(T[k].z);
+  }
+  fp12_set_one(f);
+  fp2 g0, g1, h1;
+  for (int bit = 62; bit >= 0; --bit) {
+    if (bit != 62) fp12_sqr(f, f);
+    for (int k = 0; k < n; ++k) {
+      miller_dbl_step(T[k], g0, g1, h1, P[k].x, P[k].y);
+      fp12_mul_line(f, g0, g1, h1);
+    }
+    if ((X_ABS >> bit) & 1ull) {
+      for (int k = 0; k < n; ++k) {
+        miller_add_step(T[k], g0, g1, h1, Q[k], P[k].x, P[k].y);
+        fp12_mul_line(f, g0, g1, h1);
+      }
+    }
+  }
+  fp12_conj(f, f);
+}
+
+// Stage 3, one lane per window [i0, i1): sum the scaled keys per run of equal message index and
+// the scaled signatures over the whole window, run one multi-Miller loop + final exponentiation,
+// and return true when the window verifies (or holds no pending item).
+// Accessors are callables so the same body serves the SoA device buffers and the host test.
+template <class LoadPk, class LoadSig, class LoadH>
+BLS_HD BLS_INLINE bool rlc_window(uint64_t i0, uint64_t i1, const int32_t* status, const uint32_t* msg_idx,
+                                  LoadPk load_pk, LoadSig load_sig, LoadH load_h) {
+  g1a P[RLC_W + 1];
+  g2a Q[RLC_W + 1];
+  int np = 0;
+  g2j S;
+  jac_set_inf(S);
+  g1j run;
+  uint32_t run_msg = 0xffffffffu;
+  bool any = false;
+  for (uint64_t i = i0; i < i1; ++i) {
+    if (status[i] != RLC_PENDING) continue;
+    any = true;
+    g1j qp;
+    g2j qs;
+    load_pk(qp, i);
+    load_sig(qs, i);
+    jac_add(S, S, qs);
+    const uint32_t m = msg_idx[i];
+    if (m != run_msg) {
+      if (run_msg != 0xffffffffu && !jac_is_inf(run)) {
+        jac_to_aff(P[np], run);
+        load_h(Q[np], run_msg);
+        ++np;
+      }
+      run = qp;
+      run_msg = m;
+    } else {
+      jac_add(run, run, qp);
+    }
+  }
+  if (!any) return true;
+  if (!jac_is_inf(run)) {
+    jac_to_aff(P[np], run);
+    load_h(Q[np], run_msg);
+    ++np;
+  }
+  if (!jac_is_inf(S)) {
+    P[np].x = G1_GEN_X;
+    P[np].y = G1_NEG_GEN_Y;
+    jac_to_aff(Q[np], S);
+    ++np;
+  }
+  if (np == 0) return true;
+  fp12 f, e;
+  miller_loop_multi<RLC_W + 1>(f, P, Q, np);
+  final_exponentiation(e, f);
+  return fp12_is_one(e);
+}
+
+// ---- lane bodies of the four stages (kernels in hipbls.hip; host loop in tests/native) --------
+
+// Stage 1, item i: status (final, or RLC_PENDING) and the scaled pk / sig in SoA.
+BLS_HD BLS_INLINE void rlc_items_lane(uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
+                                      uint64_t n, uint64_t n_msgs, const rlc_seed& seed, uint32_t* rpk,
+                                      uint32_t* rsig, int32_t* status) {
+  uint32_t p[36], s[72];
+  int st;
+  if (msg_idx[i] >= n_msgs) {  // device entry point: an out-of-range message index is an argument error
+    st = HIPBLS_ERR_ARG;
+    g1j ip;
+    g2j is;
+    jac_set_inf(ip);
+    jac_set_inf(is);
+    for (int k = 0; k < 36; ++k) p[k] = (&ip.x.v[0])[k];
+    for (int k = 0; k < 72; ++k) s[k] = (&is.x.c0.v[0])[k];
+  } else {
+    st = rlc_item(pks + 48 * i, sigs + 96 * i, seed, i, p, s);
+  }
+  soa_store<36>(rpk, n, i, p);
+  soa_store<72>(rsig, n, i, s);
+  status[i] = st;
+}
+
+// Stage 2, message m: H(m) in affine SoA (48 words).
+BLS_HD BLS_INLINE void rlc_hash_lane(uint64_t m, const uint8_t* msgs, const uint64_t* offs, uint64_t n_msgs,
+                                     uint32_t* H) {
+  const uint64_t o0 = offs[m], o1 = offs[m + 1];
+  g2j hj;
+  hash_to_g2(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43);
+  g2a ha;
+  jac_to_aff(ha, hj);
+  soa_store<48>(H, n_msgs, m, &ha.x.c0.v[0]);
+}
+
+// Stage 3, window w = items [w*RLC_W, ...): on success every pending item becomes HIPBLS_OK,
+// otherwise they stay pending for stage 4.  Returns (and stores in win_fail[w]) the number of items
+// left pending: 0 when the window passed.
+BLS_HD BLS_INLINE int rlc_window_lane(uint64_t w, uint64_t n, const uint32_t* msg_idx, const uint32_t* rpk,
+                                      const uint32_t* rsig, const uint32_t* H, uint64_t n_msgs, int32_t* status,
+                                      int32_t* win_fail) {
+  const uint64_t i0 = w * RLC_W;
+  const uint64_t i1 = i0 + RLC_W < n ? i0 + RLC_W : n;
+  auto load_pk = [&](g1j& q, uint64_t i) { soa_load<36>(&q.x.v[0], rpk, n, i); };
+  auto load_sig = [&](g2j& q, uint64_t i) { soa_load<72>(&q.x.c0.v[0], rsig, n, i); };
+  auto load_h = [&](g2a& q, uint32_t m) { soa_load<48>(&q.x.c0.v[0], H, n_msgs, m); };
+  const bool ok = rlc_window(i0, i1, status, msg_idx, load_pk, load_sig, load_h);
+  int left = 0;
+  for (uint64_t i = i0; i < i1; ++i)
+    if (status[i] == RLC_PENDING) {
+      if (ok)
+        status[i] = HIPBLS_OK;
+      else
+        ++left;
+    }
+  win_fail[w] = left;
+  return left;
+}
+
+// Stage 4, item i: still pending after its window failed -> tbls.Verify of the item alone.  Both
+// points already passed decoding and the subgroup tests in stage 1 and H(m) is in the table, so this
+// is the bare pairing check: e(pk, H(m)) * e(-g1, sig) == 1 (about half of a full op_verify).
+BLS_HD BLS_INLINE void rlc_fallback_lane(uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
+                                         const uint32_t* H, uint64_t n_msgs, int32_t* status) {
+  if (status[i] != RLC_PENDING) return;
+  g1a pk;
+  g2a sig, hm;
+  g1_decompress(pk, pks + 48 * i, false);
+  g2_decompress(sig, sigs + 96 * i, false);
+  soa_load<48>(&hm.x.c0.v[0], H, n_msgs, msg_idx[i]);
+  status[i] = pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+}
+
+}  // namespace bls

@@ -74,6 +74,9 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_threshold_aggregate_batch_device": ([vp, vp, vp, u64, vp, vp, vp], ctypes.c_int),
         "hipbls_sign_batch_device": ([vp, vp, vp, u64, vp, vp, vp], ctypes.c_int),
         "hipbls_secret_to_public_key_batch_device": ([vp, u64, vp, vp, vp], ctypes.c_int),
+        "hipbls_batch_verify_rlc": ([u8p, u8p, u32p, u64, u8p, u64p, u64, u8p, i32p], ctypes.c_int),
+        "hipbls_batch_verify_rlc_device": ([vp, vp, vp, u64, vp, vp, u64, u8p, vp, vp], ctypes.c_int),
+        "hipbls_rlc_stats": ([u64p, u64p, u64p], ctypes.c_int),
         "hipbls_kernel_timing": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), u64p], ctypes.c_int),
         "hipbls_kernel_timing_reset": ([], ctypes.c_int),
     }
@@ -93,6 +96,7 @@ def exported_symbols() -> List[str]:
         "hipbls_threshold_split", "hipbls_recover_secret", "hipbls_verify_batch_device",
         "hipbls_threshold_aggregate_batch_device", "hipbls_sign_batch_device",
         "hipbls_secret_to_public_key_batch_device", "hipbls_kernel_timing", "hipbls_kernel_timing_reset",
+        "hipbls_batch_verify_rlc", "hipbls_batch_verify_rlc_device", "hipbls_rlc_stats",
     ]
 
 
@@ -230,6 +234,42 @@ class HipBLS:
     def batch_verify(self, pks, msgs, sigs) -> List[Optional[TBLSError]]:
         """Per-item outcome of Verify: None when valid, else the TBLSError Verify would raise."""
         return [None if s == OK else TBLSError(VERIFY_ERRORS[s]) for s in self.batch_verify_status(pks, msgs, sigs)]
+
+    def batch_verify_rlc_status(self, pks: Sequence[bytes], msgs: Sequence[bytes], sigs: Sequence[bytes],
+                                seed: Optional[bytes] = None) -> List[int]:
+        """Random-linear-combination BatchVerify: same per-item statuses as batch_verify_status.
+        Items sharing a message (all partials of one validator) should be adjacent; the distinct
+        messages are hashed once.  seed: 32 bytes of CSPRNG output (drawn here when omitted)."""
+        n = len(pks)
+        if not (len(msgs) == n == len(sigs)):
+            raise ValueError("mismatching lengths")
+        if any(len(p) != 48 for p in pks) or any(len(s) != 96 for s in sigs):
+            raise ValueError("bad key/signature length")
+        if seed is None:
+            seed = secrets.token_bytes(32)
+        if len(seed) != 32:
+            raise ValueError("seed must be 32 bytes")
+        pos: Dict[bytes, int] = {}
+        table: List[bytes] = []
+        idx = (ctypes.c_uint32 * max(n, 1))()
+        for i, m in enumerate(msgs):
+            m = bytes(m)
+            j = pos.get(m)
+            if j is None:
+                j = pos[m] = len(table)
+                table.append(m)
+            idx[i] = j
+        blob, offs = _offsets(table)
+        st = _status_array(n)
+        _check(self.lib.hipbls_batch_verify_rlc(b"".join(pks), b"".join(sigs), idx, n, blob, offs, len(table), seed,
+                                                st), self.lib)
+        return [st[i] for i in range(n)]
+
+    def rlc_stats(self) -> Tuple[int, int, int]:
+        """(windows, windows that failed the batched check, items re-verified one by one) of the last RLC call."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self.lib.hipbls_rlc_stats(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), self.lib)
+        return a.value, b.value, c.value
 
     def threshold_aggregate(self, partial_signatures_by_index: Mapping[int, bytes]) -> bytes:
         """herumi.go:244-283."""

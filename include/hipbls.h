@@ -15,6 +15,9 @@
  *   hipbls_aggregate                   tbls.Implementation.Aggregate         tbls/tbls.go:65-67, tbls/herumi.go:220-242
  *   hipbls_threshold_split             tbls.Implementation.ThresholdSplit[Insecure] tbls/tbls.go:40-47, tbls/herumi.go:84-181
  *   hipbls_recover_secret              tbls.Implementation.RecoverSecret     tbls/tbls.go:49, tbls/herumi.go:183-218
+ *   hipbls_batch_verify_rlc            many tbls.Verify calls at once: the per-item loops of
+ *                                      core/parsigex/parsigex.go:139-163, core/validatorapi/validatorapi.go:246-283,
+ *                                      core/sigagg/sigagg.go:138-159 (optional BatchVerifier extension)
  * Underneath, these replace herumi's cgo entry points blsVerify / blsSignatureRecover /
  * blsSign / blsGetPublicKey / blsFastAggregateVerify / blsAggregateSignature
  * (github.com/herumi/bls-eth-go-binary v1.32.1, imported at tbls/herumi.go:12).
@@ -45,7 +48,7 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 1
+#define HIPBLS_ABI_VERSION 2
 int hipbls_abi_version(void);
 
 /* Select the HIP device used by the calling process (one process per GPU); idempotent.
@@ -96,6 +99,21 @@ int hipbls_threshold_split(const uint8_t* secret, const uint8_t* poly_tail, uint
 int hipbls_recover_secret(const uint8_t* shares, const uint32_t* ids, uint32_t n, uint8_t* out_secret,
                           int32_t* status);
 
+/* Random-linear-combination BatchVerify.  Item i is (pks[48 i..], message msg_idx[i], sigs[96 i..]);
+ * message m is msgs[msg_offsets[m] .. msg_offsets[m+1]) (n_msgs distinct messages, each hashed once).
+ * status[i] is exactly hipbls_verify_batch's (i.e. tbls.Verify's) outcome for the item: items are
+ * decoded and subgroup-checked one by one, windows of consecutive items are checked with one
+ * multi-pairing under 64-bit random scalars derived from seed32 (32 bytes the caller draws from a
+ * CSPRNG), and the items of a window that fails are re-verified individually.  Items sharing a
+ * message should be adjacent (e.g. all partials of one validator): each run of equal msg_idx inside
+ * a window costs one Miller loop.  HIPBLS_ERR_ARG when a msg_idx is out of range. */
+int hipbls_batch_verify_rlc(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
+                            const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs, const uint8_t* seed32,
+                            int32_t* status);
+/* Windows checked, windows that failed, and items re-verified one by one in the last RLC call
+ * (synchronizes the device). */
+int hipbls_rlc_stats(uint64_t* windows, uint64_t* windows_failed, uint64_t* items_fallback);
+
 /* ------------------------------------------- device-resident variants (inputs already in HBM) ---- */
 /* Same semantics; every pointer is a device pointer; work is enqueued on `stream` (a hipStream_t,
  * NULL = the library's stream) and the call returns without synchronizing. */
@@ -109,8 +127,15 @@ int hipbls_sign_batch_device(const uint8_t* d_sks, const uint8_t* d_msgs, const 
 int hipbls_secret_to_public_key_batch_device(const uint8_t* d_sks, uint64_t n, uint8_t* d_out_pks,
                                              int32_t* d_status, void* stream);
 
-/* Average duration (ms) of the dominant verify kernel over the calls since the last reset,
- * measured with HIP events on the stream it runs on (bench.py roofline). */
+/* As hipbls_batch_verify_rlc; seed32 is a host pointer.  An out-of-range msg_idx[i] yields
+ * status[i] = HIPBLS_ERR_ARG. */
+int hipbls_batch_verify_rlc_device(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_msg_idx, uint64_t n,
+                                   const uint8_t* d_msgs, const uint64_t* d_msg_offsets, uint64_t n_msgs,
+                                   const uint8_t* seed32, int32_t* d_status, void* stream);
+
+/* Average duration (ms) per launch of a kernel over the calls since the last reset, measured with HIP
+ * events on the stream it runs on (bench.py roofline).  Names: "verify" (k_verify_fused),
+ * "rlc_items", "rlc_hash", "rlc_window", "rlc_fallback". */
 int hipbls_kernel_timing(const char* name, double* avg_ms, uint64_t* launches);
 int hipbls_kernel_timing_reset(void);
 

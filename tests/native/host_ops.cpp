@@ -232,3 +232,47 @@ void ht_get_counts(uint64_t* out2) {
 }
 
 }  // extern "C"
+
+// ---- RLC BatchVerify: the four kernel stages of charon_amd/csrc/rlc.h run lane by lane ----------
+#include "../../charon_amd/csrc/rlc.h"
+#include <vector>
+
+extern "C" int ht_rlc_verify(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
+                             const uint8_t* msgs, const uint64_t* offs, uint64_t n_msgs, const uint8_t* seed32,
+                             int32_t* status, uint64_t* stats3, uint64_t* counts4) {
+  // counts4 (optional): Fp products (mul + sqr) spent in each of the four stages
+  rlc_seed seed;
+  for (int k = 0; k < 8; ++k)
+    seed.w[k] = (uint32_t)seed32[4 * k] << 24 | (uint32_t)seed32[4 * k + 1] << 16 | (uint32_t)seed32[4 * k + 2] << 8 |
+                (uint32_t)seed32[4 * k + 3];
+  const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
+  std::vector<uint32_t> rpk(n * 36), rsig(n * 72), H((n_msgs ? n_msgs : 1) * 48);
+  std::vector<int32_t> win(n_win);
+  uint64_t c0 = 0;
+  auto mark = [&](int k) {
+    const uint64_t c = g_fp_mul_count + g_fp_sqr_count;
+    if (counts4) counts4[k] = c - c0;
+    c0 = c;
+  };
+  c0 = g_fp_mul_count + g_fp_sqr_count;
+  for (uint64_t i = 0; i < n; ++i) rlc_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk.data(), rsig.data(), status);
+  mark(0);
+  for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, n_msgs, H.data());
+  mark(1);
+  std::vector<uint32_t> list;
+  for (uint64_t w = 0; w < n_win; ++w)
+    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, status, win.data()))
+      for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
+        if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
+  mark(2);
+  for (uint32_t i : list) rlc_fallback_lane(i, pks, sigs, msg_idx, H.data(), n_msgs, status);
+  mark(3);
+  stats3[0] = n_win;
+  stats3[1] = stats3[2] = 0;
+  for (int32_t x : win)
+    if (x > 0) {
+      stats3[1] += 1;
+      stats3[2] += (uint64_t)x;
+    }
+  return 0;
+}
