@@ -30,8 +30,12 @@ METRIC = "verified BLS partial sigs/sec (node) + threshold aggregates/sec, 1/2/4
 # (one 381-bit Montgomery product, fp_mul or fp_sqr, = 12x12 CIOS = 300 32x32->64 multiply-adds).
 # Counted by the instrumented host build of the same kernels (tests/test_work_counts.py keeps
 # this in sync).  See DESIGN.md "Roofline".
-FPMUL_PER_VERIFY = 35091
+FPMUL_PER_VERIFY = 30829
 MADS_PER_FPMUL = 300
+# RLC BatchVerify stages (charon_amd/csrc/rlc.h), same unit and source (tests/test_work_counts.py):
+# stage 1 per item, stage 2 per distinct message, stage 3 per window of 8 with 2 messages (one per
+# 4-partial validator) or 1 message (committee root), stage 4 per item re-checked after a failed window.
+RLC_FPMUL = {"item": 5832, "hash": 7144, "window_2msg": 26777, "window_1msg": 21456, "fallback": 21498}
 # gfx950 32x32->64 integer multiply-add peak (v_mad_u64_u32): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 # at half rate (measured: profiles/r01_mad_probe.txt) = 39.3e12 MAD/s.
 MAD_PEAK_T = 39.3
@@ -322,7 +326,15 @@ def main():
             tt = torch.tensor([tel], dtype=torch.float64, device=dev)
             if world > 1:
                 dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            per_win = RLC_FPMUL["window_1msg"] if shared else RLC_FPMUL["window_2msg"]
+            fpmul = (RLC_FPMUL["item"] * n4 + RLC_FPMUL["hash"] * len(roots4) + per_win * w.value
+                     + RLC_FPMUL["fallback"] * fb.value)
+            ach = fpmul * MADS_PER_FPMUL * args.rlc_steps / float(tt.item()) / 1e12
             rlc[variant] = {"verified_partial_sigs_per_s": round(n4 * args.rlc_steps * world / float(tt.item()), 1),
+                            "fpmul_per_item": round(fpmul / n4, 1),
+                            "pipeline_roofline": {"achieved": round(ach, 3), "peak": MAD_PEAK_T, "unit": "Tmad/s",
+                                                  "frac": round(ach / MAD_PEAK_T, 4),
+                                                  "note": "whole 4-stage pipeline over wall time (not one kernel)"},
                             "items_per_gpu": n4, "distinct_roots_per_gpu": len(roots4),
                             "ms_per_batch": round(1000 * float(tt.item()) / args.rlc_steps, 3),
                             "windows": w.value, "windows_failed": wf.value, "items_fallback": fb.value,

@@ -353,7 +353,10 @@ BLS_HD BLS_CALL void g2_clear_cofactor(g2j& r, const g2j& p) {
 }
 
 BLS_HD BLS_CALL bool fp2_sqrt(fp2& r, const fp2& a) {
-  fp n, s, t, x0, inv2x0, t2;
+  // a = a0 + a1 u: s = sqrt(a0^2 + a1^2), t = (a0 + s)/2, then sqrt(a) = x0 + a1/(2 x0) u with
+  // x0^2 = t, or a1/(2 x0) + x0 u with x0^2 = -t when t is not a square.  One power
+  // z = t^((p-3)/4) gives both x0 = t z and 1/x0 = z (t square) or -z (t^((p-1)/2) = -1).
+  fp n, s, t, z, x0, inv_x0, t2;
   fp_sqr(n, a.c0);
   fp_sqr(t, a.c1);
   fp_add(n, n, t);
@@ -361,13 +364,17 @@ BLS_HD BLS_CALL bool fp2_sqrt(fp2& r, const fp2& a) {
   fp_add(t, a.c0, s);
   fp_mul(t, t, FP_HALF);
   if (fp_is_zero(t)) t = a.c0;  // a1 = 0 and s = -a0: use s = a0 instead
-  fp_pow(x0, t, EXP_SQRT, 378);
+  fp_pow(z, t, EXP_SQRT_M1, 378);
+  fp_mul(x0, z, t);
   fp_sqr(t2, x0);
   const bool t_square = fp_eq(t2, t);
-  fp_add(inv2x0, x0, x0);
-  fp_inv(inv2x0, inv2x0);
+  if (t_square)
+    inv_x0 = z;
+  else
+    fp_neg(inv_x0, z);
   fp y0, y1;
-  fp_mul(y1, a.c1, inv2x0);  // a1 / (2 x0)
+  fp_mul(y1, a.c1, inv_x0);
+  fp_mul(y1, y1, FP_HALF);  // a1 / (2 x0)
   if (t_square) {
     y0 = x0;
   } else {

@@ -245,13 +245,42 @@ BLS_HD BLS_INLINE void fp_mul(fp& r, const fp& a, const fp& b) { r = fp_mul_v(a,
 BLS_HD BLS_INLINE void fp_sqr(fp& r, const fp& a) { r = fp_sqr_v(a); }
 #endif
 
-// r = a^e for a fixed exponent given as little-endian 32-bit limbs whose top set bit is top_bit
-// (left-to-right binary; the exponent is the same for every lane, so the branch is uniform).
+// r = a^e for a fixed exponent given as little-endian 32-bit limbs whose top set bit is top_bit.
+// Left-to-right sliding window of 5 bits over the odd powers a, a^3, .., a^31: for the ~380-bit
+// exponents used here (p-2, (p+1)/4, (p-3)/4, Hamming weight ~229) that is ~380 squarings + ~80
+// products instead of ~380 + 229.  The exponent is the same for every lane, so every branch and
+// table index is wave-uniform.
 BLS_HD BLS_CALL void fp_pow(fp& r, const fp& a, const uint32_t* e, int top_bit) {
-  fp acc = a;
-  for (int i = top_bit - 1; i >= 0; --i) {
-    fp_sqr(acc, acc);
-    if ((e[i >> 5] >> (i & 31)) & 1u) fp_mul(acc, acc, a);
+  constexpr int W = 5;
+  fp tbl[1 << (W - 1)];
+  fp a2;
+  tbl[0] = a;
+  fp_sqr(a2, a);
+  for (int k = 1; k < (1 << (W - 1)); ++k) fp_mul(tbl[k], tbl[k - 1], a2);
+  auto bit = [&](int i) { return (e[i >> 5] >> (i & 31)) & 1u; };
+  fp acc;
+  bool started = false;
+  int i = top_bit;
+  while (i >= 0) {
+    if (!bit(i)) {
+      if (started) fp_sqr(acc, acc);
+      --i;
+      continue;
+    }
+    int j = i - (W - 1) < 0 ? 0 : i - (W - 1);
+    while (!bit(j)) ++j;  // window [i..j] ends on a set bit, so its value is odd
+    uint32_t v = 0;
+    for (int k = i; k >= j; --k) {
+      v = (v << 1) | bit(k);
+      if (started) fp_sqr(acc, acc);
+    }
+    if (started) {
+      fp_mul(acc, acc, tbl[v >> 1]);
+    } else {
+      acc = tbl[v >> 1];
+      started = true;
+    }
+    i = j - 1;
   }
   r = acc;
 }

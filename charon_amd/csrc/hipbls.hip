@@ -357,9 +357,11 @@ struct Context {
   std::mutex mu;
   DevBuf b_pk, b_msg, b_off, b_sig, b_st, b_out, b_ids, b_pts, b_pst, b_aux;
   DevBuf r_pk, r_sig, r_h, r_win, r_midx, r_list, r_cnt;  // RLC BatchVerify workspaces
-  // RLC sub-batches in flight.  The process gets GPU_MAX_HW_QUEUES = 4 hardware queues: the caller's
-  // stream (which also hashes the messages) + 3 sub-batch streams, so no two streams share a queue.
-  static constexpr int kSub = 3;
+  // RLC sub-batches in flight.  The process gets GPU_MAX_HW_QUEUES = 4 hardware queues, shared by
+  // the caller's stream (which also hashes the messages), the library stream and these; a kernel
+  // trace (profiles/r01_rlc_trace.txt) showed a third sub-stream landing on an occupied queue and
+  // serializing behind it, so two sub-batches.
+  static constexpr int kSub = 2;
   hipStream_t sub[kSub] = {};
   hipEvent_t ev_fork = nullptr, ev_hash = nullptr, ev_join[kSub] = {};
   uint64_t r_windows = 0;                  // window count of the last RLC call (hipbls_rlc_stats)

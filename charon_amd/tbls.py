@@ -163,7 +163,8 @@ class HipBLS:
         out = ctypes.create_string_buffer(48 * max(n, 1))
         st = _status_array(n)
         _check(self.lib.hipbls_secret_to_public_key_batch(b"".join(secrets_), n, out, st), self.lib)
-        return [out.raw[48 * i:48 * i + 48] for i in range(n)], [st[i] for i in range(n)]
+        raw = out.raw  # one copy: .raw rebuilds the bytes object on every access
+        return [raw[48 * i:48 * i + 48] for i in range(n)], list(st)[:n]
 
     def _split(self, secret: bytes, total: int, threshold: int, tail: Sequence[bytes]) -> Dict[int, bytes]:
         if int.from_bytes(secret, "big") >= R:
@@ -173,7 +174,8 @@ class HipBLS:
         _check(self.lib.hipbls_threshold_split(secret, b"".join(tail), total, threshold, out, st), self.lib)
         if st[0] != OK:
             raise TBLSError("cannot unmarshal bytes into Herumi secret key")
-        return {i + 1: out.raw[32 * i:32 * i + 32] for i in range(total)}
+        raw = out.raw
+        return {i + 1: raw[32 * i:32 * i + 32] for i in range(total)}
 
     def threshold_split(self, secret: bytes, total: int, threshold: int) -> Dict[int, bytes]:
         """herumi.go:134-181: polynomial tail from the CSPRNG."""
@@ -212,7 +214,8 @@ class HipBLS:
         out = ctypes.create_string_buffer(96 * max(n, 1))
         st = _status_array(n)
         _check(self.lib.hipbls_sign_batch(b"".join(sks), blob, offs, n, out, st), self.lib)
-        return [out.raw[96 * i:96 * i + 96] for i in range(n)], [st[i] for i in range(n)]
+        raw = out.raw
+        return [raw[96 * i:96 * i + 96] for i in range(n)], list(st)[:n]
 
     def verify(self, compressed_public_key: bytes, data: bytes, signature: bytes) -> None:
         """herumi.go:285-301: raises TBLSError with the reference's message on failure."""
@@ -229,7 +232,7 @@ class HipBLS:
         blob, offs = _offsets(msgs)
         st = _status_array(n)
         _check(self.lib.hipbls_verify_batch(b"".join(pks), blob, offs, b"".join(sigs), n, st), self.lib)
-        return [st[i] for i in range(n)]
+        return list(st)[:n]
 
     def batch_verify(self, pks, msgs, sigs) -> List[Optional[TBLSError]]:
         """Per-item outcome of Verify: None when valid, else the TBLSError Verify would raise."""
@@ -263,7 +266,7 @@ class HipBLS:
         st = _status_array(n)
         _check(self.lib.hipbls_batch_verify_rlc(b"".join(pks), b"".join(sigs), idx, n, blob, offs, len(table), seed,
                                                 st), self.lib)
-        return [st[i] for i in range(n)]
+        return list(st)[:n]
 
     def rlc_stats(self) -> Tuple[int, int, int]:
         """(windows, windows that failed the batched check, items re-verified one by one) of the last RLC call."""
@@ -294,9 +297,10 @@ class HipBLS:
         st = _status_array(n_groups)
         _check(self.lib.hipbls_threshold_aggregate_batch(b"".join(sigs), arr, offs, n_groups, out, st), self.lib)
         res = []
+        raw = out.raw
         for g in range(n_groups):
             if st[g] == OK:
-                res.append(out.raw[96 * g:96 * g + 96])
+                res.append(raw[96 * g:96 * g + 96])
             elif st[g] == ERR_SIGNATURE:
                 res.append(TBLSError("cannot unmarshal signature into Herumi signature"))
             else:

@@ -27,3 +27,35 @@ def test_bench_fpmul_per_verify_matches_count():
     import bench
     got = mean_verify_count()
     assert abs(got - bench.FPMUL_PER_VERIFY) / got < 0.01, got
+
+
+def test_bench_rlc_stage_counts_match():
+    """bench.RLC_FPMUL (the RLC roofline's unit) against the host build of the four stages."""
+    import bench
+    from tests.rlc_cases import message_table, validator_batch
+    from tests.test_rlc_host import host_pk, host_sign
+    L = lib()
+
+    def run(pks, msgs, sigs):
+        table, idx = message_table(msgs)
+        n = len(pks)
+        offs = (ctypes.c_uint64 * (len(table) + 1))(*[32 * i for i in range(len(table) + 1)])
+        st = (ctypes.c_int32 * n)()
+        stats = (ctypes.c_uint64 * 3)()
+        cnt = (ctypes.c_uint64 * 4)()
+        arr = (ctypes.c_uint32 * n)(*idx)
+        L.ht_rlc_verify(b"".join(pks), b"".join(sigs), arr, ctypes.c_uint64(n), b"".join(table), offs,
+                        ctypes.c_uint64(len(table)), bytes(32), st, stats, cnt)
+        return list(stats), list(cnt)
+
+    want = bench.RLC_FPMUL
+    pks, msgs, sigs, _ = validator_batch(host_sign(L), host_pk(L), 4, 4, seed=1)
+    stats, cnt = run(pks, msgs, sigs)
+    assert abs(cnt[0] / 16 - want["item"]) / want["item"] < 0.02
+    assert abs(cnt[2] / 2 - want["window_2msg"]) / want["window_2msg"] < 0.02
+    pks, msgs, sigs, _ = validator_batch(host_sign(L), host_pk(L), 1, 16, seed=2)
+    stats, cnt = run(pks, msgs, sigs)
+    assert abs(cnt[2] / 2 - want["window_1msg"]) / want["window_1msg"] < 0.02
+    pks, msgs, sigs, _ = validator_batch(host_sign(L), host_pk(L), 4, 4, seed=3, bad=(1, 9))
+    stats, cnt = run(pks, msgs, sigs)
+    assert abs(cnt[3] / stats[2] - want["fallback"]) / want["fallback"] < 0.03
