@@ -139,6 +139,17 @@ def make_c4(impl, n_dv, rng, shared_roots=0, shares=4, nkeys=4096):
     return pks, sigs, midx, roots, set(bad)
 
 
+def traffic_from_pmc(path=os.path.join(ROOT, "profiles", "r01_pmc_verify.json")):
+    """HBM bytes per k_verify_fused launch from the committed rocprofv3 PMC passes of this build
+    (FETCH_SIZE + WRITE_SIZE, scripts/pmc_summary.py); None when absent.  Almost all of it is
+    scratch (register-spill) traffic, ~8000x the 188 B/verify of algorithmic input."""
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch_raw")
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(n_sample, rng):
     """Oracle (oracle/bls12381.py, pure Python, 1 core) timed on this host: kind 'port'."""
     from oracle import bls12381 as bls
@@ -381,7 +392,7 @@ def main():
                 "peak": MAD_PEAK_T,
                 "unit": "Tmad/s",
                 "frac": round(achieved / MAD_PEAK_T, 4),
-                "traffic": None,
+                "traffic": traffic_from_pmc(),
                 "algorithmic_unit": "%d Fp-mul-equivalents x %d MADs per verify" % (FPMUL_PER_VERIFY, MADS_PER_FPMUL),
                 "kernel_avg_ms": round(k_ms, 3),
                 "kernel_launches": int(launches.value),
