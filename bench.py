@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--rlc-validators", type=int, default=32768,
                     help="C4 validators per GPU (x4 partials; 32,768 = the 1M-partial node batch / 8 GPUs; 0 = skip)")
     ap.add_argument("--rlc-steps", type=int, default=3)
+    ap.add_argument("--keys", type=int, default=1, help="also time C2 / C4 with the resident pubshare table (0 = skip)")
     ap.add_argument("--rlc-big-validators", type=int, default=262144,
                     help="also time one GPU on the whole C4 node batch (262,144 x 4 = 1M partials; 0 = skip)")
     return ap.parse_args()
@@ -242,6 +243,36 @@ def main():
     total = n * args.steps * world
     value = total / elapsed
 
+    # ---- C2 with the resident pubshare table (extra field): same items, keys by index
+    keys_rate = None
+    if args.keys:
+        table = list(dict.fromkeys(pks))
+        pos = {k: j for j, k in enumerate(table)}
+        assert set(impl.load_pubshares(table)) == {0}
+        d_kidx = torch.tensor([pos[p] for p in pks], dtype=torch.int32).to(dev)
+        d_kst = torch.full((n,), -1, dtype=torch.int32, device=dev)
+
+        def kstep():
+            rc = lib.hipbls_verify_batch_keys_device(d_kidx.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
+                                                     d_sig.data_ptr(), n, d_kst.data_ptr(),
+                                                     ctypes.c_void_p(stream.cuda_stream))
+            assert rc == 0
+
+        kstep()
+        torch.cuda.synchronize(dev)
+        barrier()
+        ts = time.perf_counter()
+        for _ in range(args.steps):
+            kstep()
+        torch.cuda.synchronize(dev)
+        barrier()
+        tk = time.perf_counter() - ts
+        assert d_kst.cpu().tolist() == st, "key-table bitmap differs from wire-format Verify"
+        tt = torch.tensor([tk], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        keys_rate = n * args.steps * world / float(tt.item())
+
     # ---- C3: threshold aggregation + Verify of the aggregate (extra field)
     tagg = None
     if args.tagg_groups > 0:
@@ -350,6 +381,35 @@ def main():
                             "ms_per_batch": round(1000 * float(tt.item()) / args.rlc_steps, 3),
                             "windows": w.value, "windows_failed": wf.value, "items_fallback": fb.value,
                             "kernel_avg_ms": kms}
+            if args.keys and variant == "i_root_per_validator":
+                # same batch with pubshares from the resident table
+                table4 = list(dict.fromkeys(pks4))
+                pos4 = {k: j for j, k in enumerate(table4)}
+                assert set(impl.load_pubshares(table4)) == {0}
+                d_k4 = torch.tensor([pos4[p] for p in pks4], dtype=torch.int32).to(dev)
+
+                def rkstep():
+                    rc = lib.hipbls_batch_verify_rlc_keys_device(d_k4.data_ptr(), d_sig4.data_ptr(),
+                                                                 d_midx4.data_ptr(), n4, d_msg4.data_ptr(),
+                                                                 d_off4.data_ptr(), len(roots4), seed,
+                                                                 d_st4.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+                    assert rc == 0
+
+                rkstep()
+                torch.cuda.synchronize(dev)
+                barrier()
+                ts = time.perf_counter()
+                for _ in range(args.rlc_steps):
+                    rkstep()
+                torch.cuda.synchronize(dev)
+                barrier()
+                tk = time.perf_counter() - ts
+                assert d_st4.cpu().tolist() == st4, "RLC key-table bitmap differs"
+                tt = torch.tensor([tk], dtype=torch.float64, device=dev)
+                if world > 1:
+                    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                rlc[variant]["verified_partial_sigs_per_s_pubshare_table"] = round(
+                    n4 * args.rlc_steps * world / float(tt.item()), 1)
             del d_pk4, d_sig4, d_midx4, d_msg4, d_off4, d_st4
 
     if rank == 0:
@@ -371,6 +431,7 @@ def main():
                                    "distinct messages" % n,
                        "items_per_gpu": n, "parallelism": "shard-by-validator-index x %d" % world},
             "pairings_per_s": round(2 * value, 1),
+            "verified_partial_sigs_per_s_pubshare_table": round(keys_rate, 1) if keys_rate else None,
             "threshold_aggregates_per_s": round(tagg, 1) if tagg else None,
             "threshold_aggregate_workload": "C3: %d validators x 7-of-10 Lagrange in G2 + Verify of each aggregate per GPU"
                                             % args.tagg_groups if tagg else None,

@@ -278,13 +278,17 @@ __global__ void __launch_bounds__(kBlock) k_recover_secret(const uint8_t* __rest
 // The four stages run per sub-batch (a contiguous, window-aligned item range) so that several
 // sub-batches' stages overlap on separate streams (launch_rlc).
 // Stage 1: one lane per item -> status (final or RLC_PENDING), [r_i] pk_i and [r_i] sig_i in SoA.
+// pks == nullptr: public keys come from the resident pubshare table (key_idx, T, tcode, tab).
 __global__ void __launch_bounds__(kBlock) k_rlc_items(uint64_t i0, uint64_t i1, const uint8_t* __restrict__ pks,
                                                       const uint8_t* __restrict__ sigs,
                                                       const uint32_t* __restrict__ msg_idx, uint64_t n,
                                                       uint64_t n_msgs, rlc_seed seed, uint32_t* __restrict__ rpk,
-                                                      uint32_t* __restrict__ rsig, int32_t* __restrict__ status) {
+                                                      uint32_t* __restrict__ rsig, int32_t* __restrict__ status,
+                                                      const uint32_t* __restrict__ key_idx, uint64_t T,
+                                                      const int32_t* __restrict__ tcode,
+                                                      const uint32_t* __restrict__ tab) {
   const uint64_t i = i0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (i < i1) rlc_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk, rsig, status);
+  if (i < i1) rlc_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk, rsig, status, key_idx, T, tcode, tab);
 }
 
 // Stage 2: one lane per distinct message -> H(m) in affine SoA (48 words).
@@ -320,11 +324,45 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback(const uint32_t* __restr
                                                          const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
                                                          const uint32_t* __restrict__ msg_idx,
                                                          const uint32_t* __restrict__ H, uint64_t n_msgs,
-                                                         int32_t* __restrict__ status) {
+                                                         int32_t* __restrict__ status,
+                                                         const uint32_t* __restrict__ key_idx, uint64_t T,
+                                                         const uint32_t* __restrict__ tab) {
   const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t len = *list_len;
   if (j >= len || j >= cap) return;
-  rlc_fallback_lane(list[j], pks, sigs, msg_idx, H, n_msgs, status);
+  rlc_fallback_lane(list[j], pks, sigs, msg_idx, H, n_msgs, status, key_idx, T, tab);
+}
+
+// ---------------------------------------------------------------- resident pubshare table
+// Load: one lane per pubshare -> decode + subgroup test once (app/app.go:343-381 builds the same set
+// from the cluster lock at startup), keeping the affine key and [x] pk for the RLC scalars.
+__global__ void __launch_bounds__(kBlock) k_pubtab_load(const uint8_t* __restrict__ pks, uint64_t T,
+                                                        int32_t* __restrict__ code, uint32_t* __restrict__ tab,
+                                                        int32_t* __restrict__ status) {
+  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (k < T) status[k] = pubtab_load_lane(k, pks, T, code, tab);
+}
+
+// tbls.Verify with the key from the table: key_idx[i] >= T -> HIPBLS_ERR_ARG for that item.
+__global__ void __launch_bounds__(kBlock) k_verify_keys(const uint32_t* __restrict__ key_idx, uint64_t T,
+                                                        const int32_t* __restrict__ code,
+                                                        const uint32_t* __restrict__ tab,
+                                                        const uint8_t* __restrict__ msgs,
+                                                        const uint64_t* __restrict__ offs,
+                                                        const uint8_t* __restrict__ sigs, uint64_t n,
+                                                        int32_t* __restrict__ status) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = key_idx[i];
+  if (k >= T) {
+    status[i] = HIPBLS_ERR_ARG;
+    return;
+  }
+  g1a pk;
+  g1j xpk;
+  const int dp = pubtab_get(pk, xpk, k, T, code, tab);
+  const uint64_t o0 = offs[i], o1 = offs[i + 1];
+  status[i] = op_verify_decoded_pk(dp, pk, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i);
 }
 
 // ============================================================================ host runtime
@@ -357,6 +395,8 @@ struct Context {
   std::mutex mu;
   DevBuf b_pk, b_msg, b_off, b_sig, b_st, b_out, b_ids, b_pts, b_pst, b_aux;
   DevBuf r_pk, r_sig, r_h, r_win, r_midx, r_list, r_cnt;  // RLC BatchVerify workspaces
+  DevBuf t_code, t_tab, b_kidx;                            // resident pubshare table + key indices
+  uint64_t t_size = 0;
   // RLC sub-batches in flight.  The process gets GPU_MAX_HW_QUEUES = 4 hardware queues, shared by
   // the caller's stream (which also hashes the messages), the library stream and these; a kernel
   // trace (profiles/r01_rlc_trace.txt) showed a third sub-stream landing on an occupied queue and
@@ -458,8 +498,13 @@ int ensure_rlc_streams() {
 // at one wave per SIMD), so overlapping the sub-batches' stages is what fills the CUs.  The caller's
 // stream `s` forks into the sub-streams and joins back, so the call stays stream-ordered.
 int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n, const uint8_t* d_msgs,
-               const uint64_t* d_offs, uint64_t n_msgs, const uint8_t* seed32, int32_t* d_status, hipStream_t s) {
+               const uint64_t* d_offs, uint64_t n_msgs, const uint8_t* seed32, int32_t* d_status, hipStream_t s,
+               const uint32_t* d_kidx = nullptr) {
   Context& c = g_ctx;
+  // d_pks == nullptr: keys from the resident table
+  const uint64_t T = c.t_size;
+  const int32_t* tcode = (const int32_t*)c.t_code.p;
+  const uint32_t* tab = (const uint32_t*)c.t_tab.p;
   c.r_windows = 0;
   if (n == 0) return HIPBLS_OK;
   if (n > 0xffffffffull) return HIPBLS_ERR_ARG;  // fallback list holds 32-bit item indices
@@ -507,7 +552,7 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
     HIP_TRY(hipStreamWaitEvent(ss, c.ev_fork, 0));
     rc = timed("rlc_items", ss, [&] {
       hipLaunchKernelGGL(k_rlc_items, dim3((unsigned)grid_for(i1 - i0)), dim3(kBlock), 0, ss, i0, i1, d_pks, d_sigs,
-                         d_midx, n, n_msgs, seed, rpk, rsig, d_status);
+                         d_midx, n, n_msgs, seed, rpk, rsig, d_status, d_kidx, T, tcode, tab);
     });
     if (rc) return rc;
     HIP_TRY(hipStreamWaitEvent(ss, c.ev_hash, 0));
@@ -521,7 +566,7 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
     rc = timed("rlc_fallback", ss, [&] {
       hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(i1 - i0)), dim3(kBlock), 0, ss,
                          (const uint32_t*)(list + i0), (const uint32_t*)(cnt + k), i1 - i0, d_pks, d_sigs, d_midx,
-                         (const uint32_t*)H, n_msgs, d_status);
+                         (const uint32_t*)H, n_msgs, d_status, d_kidx, T, tab);
     });
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c.ev_join[k], ss));
@@ -909,6 +954,148 @@ int hipbls_batch_verify_rlc_device(const uint8_t* d_pks, const uint8_t* d_sigs, 
   std::lock_guard<std::mutex> lk(g_ctx.mu);
   return launch_rlc(d_pks, d_sigs, d_msg_idx, n, d_msgs, d_msg_offsets, n_msgs, seed32, d_status,
                     stream ? (hipStream_t)stream : g_ctx.stream);
+}
+
+int hipbls_pubshare_table_load(const uint8_t* pks, uint64_t n, int32_t* status) {
+  if ((n && (!pks || !status)) || mul_overflows(n, 240) || n > 0xffffffffull) return HIPBLS_ERR_ARG;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  Context& c = g_ctx;
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  HIP_TRY(hipDeviceSynchronize());  // no call may still read the old table
+  c.t_size = 0;
+  if (n == 0) return HIPBLS_OK;
+  HIP_TRY(c.b_pk.ensure(n * 48));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(c.t_code.ensure(n * 4));
+  HIP_TRY(c.t_tab.ensure(n * PUBTAB_WORDS * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(k_pubtab_load, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_pk.p, n,
+                     (int32_t*)c.t_code.p, (uint32_t*)c.t_tab.p, (int32_t*)c.b_st.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  c.t_size = n;
+  return HIPBLS_OK;
+}
+
+int hipbls_pubshare_table_size(uint64_t* n) {
+  if (!n) return HIPBLS_ERR_ARG;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  *n = g_ctx.t_size;
+  return HIPBLS_OK;
+}
+
+int hipbls_verify_batch_keys(const uint32_t* key_idx, const uint8_t* msgs, const uint64_t* msg_offsets,
+                             const uint8_t* sigs, uint64_t n, int32_t* status) {
+  if (n == 0) return HIPBLS_OK;
+  if (!key_idx || !msg_offsets || !sigs || !status || mul_overflows(n, 96)) return HIPBLS_ERR_ARG;
+  const uint64_t msg_total = msg_offsets[n];
+  if (msg_total && !msgs) return HIPBLS_ERR_ARG;
+  for (uint64_t i = 0; i < n; ++i)
+    if (msg_offsets[i + 1] < msg_offsets[i] || msg_offsets[i + 1] - msg_offsets[i] > 0xffffffffull)
+      return HIPBLS_ERR_ARG;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  Context& c = g_ctx;
+  for (uint64_t i = 0; i < n; ++i)
+    if (key_idx[i] >= c.t_size) {
+      g_last_error = "key index outside the pubshare table";
+      return HIPBLS_ERR_ARG;
+    }
+  HIP_TRY(c.b_kidx.ensure(n * 4));
+  HIP_TRY(c.b_sig.ensure(n * 96));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_off.ensure((n + 1) * 8));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  rc = timed("verify_keys", c.stream, [&] {
+    hipLaunchKernelGGL(k_verify_keys, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream,
+                       (const uint32_t*)c.b_kidx.p, c.t_size, (const int32_t*)c.t_code.p, (const uint32_t*)c.t_tab.p,
+                       (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p, (const uint8_t*)c.b_sig.p, n,
+                       (int32_t*)c.b_st.p);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int hipbls_verify_batch_keys_device(const uint32_t* d_key_idx, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
+                                    const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream) {
+  if (n == 0) return HIPBLS_OK;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  Context& c = g_ctx;
+  hipStream_t s = stream ? (hipStream_t)stream : c.stream;
+  return timed("verify_keys", s, [&] {
+    hipLaunchKernelGGL(k_verify_keys, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_key_idx, c.t_size,
+                       (const int32_t*)c.t_code.p, (const uint32_t*)c.t_tab.p, d_msgs, d_msg_offsets, d_sigs, n,
+                       d_status);
+  });
+}
+
+int hipbls_batch_verify_rlc_keys(const uint32_t* key_idx, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
+                                 const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs,
+                                 const uint8_t* seed32, int32_t* status) {
+  if (n == 0) return HIPBLS_OK;
+  if (!key_idx || !sigs || !msg_idx || !msg_offsets || !seed32 || !status || mul_overflows(n, 288))
+    return HIPBLS_ERR_ARG;
+  for (uint64_t i = 0; i < n; ++i)
+    if (msg_idx[i] >= n_msgs) {
+      g_last_error = "message index out of range";
+      return HIPBLS_ERR_ARG;
+    }
+  for (uint64_t m = 0; m < n_msgs; ++m)
+    if (msg_offsets[m + 1] < msg_offsets[m] || msg_offsets[m + 1] - msg_offsets[m] > 0xffffffffull)
+      return HIPBLS_ERR_ARG;
+  const uint64_t msg_total = msg_offsets[n_msgs];
+  if (msg_total && !msgs) return HIPBLS_ERR_ARG;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  Context& c = g_ctx;
+  for (uint64_t i = 0; i < n; ++i)
+    if (key_idx[i] >= c.t_size) {
+      g_last_error = "key index outside the pubshare table";
+      return HIPBLS_ERR_ARG;
+    }
+  HIP_TRY(c.b_kidx.ensure(n * 4));
+  HIP_TRY(c.b_sig.ensure(n * 96));
+  HIP_TRY(c.r_midx.ensure(n * 4));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_off.ensure((n_msgs + 1) * 8));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.r_midx.p, msg_idx, n * 4, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n_msgs + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  rc = launch_rlc(nullptr, (const uint8_t*)c.b_sig.p, (const uint32_t*)c.r_midx.p, n, (const uint8_t*)c.b_msg.p,
+                  (const uint64_t*)c.b_off.p, n_msgs, seed32, (int32_t*)c.b_st.p, c.stream,
+                  (const uint32_t*)c.b_kidx.p);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int hipbls_batch_verify_rlc_keys_device(const uint32_t* d_key_idx, const uint8_t* d_sigs, const uint32_t* d_msg_idx,
+                                        uint64_t n, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
+                                        uint64_t n_msgs, const uint8_t* seed32, int32_t* d_status, void* stream) {
+  if (n == 0) return HIPBLS_OK;
+  if (!seed32 || !d_key_idx || mul_overflows(n, 288)) return HIPBLS_ERR_ARG;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  return launch_rlc(nullptr, d_sigs, d_msg_idx, n, d_msgs, d_msg_offsets, n_msgs, seed32, d_status,
+                    stream ? (hipStream_t)stream : g_ctx.stream, d_key_idx);
 }
 
 int hipbls_rlc_stats(uint64_t* windows, uint64_t* windows_failed, uint64_t* items_fallback) {

@@ -87,19 +87,18 @@ BLS_HD BLS_CALL int g1_decompress_keep_x(g1a& out, g1j& xP, const uint8_t* b) {
   return DEC_OK;
 }
 
-// Stage 1, one lane per item: decode + subgroup-check pk and sig in herumi's order, then store
-// [r_i] pk_i (G1 Jacobian, 36 words) and [r_i] sig_i (G2 Jacobian, 72 words).  Items that already
-// have their final status (bad encoding, infinity) store the point at infinity.
-BLS_HD BLS_CALL int rlc_item(const uint8_t* pk48, const uint8_t* sig96, const rlc_seed& seed, uint64_t i,
-                             uint32_t* rpk36, uint32_t* rsig72) {
+// Stage 1 with the public key already decoded: dp = its DEC_* code, pk affine, xpk = [x] pk (from
+// g1_decompress_keep_x, either just now or once at load time in the resident pubshare table).
+// Decodes + subgroup-checks the signature in herumi's order, then stores [r_i] pk_i (G1 Jacobian,
+// 36 words) and [r_i] sig_i (G2 Jacobian, 72 words).  Items that already have their final status
+// (bad encoding, infinity) store the point at infinity.
+BLS_HD BLS_CALL int rlc_item_decoded(int dp, const g1a& pk, const g1j& xpk, const uint8_t* sig96, const rlc_seed& seed,
+                                     uint64_t i, uint32_t* rpk36, uint32_t* rsig72) {
   g1j rp;
   g2j rs;
   jac_set_inf(rp);
   jac_set_inf(rs);
-  g1a pk;
-  g1j xpk;
   int st = RLC_PENDING;
-  const int dp = g1_decompress_keep_x(pk, xpk, pk48);
   if (dp == DEC_BAD) st = HIPBLS_ERR_PUBKEY;
   g2a sig;
   if (st == RLC_PENDING) {
@@ -125,6 +124,55 @@ BLS_HD BLS_CALL int rlc_item(const uint8_t* pk48, const uint8_t* sig96, const rl
   const uint32_t* s = &rs.x.c0.v[0];
   for (int k = 0; k < 72; ++k) rsig72[k] = s[k];
   return st;
+}
+
+// Stage 1, one lane per item, from the wire-format public key.
+BLS_HD BLS_CALL int rlc_item(const uint8_t* pk48, const uint8_t* sig96, const rlc_seed& seed, uint64_t i,
+                             uint32_t* rpk36, uint32_t* rsig72) {
+  g1a pk;
+  g1j xpk;
+  const int dp = g1_decompress_keep_x(pk, xpk, pk48);
+  return rlc_item_decoded(dp, pk, xpk, sig96, seed, i, rpk36, rsig72);
+}
+
+// ---- resident pubshare table: every pubshare decoded + subgroup-checked once ----
+// SoA with stride T (table size): code[T] (DEC_*), then 24 words affine (x, y), then 36 words [x]pk.
+constexpr int PUBTAB_WORDS = 24 + 36;
+
+BLS_HD BLS_INLINE int pubtab_load_lane(uint64_t k, const uint8_t* pks, uint64_t T, int32_t* code, uint32_t* tab) {
+  g1a pk;
+  g1j xpk;
+  const int dp = g1_decompress_keep_x(pk, xpk, pks + 48 * k);
+  if (dp != DEC_OK) {
+    fp_set_zero(pk.x);
+    fp_set_zero(pk.y);
+    jac_set_inf(xpk);
+  }
+  soa_store<24>(tab, T, k, &pk.x.v[0]);
+  soa_store<36>(tab + 24 * T, T, k, &xpk.x.v[0]);
+  code[k] = dp;
+  return dp == DEC_BAD ? HIPBLS_ERR_PUBKEY : HIPBLS_OK;
+}
+
+BLS_HD BLS_INLINE int pubtab_get(g1a& pk, g1j& xpk, uint64_t k, uint64_t T, const int32_t* code, const uint32_t* tab) {
+  soa_load<24>(&pk.x.v[0], tab, T, k);
+  soa_load<36>(&xpk.x.v[0], tab + 24 * T, T, k);
+  return code[k];
+}
+
+// tbls.Verify with the public key taken from the table (same statuses as op_verify).
+BLS_HD BLS_CALL int op_verify_decoded_pk(int dp, const g1a& pk, const uint8_t* msg, uint32_t msg_len,
+                                         const uint8_t* sig96) {
+  if (dp == DEC_BAD) return HIPBLS_ERR_PUBKEY;
+  g2a sig;
+  const int ds = g2_decompress(sig, sig96, true);
+  if (ds == DEC_BAD) return HIPBLS_ERR_SIGNATURE;
+  if (dp == DEC_INF || ds == DEC_INF) return HIPBLS_ERR_VERIFY;
+  g2j hj;
+  hash_to_g2(hj, msg, msg_len, DST_POP, 43);
+  g2a hm;
+  jac_to_aff(hm, hj);
+  return pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }
 
 // Multi-Miller loop over up to MAXN pairs with one shared Fp12 squaring chain (pairing.h steps).
@@ -212,12 +260,14 @@ BLS_HD BLS_INLINE bool rlc_window(uint64_t i0, uint64_t i1, const int32_t* statu
 // ---- lane bodies of the four stages (kernels in hipbls.hip; host loop in tests/native) --------
 
 // Stage 1, item i: status (final, or RLC_PENDING) and the scaled pk / sig in SoA.
+// pks == nullptr: the keys come from the resident table (key_idx[i] < T).
 BLS_HD BLS_INLINE void rlc_items_lane(uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
                                       uint64_t n, uint64_t n_msgs, const rlc_seed& seed, uint32_t* rpk,
-                                      uint32_t* rsig, int32_t* status) {
+                                      uint32_t* rsig, int32_t* status, const uint32_t* key_idx = nullptr,
+                                      uint64_t T = 0, const int32_t* tcode = nullptr, const uint32_t* tab = nullptr) {
   uint32_t p[36], s[72];
   int st;
-  if (msg_idx[i] >= n_msgs) {  // device entry point: an out-of-range message index is an argument error
+  if (msg_idx[i] >= n_msgs || (!pks && key_idx[i] >= T)) {  // device entry point: out-of-range index
     st = HIPBLS_ERR_ARG;
     g1j ip;
     g2j is;
@@ -225,8 +275,13 @@ BLS_HD BLS_INLINE void rlc_items_lane(uint64_t i, const uint8_t* pks, const uint
     jac_set_inf(is);
     for (int k = 0; k < 36; ++k) p[k] = (&ip.x.v[0])[k];
     for (int k = 0; k < 72; ++k) s[k] = (&is.x.c0.v[0])[k];
-  } else {
+  } else if (pks) {
     st = rlc_item(pks + 48 * i, sigs + 96 * i, seed, i, p, s);
+  } else {
+    g1a pk;
+    g1j xpk;
+    const int dp = pubtab_get(pk, xpk, key_idx[i], T, tcode, tab);
+    st = rlc_item_decoded(dp, pk, xpk, sigs + 96 * i, seed, i, p, s);
   }
   soa_store<36>(rpk, n, i, p);
   soa_store<72>(rsig, n, i, s);
@@ -272,11 +327,16 @@ BLS_HD BLS_INLINE int rlc_window_lane(uint64_t w, uint64_t n, const uint32_t* ms
 // points already passed decoding and the subgroup tests in stage 1 and H(m) is in the table, so this
 // is the bare pairing check: e(pk, H(m)) * e(-g1, sig) == 1 (about half of a full op_verify).
 BLS_HD BLS_INLINE void rlc_fallback_lane(uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
-                                         const uint32_t* H, uint64_t n_msgs, int32_t* status) {
+                                         const uint32_t* H, uint64_t n_msgs, int32_t* status,
+                                         const uint32_t* key_idx = nullptr, uint64_t T = 0,
+                                         const uint32_t* tab = nullptr) {
   if (status[i] != RLC_PENDING) return;
   g1a pk;
   g2a sig, hm;
-  g1_decompress(pk, pks + 48 * i, false);
+  if (pks)
+    g1_decompress(pk, pks + 48 * i, false);
+  else
+    soa_load<24>(&pk.x.v[0], tab, T, key_idx[i]);
   g2_decompress(sig, sigs + 96 * i, false);
   soa_load<48>(&hm.x.c0.v[0], H, n_msgs, msg_idx[i]);
   status[i] = pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;

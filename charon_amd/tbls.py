@@ -77,6 +77,12 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_batch_verify_rlc": ([u8p, u8p, u32p, u64, u8p, u64p, u64, u8p, i32p], ctypes.c_int),
         "hipbls_batch_verify_rlc_device": ([vp, vp, vp, u64, vp, vp, u64, u8p, vp, vp], ctypes.c_int),
         "hipbls_rlc_stats": ([u64p, u64p, u64p], ctypes.c_int),
+        "hipbls_pubshare_table_load": ([u8p, u64, i32p], ctypes.c_int),
+        "hipbls_pubshare_table_size": ([u64p], ctypes.c_int),
+        "hipbls_verify_batch_keys": ([u32p, u8p, u64p, u8p, u64, i32p], ctypes.c_int),
+        "hipbls_batch_verify_rlc_keys": ([u32p, u8p, u32p, u64, u8p, u64p, u64, u8p, i32p], ctypes.c_int),
+        "hipbls_verify_batch_keys_device": ([vp, vp, vp, vp, u64, vp, vp], ctypes.c_int),
+        "hipbls_batch_verify_rlc_keys_device": ([vp, vp, vp, u64, vp, vp, u64, u8p, vp, vp], ctypes.c_int),
         "hipbls_kernel_timing": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), u64p], ctypes.c_int),
         "hipbls_kernel_timing_reset": ([], ctypes.c_int),
     }
@@ -97,6 +103,8 @@ def exported_symbols() -> List[str]:
         "hipbls_threshold_aggregate_batch_device", "hipbls_sign_batch_device",
         "hipbls_secret_to_public_key_batch_device", "hipbls_kernel_timing", "hipbls_kernel_timing_reset",
         "hipbls_batch_verify_rlc", "hipbls_batch_verify_rlc_device", "hipbls_rlc_stats",
+        "hipbls_pubshare_table_load", "hipbls_pubshare_table_size", "hipbls_verify_batch_keys",
+        "hipbls_batch_verify_rlc_keys", "hipbls_verify_batch_keys_device", "hipbls_batch_verify_rlc_keys_device",
     ]
 
 
@@ -266,6 +274,53 @@ class HipBLS:
         st = _status_array(n)
         _check(self.lib.hipbls_batch_verify_rlc(b"".join(pks), b"".join(sigs), idx, n, blob, offs, len(table), seed,
                                                 st), self.lib)
+        return list(st)[:n]
+
+    # ---------------------------------------------------------------- resident pubshare table (§8f.2)
+    def load_pubshares(self, pks: Sequence[bytes]) -> List[int]:
+        """Decode + subgroup-check every pubshare once (charon: app/app.go:343-381 at startup).
+        Returns per-key status (OK / ERR_PUBKEY); keys are then named by their index."""
+        n = len(pks)
+        if any(len(p) != 48 for p in pks):
+            raise ValueError("bad key length")
+        st = _status_array(n)
+        _check(self.lib.hipbls_pubshare_table_load(b"".join(pks), n, st), self.lib)
+        return list(st)[:n]
+
+    def batch_verify_keys_status(self, key_idx: Sequence[int], msgs: Sequence[bytes],
+                                 sigs: Sequence[bytes]) -> List[int]:
+        """batch_verify_status with pks[i] = loaded table[key_idx[i]]."""
+        n = len(key_idx)
+        if not (len(msgs) == n == len(sigs)):
+            raise ValueError("mismatching lengths")
+        blob, offs = _offsets(msgs)
+        st = _status_array(n)
+        idx = (ctypes.c_uint32 * max(n, 1))(*key_idx)
+        _check(self.lib.hipbls_verify_batch_keys(idx, blob, offs, b"".join(sigs), n, st), self.lib)
+        return list(st)[:n]
+
+    def batch_verify_rlc_keys_status(self, key_idx: Sequence[int], msgs: Sequence[bytes], sigs: Sequence[bytes],
+                                     seed: Optional[bytes] = None) -> List[int]:
+        """batch_verify_rlc_status with pks[i] = loaded table[key_idx[i]]."""
+        n = len(key_idx)
+        if not (len(msgs) == n == len(sigs)):
+            raise ValueError("mismatching lengths")
+        seed = secrets.token_bytes(32) if seed is None else seed
+        pos: Dict[bytes, int] = {}
+        table: List[bytes] = []
+        midx = (ctypes.c_uint32 * max(n, 1))()
+        for i, m in enumerate(msgs):
+            m = bytes(m)
+            j = pos.get(m)
+            if j is None:
+                j = pos[m] = len(table)
+                table.append(m)
+            midx[i] = j
+        blob, offs = _offsets(table)
+        st = _status_array(n)
+        kidx = (ctypes.c_uint32 * max(n, 1))(*key_idx)
+        _check(self.lib.hipbls_batch_verify_rlc_keys(kidx, b"".join(sigs), midx, n, blob, offs, len(table), seed, st),
+               self.lib)
         return list(st)[:n]
 
     def rlc_stats(self) -> Tuple[int, int, int]:

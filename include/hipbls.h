@@ -15,6 +15,9 @@
  *   hipbls_aggregate                   tbls.Implementation.Aggregate         tbls/tbls.go:65-67, tbls/herumi.go:220-242
  *   hipbls_threshold_split             tbls.Implementation.ThresholdSplit[Insecure] tbls/tbls.go:40-47, tbls/herumi.go:84-181
  *   hipbls_recover_secret              tbls.Implementation.RecoverSecret     tbls/tbls.go:49, tbls/herumi.go:183-218
+ *   hipbls_pubshare_table_load         the pubshare set charon builds from the cluster lock at startup
+ *                                      (app/app.go:343-381, core/parsigex/parsigex.go:139-163 lookup)
+ *   hipbls_verify_batch_keys           tbls.Verify with that pubshare (tbls/herumi.go:285-301)
  *   hipbls_batch_verify_rlc            many tbls.Verify calls at once: the per-item loops of
  *                                      core/parsigex/parsigex.go:139-163, core/validatorapi/validatorapi.go:246-283,
  *                                      core/sigagg/sigagg.go:138-159 (optional BatchVerifier extension)
@@ -48,7 +51,7 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 2
+#define HIPBLS_ABI_VERSION 3
 int hipbls_abi_version(void);
 
 /* Select the HIP device used by the calling process (one process per GPU); idempotent.
@@ -110,6 +113,20 @@ int hipbls_recover_secret(const uint8_t* shares, const uint32_t* ids, uint32_t n
 int hipbls_batch_verify_rlc(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
                             const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs, const uint8_t* seed32,
                             int32_t* status);
+/* Resident pubshare table: decode + subgroup-check n public keys once and keep
+ * them in HBM; replaces the previous table.  status[k] = OK | ERR_PUBKEY (an infinity key loads and
+ * later verifies as ERR_VERIFY, like Verify).  The *_keys entry points name keys by table index and
+ * return exactly what the wire-format calls return for the same key bytes. */
+int hipbls_pubshare_table_load(const uint8_t* pks, uint64_t n, int32_t* status);
+int hipbls_pubshare_table_size(uint64_t* n);
+/* hipbls_verify_batch with pks[i] = table[key_idx[i]]; HIPBLS_ERR_ARG when an index is outside the table. */
+int hipbls_verify_batch_keys(const uint32_t* key_idx, const uint8_t* msgs, const uint64_t* msg_offsets,
+                             const uint8_t* sigs, uint64_t n, int32_t* status);
+/* hipbls_batch_verify_rlc with pks[i] = table[key_idx[i]]. */
+int hipbls_batch_verify_rlc_keys(const uint32_t* key_idx, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
+                                 const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs,
+                                 const uint8_t* seed32, int32_t* status);
+
 /* Windows checked, windows that failed, and items re-verified one by one in the last RLC call
  * (synchronizes the device). */
 int hipbls_rlc_stats(uint64_t* windows, uint64_t* windows_failed, uint64_t* items_fallback);
@@ -133,8 +150,16 @@ int hipbls_batch_verify_rlc_device(const uint8_t* d_pks, const uint8_t* d_sigs, 
                                    const uint8_t* d_msgs, const uint64_t* d_msg_offsets, uint64_t n_msgs,
                                    const uint8_t* seed32, int32_t* d_status, void* stream);
 
+/* Device variants of the *_keys calls: an out-of-range key or message index yields
+ * status[i] = HIPBLS_ERR_ARG. */
+int hipbls_verify_batch_keys_device(const uint32_t* d_key_idx, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
+                                    const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream);
+int hipbls_batch_verify_rlc_keys_device(const uint32_t* d_key_idx, const uint8_t* d_sigs, const uint32_t* d_msg_idx,
+                                        uint64_t n, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
+                                        uint64_t n_msgs, const uint8_t* seed32, int32_t* d_status, void* stream);
+
 /* Average duration (ms) per launch of a kernel over the calls since the last reset, measured with HIP
- * events on the stream it runs on (bench.py roofline).  Names: "verify" (k_verify_fused),
+ * events on the stream it runs on (bench.py roofline).  Names: "verify" (k_verify_fused), "verify_keys",
  * "rlc_items", "rlc_hash", "rlc_window", "rlc_fallback". */
 int hipbls_kernel_timing(const char* name, double* avg_ms, uint64_t* launches);
 int hipbls_kernel_timing_reset(void);

@@ -276,3 +276,49 @@ extern "C" int ht_rlc_verify(const uint8_t* pks, const uint8_t* sigs, const uint
     }
   return 0;
 }
+
+// Same pipeline with the public keys from a resident pubshare table (tab_pks, T) by key_idx.
+extern "C" int ht_rlc_verify_keys(const uint8_t* tab_pks, uint64_t T, const uint32_t* key_idx, const uint8_t* sigs,
+                                  const uint32_t* msg_idx, uint64_t n, const uint8_t* msgs, const uint64_t* offs,
+                                  uint64_t n_msgs, const uint8_t* seed32, int32_t* status, int32_t* tab_status,
+                                  uint64_t* stats3) {
+  std::vector<int32_t> code(T);
+  std::vector<uint32_t> tab(T * PUBTAB_WORDS);
+  for (uint64_t k = 0; k < T; ++k) tab_status[k] = pubtab_load_lane(k, tab_pks, T, code.data(), tab.data());
+  rlc_seed seed;
+  for (int k = 0; k < 8; ++k)
+    seed.w[k] = (uint32_t)seed32[4 * k] << 24 | (uint32_t)seed32[4 * k + 1] << 16 | (uint32_t)seed32[4 * k + 2] << 8 |
+                (uint32_t)seed32[4 * k + 3];
+  const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
+  std::vector<uint32_t> rpk(n * 36), rsig(n * 72), H((n_msgs ? n_msgs : 1) * 48);
+  std::vector<int32_t> win(n_win);
+  for (uint64_t i = 0; i < n; ++i)
+    rlc_items_lane(i, nullptr, sigs, msg_idx, n, n_msgs, seed, rpk.data(), rsig.data(), status, key_idx, T,
+                   code.data(), tab.data());
+  for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, n_msgs, H.data());
+  std::vector<uint32_t> list;
+  for (uint64_t w = 0; w < n_win; ++w)
+    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, status, win.data()))
+      for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
+        if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
+  for (uint32_t i : list) rlc_fallback_lane(i, nullptr, sigs, msg_idx, H.data(), n_msgs, status, key_idx, T, tab.data());
+  stats3[0] = n_win;
+  stats3[1] = stats3[2] = 0;
+  for (int32_t x : win)
+    if (x > 0) {
+      stats3[1] += 1;
+      stats3[2] += (uint64_t)x;
+    }
+  return 0;
+}
+
+// tbls.Verify with the key from a table (k_verify_keys body)
+extern "C" int ht_verify_key(const uint8_t* pk48, const uint8_t* msg, uint32_t len, const uint8_t* sig) {
+  int32_t code;
+  uint32_t tab[PUBTAB_WORDS];
+  pubtab_load_lane(0, pk48, 1, &code, tab);
+  g1a pk;
+  g1j xpk;
+  const int dp = pubtab_get(pk, xpk, 0, 1, &code, tab);
+  return op_verify_decoded_pk(dp, pk, msg, len, sig);
+}

@@ -105,3 +105,31 @@ def test_rlc_large_properties(impl):
     assert windows == n // 8
     assert failed == len({i // 8 for i in bad})
     assert fallback == 8 * failed
+
+
+# ---------------------------------------------------------------- resident pubshare table (§8f.2)
+def test_pubshare_table_verify_and_rlc_match_wire(impl):
+    """Keys by table index give exactly the wire-format statuses (Verify and RLC), including a bad
+    table entry, an infinity key and an index outside the table (argument error)."""
+    from tests.rlc_cases import fixture_batch
+    pks, msgs, sigs, want = fixture_batch()
+    table = list(dict.fromkeys(pks))  # distinct keys, first-seen order
+    tst = impl.load_pubshares(table)
+    assert tst == [1 if impl.batch_verify_status([k], [b"x"], [sigs[0]])[0] == 1 else 0 for k in table]
+    kidx = [table.index(p) for p in pks]
+    assert impl.batch_verify_keys_status(kidx, msgs, sigs) == want
+    assert impl.batch_verify_rlc_keys_status(kidx, msgs, sigs) == want
+    with pytest.raises(ValueError):
+        impl.batch_verify_keys_status([len(table)], [msgs[0]], [sigs[0]])
+
+
+def test_pubshare_table_large(impl):
+    sign, pk = sign_batch_fns(impl)
+    pks, msgs, sigs, _ = validator_batch(sign, pk, 64, 4, seed=31, bad=(3, 100, 200))
+    table = sorted(set(pks))
+    assert set(impl.load_pubshares(table)) == {0}
+    kidx = [table.index(p) for p in pks]
+    wire = impl.batch_verify_status(pks, msgs, sigs)
+    assert impl.batch_verify_keys_status(kidx, msgs, sigs) == wire
+    assert impl.batch_verify_rlc_keys_status(kidx, msgs, sigs) == wire
+    assert impl.batch_verify_rlc_status(pks, msgs, sigs) == wire

@@ -81,3 +81,47 @@ def test_rlc_seed_independent():
     a, _ = rlc(L, pks, msgs, sigs, seed=bytes(32))
     b, _ = rlc(L, pks, msgs, sigs, seed=b"\xff" * 32)
     assert a == b
+
+
+def rlc_keys(L, table_pks, key_idx, msgs, sigs, seed=SEED):
+    table, idx = message_table(msgs)
+    n = len(sigs)
+    offs = (ctypes.c_uint64 * (len(table) + 1))()
+    acc = 0
+    for m, t in enumerate(table):
+        offs[m] = acc
+        acc += len(t)
+    offs[len(table)] = acc
+    st = (ctypes.c_int32 * max(n, 1))()
+    tst = (ctypes.c_int32 * max(len(table_pks), 1))()
+    stats = (ctypes.c_uint64 * 3)()
+    rc = L.ht_rlc_verify_keys(b"".join(table_pks), ctypes.c_uint64(len(table_pks)),
+                              (ctypes.c_uint32 * max(n, 1))(*key_idx), b"".join(sigs),
+                              (ctypes.c_uint32 * max(n, 1))(*idx), ctypes.c_uint64(n), b"".join(table), offs,
+                              ctypes.c_uint64(len(table)), seed, st, tst, stats)
+    assert rc == 0
+    return [st[i] for i in range(n)], [tst[i] for i in range(len(table_pks))], list(stats)
+
+
+def test_pubshare_table_verify_matches_wire_verify():
+    """k_verify_keys body: key from the decoded table == op_verify on the wire key (fixtures)."""
+    L = lib()
+    pks, msgs, sigs, want = fixture_batch()
+    got = [L.ht_verify_key(p, m, len(m), s) for p, m, s in zip(pks, msgs, sigs)]
+    assert got == want
+
+
+def test_rlc_with_pubshare_table():
+    """Keys by table index (shuffled table, repeated keys, one bad table entry) == per-item Verify."""
+    L = lib()
+    pks, msgs, sigs, _ = validator_batch(host_sign(L), host_pk(L), 4, 4, seed=17, bad=(6,))
+    order = list(range(len(pks)))[::-1]
+    table_pks = [pks[i] for i in order] + [bytes(48)]       # last entry: not a valid encoding
+    key_idx = [len(pks) - 1 - i for i in range(len(pks))]
+    key_idx[11] = len(pks)                                   # item 11 names the bad key
+    got, tst, (windows, failed, fallback) = rlc_keys(L, table_pks, key_idx, msgs, sigs)
+    assert tst == [0] * len(pks) + [1]
+    wire = [bls.verify_status(table_pks[k], m, s) for k, m, s in zip(key_idx, msgs, sigs)]
+    assert got == wire
+    assert got[11] == 1 and got[6] == 3 and got.count(0) == 14
+    assert windows == 2 and failed == 1
