@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--rlc-validators", type=int, default=32768,
                     help="C4 validators per GPU (x4 partials; 32,768 = the 1M-partial node batch / 8 GPUs; 0 = skip)")
     ap.add_argument("--rlc-steps", type=int, default=3)
+    ap.add_argument("--c5", type=int, default=1, help="time the C5 full-slot mix (0 = skip)")
     ap.add_argument("--keys", type=int, default=1, help="also time C2 / C4 with the resident pubshare table (0 = skip)")
     ap.add_argument("--rlc-big-validators", type=int, default=262144,
                     help="also time one GPU on the whole C4 node batch (262,144 x 4 = 1M partials; 0 = skip)")
@@ -412,6 +413,76 @@ def main():
                     n4 * args.rlc_steps * world / float(tt.item()), 1)
             del d_pk4, d_sig4, d_midx4, d_msg4, d_off4, d_st4
 
+    # ---- C5: full-slot mix on this rank's shard: RLC over the C4 shard + 32 validators x 4 proposer
+    # partials (own roots), concurrently with a 512-key sync-committee FastAggregateVerify
+    c5 = None
+    if args.c5 and args.rlc_validators > 0:
+        t0 = time.time()
+        pks5, sigs5, midx5, roots5, bad5 = make_c4(impl, args.rlc_validators, rng)
+        ppks, psigs, pmidx, proots, pbad = make_c4(impl, 32, rng, nkeys=128)
+        off = len(roots5)
+        base = len(pks5)
+        pks5 += ppks
+        sigs5 += psigs
+        midx5 += [m + off for m in pmidx]
+        roots5 += proots
+        bad5 |= {base + i for i in pbad}
+        n5 = len(pks5)
+        sync_sks = [rng.randrange(1, R_ORDER).to_bytes(32, "big") for _ in range(512)]
+        sync_pks, _ = impl.secret_to_public_key_batch(sync_sks)
+        sync_root = rng.randbytes(32)
+        ssigs, _ = impl.sign_batch(sync_sks, [sync_root] * 512)
+        sync_agg = impl.aggregate(ssigs)
+        log("rank %d: C5 data (%d partials + 512-key sync aggregate) in %.1fs" % (rank, n5, time.time() - t0))
+        d_pk5 = torch.frombuffer(bytearray(b"".join(pks5)), dtype=torch.uint8).to(dev)
+        d_sig5 = torch.frombuffer(bytearray(b"".join(sigs5)), dtype=torch.uint8).to(dev)
+        d_midx5 = torch.tensor(midx5, dtype=torch.int32).to(dev)
+        d_msg5 = torch.frombuffer(bytearray(b"".join(roots5)), dtype=torch.uint8).to(dev)
+        d_off5 = torch.arange(0, 32 * (len(roots5) + 1), 32, dtype=torch.int64).to(dev)
+        d_st5 = torch.full((n5,), -7, dtype=torch.int32, device=dev)
+        d_spk = torch.frombuffer(bytearray(b"".join(sync_pks)), dtype=torch.uint8).to(dev)
+        d_skoff = torch.tensor([0, 512], dtype=torch.int64).to(dev)
+        d_ssig = torch.frombuffer(bytearray(sync_agg), dtype=torch.uint8).to(dev)
+        d_smsg = torch.frombuffer(bytearray(sync_root), dtype=torch.uint8).to(dev)
+        d_smoff = torch.tensor([0, 32], dtype=torch.int64).to(dev)
+        d_sst = torch.full((1,), -7, dtype=torch.int32, device=dev)
+        seed5 = os.urandom(32)
+
+        def c5step():
+            # the sync-committee check goes on the library's own stream (NULL) and overlaps the RLC
+            rc = lib.hipbls_verify_aggregate_batch_device(d_spk.data_ptr(), 512, d_skoff.data_ptr(), 1,
+                                                          d_ssig.data_ptr(), d_smsg.data_ptr(), d_smoff.data_ptr(),
+                                                          d_sst.data_ptr(), None)
+            assert rc == 0
+            rc = lib.hipbls_batch_verify_rlc_device(d_pk5.data_ptr(), d_sig5.data_ptr(), d_midx5.data_ptr(), n5,
+                                                    d_msg5.data_ptr(), d_off5.data_ptr(), len(roots5), seed5,
+                                                    d_st5.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+            assert rc == 0
+
+        c5step()
+        torch.cuda.synchronize()
+        barrier()
+        ts = time.perf_counter()
+        for _ in range(args.rlc_steps):
+            c5step()
+        torch.cuda.synchronize()
+        barrier()
+        t5 = time.perf_counter() - ts
+        assert {i for i, x in enumerate(d_st5.cpu().tolist()) if x != 0} == bad5, "C5 bitmap mismatch"
+        assert d_sst.cpu().tolist() == [0], "sync-committee FastAggregateVerify failed"
+        tt = torch.tensor([t5], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t5 = float(tt.item())
+        c5 = {"workload": "C5 (BASELINE configs[4]) per GPU: RLC BatchVerify of the C4 shard (%d validators x 4, "
+                          "one root each) + 32 validators x 4 proposer partials (own roots), 1%% corrupted, with a "
+                          "512-key sync-committee FastAggregateVerify (hash-to-G2 of its root) overlapped"
+                          % args.rlc_validators,
+              "partials_per_slot_per_gpu": n5, "ms_per_slot": round(1000 * t5 / args.rlc_steps, 3),
+              "verified_partial_sigs_per_s": round(n5 * args.rlc_steps * world / t5, 1),
+              "sync_aggregate_verifies_per_s": round(args.rlc_steps * world / t5, 3)}
+        del d_pk5, d_sig5, d_midx5, d_msg5, d_off5, d_st5
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -436,6 +507,8 @@ def main():
             "threshold_aggregate_workload": "C3: %d validators x 7-of-10 Lagrange in G2 + Verify of each aggregate per GPU"
                                             % args.tagg_groups if tagg else None,
         }
+        if c5:
+            out["full_slot_mix"] = c5
         if rlc:
             out["rlc_batch_verify"] = dict(rlc, workload="C4 (BASELINE configs[3]): validators x 4 partials per GPU, "
                                                         "items grouped by validator, 1%% corrupted (swapped share / "

@@ -146,50 +146,107 @@ __global__ void __launch_bounds__(kBlock) k_g1_decode(const uint8_t* __restrict_
   code[i] = st;
 }
 
-// FastAggregateVerify tail: one lane sums the decoded keys, hashes, pairs.
-__global__ void __launch_bounds__(kBlock) k_fast_aggregate_verify_tail(const uint32_t* __restrict__ pts, const int32_t* __restrict__ code,
-                                             uint64_t n, const uint8_t* __restrict__ sig,
-                                             const uint8_t* __restrict__ msg, uint64_t msg_len,
-                                             int32_t* __restrict__ status) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  g2a s;
-  const int ds = g2_decompress(s, sig, true);
-  if (ds == DEC_BAD) {
-    *status = HIPBLS_ERR_SIGNATURE;
-    return;
+// FastAggregateVerify (tbls/herumi.go:315-339), one workgroup of two waves per group g over keys
+// [goff[g], goff[g+1]) decoded by k_g1_decode: wave 0 sums the keys (strided, then an LDS tree),
+// wave 1 meanwhile decodes the signature and hashes the message; lane 0 then runs the pairing.
+// Status order follows the reference: signature decode error, then key decode error, then
+// "signature verification failed" (also for an empty key list, an infinity key or signature).
+constexpr int kFavBlock = 128;
+__global__ void __launch_bounds__(kFavBlock) k_fav_batch(const uint32_t* __restrict__ pts,
+                                                         const int32_t* __restrict__ code, uint64_t nkeys,
+                                                         const uint64_t* __restrict__ goff,
+                                                         const uint8_t* __restrict__ sigs,
+                                                         const uint8_t* __restrict__ msgs,
+                                                         const uint64_t* __restrict__ moffs,
+                                                         int32_t* __restrict__ status) {
+  __shared__ uint32_t red[64 * 36];
+  __shared__ uint32_t sh_sig[48], sh_hm[48];
+  __shared__ int sh_ds, sh_bad, sh_inf;
+  const uint64_t g = blockIdx.x;
+  const uint64_t k0 = goff[g], k1 = goff[g + 1];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    sh_bad = 0;
+    sh_inf = 0;
   }
-  for (uint64_t i = 0; i < n; ++i)
-    if (code[i] == DEC_BAD) {
-      *status = HIPBLS_ERR_PUBKEY;
-      return;
+  __syncthreads();
+  if (tid < 64) {
+    g1j acc;
+    jac_set_inf(acc);
+    int bad = 0, inf = 0;
+    for (uint64_t k = k0 + tid; k < k1; k += 64) {
+      const int c = code[k];
+      if (c == DEC_BAD) {
+        bad = 1;
+      } else if (c == DEC_INF) {
+        inf = 1;
+      } else {
+        g1a a;
+        soa_load<24>(&a.x.v[0], pts, nkeys, k);
+        jac_add_aff(acc, acc, a);
+      }
     }
-  if (n == 0 || ds == DEC_INF) {
-    *status = HIPBLS_ERR_VERIFY;
-    return;
-  }
-  g1j acc;
-  jac_set_inf(acc);
-  for (uint64_t i = 0; i < n; ++i) {
-    if (code[i] == DEC_INF) {
-      *status = HIPBLS_ERR_VERIFY;  // KeyValidate rejects the identity key
-      return;
+    if (bad) atomicOr(&sh_bad, 1);
+    if (inf) atomicOr(&sh_inf, 1);
+    for (int w = 0; w < 36; ++w) red[w * 64 + tid] = (&acc.x.v[0])[w];
+  } else if (tid == 64) {
+    g2a sg;
+    const int ds = g2_decompress(sg, sigs + 96 * g, true);
+    sh_ds = ds;
+    g2a hm;
+    if (ds == DEC_OK) {
+      g2j hj;
+      const uint64_t o0 = moffs[g], o1 = moffs[g + 1];
+      hash_to_g2(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43);
+      jac_to_aff(hm, hj);
+    } else {
+      fp2_set_zero(sg.x);
+      fp2_set_zero(sg.y);
+      hm = sg;
     }
-    g1a a;
-    uint32_t* dst = &a.x.v[0];
-    for (int w = 0; w < 24; ++w) dst[w] = pts[(uint64_t)w * n + i];
-    jac_add_aff(acc, acc, a);
+    for (int w = 0; w < 48; ++w) {
+      sh_sig[w] = (&sg.x.c0.v[0])[w];
+      sh_hm[w] = (&hm.x.c0.v[0])[w];
+    }
   }
-  if (jac_is_inf(acc)) {
-    *status = HIPBLS_ERR_VERIFY;
-    return;
+  __syncthreads();
+  for (int half = 32; half >= 1; half >>= 1) {  // every thread reaches every barrier
+    if (tid < half) {
+      g1j x, y;
+      for (int w = 0; w < 36; ++w) {
+        (&x.x.v[0])[w] = red[w * 64 + tid];
+        (&y.x.v[0])[w] = red[w * 64 + tid + half];
+      }
+      jac_add(x, x, y);
+      for (int w = 0; w < 36; ++w) red[w * 64 + tid] = (&x.x.v[0])[w];
+    }
+    __syncthreads();
   }
-  g1a pk;
-  jac_to_aff(pk, acc);
-  g2j hj;
-  hash_to_g2(hj, msg, (uint32_t)msg_len, DST_POP, 43);
-  g2a hm;
-  jac_to_aff(hm, hj);
-  *status = pairing_check_verify(pk, hm, s) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+  if (tid != 0) return;
+  int st;
+  if (sh_ds == DEC_BAD) {
+    st = HIPBLS_ERR_SIGNATURE;
+  } else if (sh_bad) {
+    st = HIPBLS_ERR_PUBKEY;
+  } else if (k1 == k0 || sh_ds == DEC_INF || sh_inf) {
+    st = HIPBLS_ERR_VERIFY;  // KeyValidate rejects the identity key; empty set is false [ext]
+  } else {
+    g1j sum;
+    for (int w = 0; w < 36; ++w) (&sum.x.v[0])[w] = red[w * 64];
+    if (jac_is_inf(sum)) {
+      st = HIPBLS_ERR_VERIFY;
+    } else {
+      g1a pk;
+      jac_to_aff(pk, sum);
+      g2a sg, hm;
+      for (int w = 0; w < 48; ++w) {
+        (&sg.x.c0.v[0])[w] = sh_sig[w];
+        (&hm.x.c0.v[0])[w] = sh_hm[w];
+      }
+      st = pairing_check_verify(pk, hm, sg) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+    }
+  }
+  status[g] = st;
 }
 
 __global__ void __launch_bounds__(kBlock) k_aggregate(const uint8_t* __restrict__ sigs, uint64_t n, uint8_t* __restrict__ out,
@@ -784,32 +841,74 @@ int hipbls_secret_to_public_key_batch_device(const uint8_t* d_sks, uint64_t n, u
   return HIPBLS_OK;
 }
 
-int hipbls_verify_aggregate(const uint8_t* pks, uint64_t n, const uint8_t* sig, const uint8_t* msg, uint64_t msg_len,
-                            int32_t* status) {
-  if (!sig || !status || (n && !pks) || (msg_len && !msg) || mul_overflows(n, 48)) return HIPBLS_ERR_ARG;
+int launch_fav(const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_goff, uint64_t n_groups, const uint8_t* d_sigs,
+               const uint8_t* d_msgs, const uint64_t* d_moffs, int32_t* d_status, hipStream_t s) {
+  Context& c = g_ctx;
+  if (n_groups == 0) return HIPBLS_OK;
+  HIP_TRY(c.b_pts.ensure((nkeys ? nkeys : 1) * 24 * 4));
+  HIP_TRY(c.b_pst.ensure((nkeys ? nkeys : 1) * 4));
+  if (nkeys)
+    hipLaunchKernelGGL(k_g1_decode, dim3((unsigned)grid_for(nkeys)), dim3(kBlock), 0, s, d_pks, nkeys,
+                       (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);
+  return timed("fav", s, [&] {
+    hipLaunchKernelGGL(k_fav_batch, dim3((unsigned)n_groups), dim3(kFavBlock), 0, s, (const uint32_t*)c.b_pts.p,
+                       (const int32_t*)c.b_pst.p, nkeys, d_goff, d_sigs, d_msgs, d_moffs, d_status);
+  });
+}
+
+int hipbls_verify_aggregate_batch(const uint8_t* pks, const uint64_t* key_offsets, uint64_t n_groups,
+                                  const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_offsets,
+                                  int32_t* status) {
+  if (n_groups == 0) return HIPBLS_OK;
+  if (!key_offsets || !sigs || !msg_offsets || !status || key_offsets[0] != 0 || msg_offsets[0] != 0 ||
+      mul_overflows(n_groups, 96))
+    return HIPBLS_ERR_ARG;
+  for (uint64_t g = 0; g < n_groups; ++g)
+    if (key_offsets[g + 1] < key_offsets[g] || msg_offsets[g + 1] < msg_offsets[g] ||
+        msg_offsets[g + 1] - msg_offsets[g] > 0xffffffffull)
+      return HIPBLS_ERR_ARG;
+  const uint64_t nkeys = key_offsets[n_groups], msg_total = msg_offsets[n_groups];
+  if ((nkeys && !pks) || (msg_total && !msgs) || mul_overflows(nkeys, 96)) return HIPBLS_ERR_ARG;
   int rc = ensure_init();
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(g_ctx.mu);
   Context& c = g_ctx;
-  HIP_TRY(c.b_pk.ensure((n ? n : 1) * 48));
-  HIP_TRY(c.b_sig.ensure(96));
-  HIP_TRY(c.b_msg.ensure(msg_len ? msg_len : 1));
-  HIP_TRY(c.b_pts.ensure((n ? n : 1) * 24 * 4));
-  HIP_TRY(c.b_pst.ensure((n ? n : 1) * 4));
-  HIP_TRY(c.b_st.ensure(4));
-  if (n) HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sig, 96, hipMemcpyHostToDevice, c.stream));
-  if (msg_len) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msg, msg_len, hipMemcpyHostToDevice, c.stream));
-  if (n)
-    hipLaunchKernelGGL(k_g1_decode, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_pk.p,
-                       n, (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);
-  hipLaunchKernelGGL(k_fast_aggregate_verify_tail, dim3(1), dim3(kBlock), 0, c.stream, (const uint32_t*)c.b_pts.p,
-                     (const int32_t*)c.b_pst.p, n, (const uint8_t*)c.b_sig.p, (const uint8_t*)c.b_msg.p, msg_len,
-                     (int32_t*)c.b_st.p);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(c.b_pk.ensure((nkeys ? nkeys : 1) * 48));
+  HIP_TRY(c.b_ids.ensure((n_groups + 1) * 8));
+  HIP_TRY(c.b_sig.ensure(n_groups * 96));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_off.ensure((n_groups + 1) * 8));
+  HIP_TRY(c.b_st.ensure(n_groups * 4));
+  if (nkeys) HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, nkeys * 48, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_ids.p, key_offsets, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_groups * 96, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  rc = launch_fav((const uint8_t*)c.b_pk.p, nkeys, (const uint64_t*)c.b_ids.p, n_groups, (const uint8_t*)c.b_sig.p,
+                  (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p, (int32_t*)c.b_st.p, c.stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
   HIP_TRY(hipStreamSynchronize(c.stream));
   return HIPBLS_OK;
+}
+
+int hipbls_verify_aggregate_batch_device(const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_key_offsets,
+                                         uint64_t n_groups, const uint8_t* d_sigs, const uint8_t* d_msgs,
+                                         const uint64_t* d_msg_offsets, int32_t* d_status, void* stream) {
+  if (n_groups == 0) return HIPBLS_OK;
+  int rc = ensure_init();
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  return launch_fav(d_pks, nkeys, d_key_offsets, n_groups, d_sigs, d_msgs, d_msg_offsets, d_status,
+                    stream ? (hipStream_t)stream : g_ctx.stream);
+}
+
+int hipbls_verify_aggregate(const uint8_t* pks, uint64_t n, const uint8_t* sig, const uint8_t* msg, uint64_t msg_len,
+                            int32_t* status) {
+  if (!sig || !status || (n && !pks) || (msg_len && !msg) || mul_overflows(n, 48)) return HIPBLS_ERR_ARG;
+  const uint64_t koff[2] = {0, n}, moff[2] = {0, msg_len};
+  static const uint8_t empty = 0;
+  return hipbls_verify_aggregate_batch(n ? pks : &empty, koff, 1, sig, msg_len ? msg : &empty, moff, status);
 }
 
 int hipbls_aggregate(const uint8_t* sigs, uint64_t n, uint8_t* out_sig, int32_t* status) {

@@ -78,6 +78,8 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_batch_verify_rlc_device": ([vp, vp, vp, u64, vp, vp, u64, u8p, vp, vp], ctypes.c_int),
         "hipbls_rlc_stats": ([u64p, u64p, u64p], ctypes.c_int),
         "hipbls_pubshare_table_load": ([u8p, u64, i32p], ctypes.c_int),
+        "hipbls_verify_aggregate_batch": ([u8p, u64p, u64, u8p, u8p, u64p, i32p], ctypes.c_int),
+        "hipbls_verify_aggregate_batch_device": ([vp, u64, vp, u64, vp, vp, vp, vp, vp], ctypes.c_int),
         "hipbls_pubshare_table_size": ([u64p], ctypes.c_int),
         "hipbls_verify_batch_keys": ([u32p, u8p, u64p, u8p, u64, i32p], ctypes.c_int),
         "hipbls_batch_verify_rlc_keys": ([u32p, u8p, u32p, u64, u8p, u64p, u64, u8p, i32p], ctypes.c_int),
@@ -103,7 +105,8 @@ def exported_symbols() -> List[str]:
         "hipbls_threshold_aggregate_batch_device", "hipbls_sign_batch_device",
         "hipbls_secret_to_public_key_batch_device", "hipbls_kernel_timing", "hipbls_kernel_timing_reset",
         "hipbls_batch_verify_rlc", "hipbls_batch_verify_rlc_device", "hipbls_rlc_stats",
-        "hipbls_pubshare_table_load", "hipbls_pubshare_table_size", "hipbls_verify_batch_keys",
+        "hipbls_pubshare_table_load", "hipbls_pubshare_table_size", "hipbls_verify_aggregate_batch",
+        "hipbls_verify_aggregate_batch_device", "hipbls_verify_batch_keys",
         "hipbls_batch_verify_rlc_keys", "hipbls_verify_batch_keys_device", "hipbls_batch_verify_rlc_keys_device",
     ]
 
@@ -373,6 +376,22 @@ class HipBLS:
             raise TBLSError("cannot set compressed public key in Herumi format")
         if st[0] != OK:
             raise TBLSError("signature verification failed")
+
+    def batch_verify_aggregate_status(self, groups: Sequence[Tuple[Sequence[bytes], bytes, bytes]]) -> List[int]:
+        """One FastAggregateVerify per (shares, signature, data) group in one launch; per-group status
+        (OK / ERR_SIGNATURE / ERR_PUBKEY / ERR_VERIFY, as verify_aggregate raises)."""
+        g = len(groups)
+        koffs = (ctypes.c_uint64 * (g + 1))()
+        keys: List[bytes] = []
+        for j, (shares, _, _) in enumerate(groups):
+            koffs[j] = len(keys)
+            keys.extend(bytes(s) for s in shares)
+        koffs[g] = len(keys)
+        blob, moffs = _offsets([bytes(d) for _, _, d in groups])
+        st = _status_array(g)
+        _check(self.lib.hipbls_verify_aggregate_batch(b"".join(keys), koffs, g, b"".join(bytes(s) for _, s, _ in groups),
+                                                      blob, moffs, st), self.lib)
+        return list(st)[:g]
 
     def aggregate(self, signs: Sequence[bytes]) -> bytes:
         """herumi.go:220-242."""

@@ -11,7 +11,7 @@
  *   hipbls_threshold_aggregate_batch   tbls.Implementation.ThresholdAggregate tbls/tbls.go:50-51, tbls/herumi.go:244-283
  *   hipbls_sign_batch                  tbls.Implementation.Sign              tbls/tbls.go:57-59, tbls/herumi.go:303-313
  *   hipbls_secret_to_public_key_batch  tbls.Implementation.SecretToPublicKey tbls/tbls.go:36-38, tbls/herumi.go:67-80
- *   hipbls_verify_aggregate            tbls.Implementation.VerifyAggregate   tbls/tbls.go:61-63, tbls/herumi.go:315-339
+ *   hipbls_verify_aggregate[_batch]    tbls.Implementation.VerifyAggregate   tbls/tbls.go:61-63, tbls/herumi.go:315-339
  *   hipbls_aggregate                   tbls.Implementation.Aggregate         tbls/tbls.go:65-67, tbls/herumi.go:220-242
  *   hipbls_threshold_split             tbls.Implementation.ThresholdSplit[Insecure] tbls/tbls.go:40-47, tbls/herumi.go:84-181
  *   hipbls_recover_secret              tbls.Implementation.RecoverSecret     tbls/tbls.go:49, tbls/herumi.go:183-218
@@ -51,7 +51,7 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 3
+#define HIPBLS_ABI_VERSION 4
 int hipbls_abi_version(void);
 
 /* Select the HIP device used by the calling process (one process per GPU); idempotent.
@@ -88,6 +88,14 @@ int hipbls_secret_to_public_key_batch(const uint8_t* sks, uint64_t n, uint8_t* o
 /* FastAggregateVerify(pks[0..n), sig, msg).  *status = OK | ERR_PUBKEY | ERR_SIGNATURE | ERR_VERIFY. */
 int hipbls_verify_aggregate(const uint8_t* pks, uint64_t n, const uint8_t* sig, const uint8_t* msg,
                             uint64_t msg_len, int32_t* status);
+
+/* n_groups FastAggregateVerify calls in one launch: group g checks sigs[96 g ..] over message
+ * msgs[msg_offsets[g] .. msg_offsets[g+1]) against the keys pks[48 k ..], k in
+ * [key_offsets[g], key_offsets[g+1]).  status[g] as hipbls_verify_aggregate.  Sync-committee and
+ * cluster-lock checks (cluster/lock.go:178,267) batch this way. */
+int hipbls_verify_aggregate_batch(const uint8_t* pks, const uint64_t* key_offsets, uint64_t n_groups,
+                                  const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_offsets,
+                                  int32_t* status);
 
 /* Plain G2 sum of n signatures.  *status = OK | ERR_SIGNATURE | ERR_COMBINE (n == 0). */
 int hipbls_aggregate(const uint8_t* sigs, uint64_t n, uint8_t* out_sig, int32_t* status);
@@ -149,6 +157,11 @@ int hipbls_secret_to_public_key_batch_device(const uint8_t* d_sks, uint64_t n, u
 int hipbls_batch_verify_rlc_device(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_msg_idx, uint64_t n,
                                    const uint8_t* d_msgs, const uint64_t* d_msg_offsets, uint64_t n_msgs,
                                    const uint8_t* seed32, int32_t* d_status, void* stream);
+
+/* Device variant of hipbls_verify_aggregate_batch (nkeys = key_offsets[n_groups], passed explicitly). */
+int hipbls_verify_aggregate_batch_device(const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_key_offsets,
+                                         uint64_t n_groups, const uint8_t* d_sigs, const uint8_t* d_msgs,
+                                         const uint64_t* d_msg_offsets, int32_t* d_status, void* stream);
 
 /* Device variants of the *_keys calls: an out-of-range key or message index yields
  * status[i] = HIPBLS_ERR_ARG. */

@@ -186,3 +186,42 @@ def test_batch_verify_large_properties(impl):
     got = impl.batch_verify_status([pks[o] for o in owner], vm, sigs)
     assert [i for i, s in enumerate(got) if s != 0] == sorted(bad)
     assert all(got[i] == 3 for i in bad)
+
+
+# ---------------------------------------------------------------- batched FastAggregateVerify
+def test_batch_verify_aggregate_vs_oracle(impl):
+    """Several FastAggregateVerify groups in one launch == oracle.verify_aggregate per group,
+    including the error order (signature, then key), empty and infinity cases, and a group wider than
+    one wave (strided key sum + LDS tree)."""
+    from oracle import bls12381 as bls
+    rng = random.Random(41)
+    sks = [rng.randrange(1, 2 ** 254).to_bytes(32, "big") for _ in range(70)]
+    pks, _ = impl.secret_to_public_key_batch(sks)
+    msg = b"sync committee root".ljust(32, b"\0")
+    sigs, _ = impl.sign_batch(sks, [msg] * 70)
+    agg3 = impl.aggregate(sigs[:3])
+    agg70 = impl.aggregate(sigs)
+    bad_sig = bytearray(agg3)
+    bad_sig[0] &= 0x7F
+    inf_pk = bytes([0xC0]) + bytes(47)
+    groups = [
+        (pks[:3], agg3, msg),                  # valid
+        (pks[:3], agg3, msg[::-1]),            # wrong message
+        (pks[:3], bytes(bad_sig), msg),        # signature encoding error wins
+        ([pks[0], bytes(48), pks[2]], agg3, msg),  # key encoding error
+        ([], agg3, msg),                       # empty set
+        (pks[:3] + [inf_pk], agg3, msg),       # identity key
+        (pks, agg70, msg),                     # 70 keys
+        (pks[:69], agg70, msg),                # one key missing
+    ]
+    got = impl.batch_verify_aggregate_status(groups)
+
+    def want(shares, sig, data):
+        try:
+            bls.verify_aggregate(shares, sig, data)
+            return 0
+        except bls.BLSError as e:
+            return {"cannot unmarshal signature into Herumi signature": 2,
+                    "cannot set compressed public key in Herumi format": 1}.get(str(e), 3)
+    assert got == [0, 3, 2, 1, 3, 3, 0, 3]
+    assert got[:6] == [want(*g) for g in groups[:6]]
