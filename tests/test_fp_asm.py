@@ -1,0 +1,51 @@
+"""The gfx950 Montgomery product is hand-written asm (charon_amd/tools/gen_fp_asm.py), which the host
+build never runs.  These CPU tests interpret the EMITTED instruction stream (the text inside
+charon_amd/csrc/fp_asm_gfx950.h) lane-scalar and compare it with Python big-integer Montgomery
+products, so a schedule change is checked here before it reaches a GPU.  The GPU parity tests then
+cover it end to end through every curve and pairing result."""
+import os
+import random
+import re
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "charon_amd", "tools"))
+import gen_fp_asm as g  # noqa: E402
+
+R_INV = pow(pow(2, 384, g.P), -1, g.P)
+
+
+def _limbs(x):
+    return [(x >> (32 * i)) & 0xFFFFFFFF for i in range(12)]
+
+
+def _val(limbs):
+    return sum(v << (32 * i) for i, v in enumerate(limbs))
+
+
+def _header_body():
+    text = open(os.path.join(ROOT, "charon_amd", "csrc", "fp_asm_gfx950.h")).read()
+    return [s.replace("\\n\\t", "") for s in re.findall(r'^\s+"([^"]*)"', text, re.M)]
+
+
+def _cases(n, seed):
+    rnd = random.Random(seed)
+    edge = [0, 1, 2, g.P - 1, g.P - 2, (g.P - 1) // 2, (1 << 380), g.P - (1 << 32)]
+    return edge + [rnd.randrange(g.P) for _ in range(n)]
+
+
+def test_header_matches_generator():
+    assert _header_body() == g.gen_mul(), "fp_asm_gfx950.h is stale: rerun charon_amd/tools/gen_fp_asm.py"
+
+
+@pytest.mark.parametrize("body_name", ["emitted", "two_chain_experiment"])
+def test_product_schedule_is_montgomery(body_name):
+    body = _header_body() if body_name == "emitted" else g.gen_mul2()
+    cases = _cases(400, 7)
+    rnd = random.Random(8)
+    for a in cases:
+        for b in (a, rnd.choice(cases)):
+            got = _val(g.emulate(body, _limbs(a), _limbs(b)))
+            assert got == a * b * R_INV % g.P, (hex(a), hex(b))
