@@ -352,6 +352,59 @@ BLS_HD BLS_CALL void g2_clear_cofactor(g2j& r, const g2j& p) {
   jac_add(r, t3, np);
 }
 
+// k (8 little-endian limbs, k < 2^256) -> k / |x| in place; returns k mod |x|.  Bitwise long
+// division: 256 shift-subtract steps on a 64-bit remainder (|x| < 2^64; when the remainder's top
+// bit is set, 2*rem + b exceeds |x| and the wrapped difference is exact).
+BLS_HD BLS_INLINE uint64_t u256_divmod_xabs(uint32_t* k) {
+  uint64_t rem = 0;
+  for (int w = 7; w >= 0; --w) {
+    uint32_t q = 0;
+    for (int b = 31; b >= 0; --b) {
+      const uint64_t top = rem >> 63;
+      rem = (rem << 1) | ((k[w] >> b) & 1u);
+      if (top || rem >= X_ABS) {
+        rem -= X_ABS;
+        q |= 1u << b;
+      }
+    }
+    k[w] = q;
+  }
+  return rem;
+}
+
+// r = [k] P for P in G2 (subgroup-checked) and a plain scalar k < r, 4-dimensional GLS split.
+// On G2, psi = [x] and x = -|x|, so with k = e0 + e1|x| + e2|x|^2 + e3|x|^3 (base-|x| digits,
+// r < |x|^4) [k]P = sum_i e_i (-psi)^i(P): 64 doublings and <= 64 additions over a 16-entry
+// subset-sum table instead of a 255-bit double-and-add.
+BLS_HD BLS_CALL void g2_mul_glv4(g2j& r, const g2j& p, const uint32_t* k_plain) {
+  uint32_t k[8];
+  for (int i = 0; i < 8; ++i) k[i] = k_plain[i];
+  uint64_t e[4];
+  for (int i = 0; i < 3; ++i) e[i] = u256_divmod_xabs(k);
+  e[3] = (uint64_t)k[0] | ((uint64_t)k[1] << 32);
+  g2j tab[16];
+  jac_set_inf(tab[0]);
+  tab[1] = p;                   // P
+  g2_psi(tab[2], tab[1]);
+  jac_neg(tab[2], tab[2]);      // -psi(P)
+  g2_psi2(tab[4], tab[1]);      // psi^2(P)
+  g2_psi(tab[8], tab[4]);
+  jac_neg(tab[8], tab[8]);      // -psi^3(P)
+  for (int d = 3; d < 16; ++d) {
+    const int low = d & -d;
+    if (d != low) jac_add(tab[d], tab[d ^ low], tab[low]);
+  }
+  g2j acc;
+  jac_set_inf(acc);
+  for (int bit = 63; bit >= 0; --bit) {
+    jac_dbl(acc, acc);
+    const int d = (int)((e[0] >> bit) & 1u) | (int)(((e[1] >> bit) & 1u) << 1) |
+                  (int)(((e[2] >> bit) & 1u) << 2) | (int)(((e[3] >> bit) & 1u) << 3);
+    if (d) jac_add(acc, acc, tab[d]);
+  }
+  r = acc;
+}
+
 BLS_HD BLS_CALL bool fp2_sqrt(fp2& r, const fp2& a) {
   // a = a0 + a1 u: s = sqrt(a0^2 + a1^2), t = (a0 + s)/2, then sqrt(a) = x0 + a1/(2 x0) u with
   // x0^2 = t, or a1/(2 x0) + x0 u with x0^2 = -t when t is not a square.  One power

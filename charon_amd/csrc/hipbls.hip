@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(kBlock) k_tagg_scale(const uint8_t* __restrict
     lagrange_at_zero(lam, ids + g0, t, me);
     g2j sj;
     jac_from_aff(sj, s);
-    jac_mul_limbs(acc, sj, lam.v, 8);
+    g2_mul_glv4(acc, sj, lam.v);
   }
   const uint32_t* src = &acc.x.c0.v[0];
   for (int w = 0; w < 72; ++w) pts[(uint64_t)w * n_parts + k] = src[w];

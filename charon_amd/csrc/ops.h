@@ -73,7 +73,7 @@ BLS_HD BLS_CALL int op_sign(uint8_t* out96, const uint8_t* sk32, const uint8_t* 
   if (!fr_plain_from_be32(sk, sk32)) return HIPBLS_ERR_SECRET;
   g2j h, s;
   hash_to_g2(h, msg, msg_len, DST_POP, 43);
-  jac_mul_limbs(s, h, sk.v, 8);
+  g2_mul_glv4(s, h, sk.v);
   g2_compress(out96, s);
   return HIPBLS_OK;
 }

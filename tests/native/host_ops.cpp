@@ -206,11 +206,27 @@ int ht_threshold_aggregate(const uint8_t* sigs, const uint32_t* ids, int n, uint
     fr lam;
     lagrange_at_zero(lam, ids, n, i);
     g2j t;
-    jac_mul_limbs(t, sj, lam.v, 8);
+    g2_mul_glv4(t, sj, lam.v);
     jac_add(acc, acc, t);
   }
   g2_compress(out96, acc);
   return HIPBLS_OK;
+}
+
+// [k] P on G2 by the 4-dimensional GLS split (k: 8 plain little-endian limbs) or, with glv = 0,
+// by plain double-and-add; P is a subgroup-checked compressed point.  Returns the decode status.
+int ht_g2_mul(const uint8_t* p96, const uint32_t* k8, int glv, uint8_t* out96) {
+  g2a a;
+  const int st = g2_decompress(a, p96, true);
+  if (st != DEC_OK) return st;
+  g2j pj, r;
+  jac_from_aff(pj, a);
+  if (glv)
+    g2_mul_glv4(r, pj, k8);
+  else
+    jac_mul_limbs(r, pj, k8, 8);
+  g2_compress(out96, r);
+  return DEC_OK;
 }
 
 // Fp-multiplication counts of one op_verify call (mul, sqr)
