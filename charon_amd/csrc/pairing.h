@@ -112,6 +112,18 @@ BLS_HD BLS_CALL void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bo
   for (int bit = 62; bit >= 0; --bit) {
     if (!first) fp12_sqr(f, f);
     first = false;
+    if (n == 2 && !skip[0] && !skip[1]) {  // both lines live: one line-pair product (fp12_mul_line2)
+      fp2 a0, a1, ah;
+      miller_dbl_step(T[0], a0, a1, ah, P[0].x, P[0].y);
+      miller_dbl_step(T[1], g0, g1, h1, P[1].x, P[1].y);
+      fp12_mul_line2(f, a0, a1, ah, g0, g1, h1);
+      if ((X_ABS >> bit) & 1ull) {
+        miller_add_step(T[0], a0, a1, ah, Q[0], P[0].x, P[0].y);
+        miller_add_step(T[1], g0, g1, h1, Q[1], P[1].x, P[1].y);
+        fp12_mul_line2(f, a0, a1, ah, g0, g1, h1);
+      }
+      continue;
+    }
     for (int i = 0; i < n; ++i) {
       miller_dbl_step(T[i], g0, g1, h1, P[i].x, P[i].y);
       if (!skip[i]) fp12_mul_line(f, g0, g1, h1);

@@ -320,6 +320,65 @@ BLS_HD BLS_CALL void fp12_mul_line(fp12& f, const fp2& g0, const fp2& g1, const 
   fp6_mul_v(t1, t1);
   fp6_add(f.c0, t0, t1);
 }
+// f *= la * lb for two M-twist lines l = (g0 + g1 v) + (h1 v) w.  The line product is
+// (c0 dense) + (x v + y v^2) w with w^2 = v, v^3 = xi (6 Fp2 products); multiplying it into f
+// costs 17 more, 23 in all instead of 26 for two fp12_mul_line calls.
+BLS_HD BLS_CALL void fp12_mul_line2(fp12& f, const fp2& ga0, const fp2& ga1, const fp2& ha1, const fp2& gb0,
+                                    const fp2& gb1, const fp2& hb1) {
+  fp2 p00, p11, phh, sa, sb, t;
+  fp6 L0;
+  fp2 x, y;
+  fp2_mul(p00, ga0, gb0);
+  fp2_mul(p11, ga1, gb1);
+  fp2_mul(phh, ha1, hb1);
+  fp2_add(sa, ga0, ga1);
+  fp2_add(sb, gb0, gb1);
+  fp2_mul(t, sa, sb);
+  fp2_sub(t, t, p00);
+  fp2_sub(L0.c1, t, p11);   // ga0 gb1 + ga1 gb0
+  fp2_mul_xi(t, phh);
+  fp2_add(L0.c0, p00, t);   // ga0 gb0 + xi ha1 hb1
+  L0.c2 = p11;              // ga1 gb1
+  fp2_add(sa, ga0, ha1);
+  fp2_add(sb, gb0, hb1);
+  fp2_mul(x, sa, sb);
+  fp2_sub(x, x, p00);
+  fp2_sub(x, x, phh);       // ga0 hb1 + ha1 gb0
+  fp2_add(sa, ga1, ha1);
+  fp2_add(sb, gb1, hb1);
+  fp2_mul(y, sa, sb);
+  fp2_sub(y, y, p11);
+  fp2_sub(y, y, phh);       // ga1 hb1 + ha1 gb1
+  // f = (F0 + F1 w)(L0 + L1 w), L1 = x v + y v^2
+  fp6 t0, t1, s, l;
+  fp6_mul(t0, f.c0, L0);
+  {  // t1 = F1 * (x v + y v^2) = xi(a1 y + a2 x) + (a0 x + xi a2 y) v + (a0 y + a1 x) v^2
+    const fp6& a = f.c1;
+    fp2 m1, m2, m0, u, w2;
+    fp2_mul(m1, a.c1, x);
+    fp2_mul(m2, a.c2, y);
+    fp2_mul(m0, a.c0, x);
+    fp2_add(u, a.c1, a.c2);
+    fp2_add(w2, x, y);
+    fp2_mul(u, u, w2);
+    fp2_sub(u, u, m1);
+    fp2_sub(u, u, m2);
+    fp2_mul_xi(t1.c0, u);
+    fp2_mul_xi(u, m2);
+    fp2_add(t1.c1, m0, u);
+    fp2_mul(u, a.c0, y);
+    fp2_add(t1.c2, u, m1);
+  }
+  fp6_add(s, f.c0, f.c1);
+  l.c0 = L0.c0;
+  fp2_add(l.c1, L0.c1, x);
+  fp2_add(l.c2, L0.c2, y);
+  fp6_mul(s, s, l);
+  fp6_sub(s, s, t0);
+  fp6_sub(f.c1, s, t1);
+  fp6_mul_v(t1, t1);
+  fp6_add(f.c0, t0, t1);
+}
 BLS_HD BLS_CALL void fp12_frobenius(fp12& r, const fp12& a, int j) {
   // coefficient of w^k (k = 2i + h for a.c_h.c_i) is conj^j(c) * gamma_{j,k}
   const fp2* g = j == 1 ? FROB1 : (j == 2 ? FROB2 : FROB3);
