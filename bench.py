@@ -35,7 +35,7 @@ MADS_PER_FPMUL = 300
 # RLC BatchVerify stages (charon_amd/csrc/rlc.h), same unit and source (tests/test_work_counts.py):
 # stage 1 per item, stage 2 per distinct message, stage 3 per window of 8 with 2 messages (one per
 # 4-partial validator) or 1 message (committee root), stage 4 per item re-checked after a failed window.
-RLC_FPMUL = {"item": 5832, "hash": 7144, "window_2msg": 26777, "window_1msg": 21456, "fallback": 20886}
+RLC_FPMUL = {"item": 5832, "hash": 7144, "window_2msg": 26165, "window_1msg": 20844, "fallback": 20886}
 # gfx950 32x32->64 integer multiply-add peak (v_mad_u64_u32): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 # at half rate (measured: profiles/r01_mad_probe.txt) = 39.3e12 MAD/s.
 MAD_PEAK_T = 39.3

@@ -188,14 +188,29 @@ BLS_HD BLS_CALL void miller_loop_multi(fp12& f, const g1a* P, const g2a* Q, int 
   fp2 g0, g1, h1;
   for (int bit = 62; bit >= 0; --bit) {
     if (bit != 62) fp12_sqr(f, f);
-    for (int k = 0; k < n; ++k) {
-      miller_dbl_step(T[k], g0, g1, h1, P[k].x, P[k].y);
-      fp12_mul_line(f, g0, g1, h1);
+    // lines two at a time (fp12_mul_line2): one f update per pair of lines
+    for (int k = 0; k < n; k += 2) {
+      if (k + 1 < n) {
+        fp2 a0, a1, ah;
+        miller_dbl_step(T[k], a0, a1, ah, P[k].x, P[k].y);
+        miller_dbl_step(T[k + 1], g0, g1, h1, P[k + 1].x, P[k + 1].y);
+        fp12_mul_line2(f, a0, a1, ah, g0, g1, h1);
+      } else {
+        miller_dbl_step(T[k], g0, g1, h1, P[k].x, P[k].y);
+        fp12_mul_line(f, g0, g1, h1);
+      }
     }
     if ((X_ABS >> bit) & 1ull) {
-      for (int k = 0; k < n; ++k) {
-        miller_add_step(T[k], g0, g1, h1, Q[k], P[k].x, P[k].y);
-        fp12_mul_line(f, g0, g1, h1);
+      for (int k = 0; k < n; k += 2) {
+        if (k + 1 < n) {
+          fp2 a0, a1, ah;
+          miller_add_step(T[k], a0, a1, ah, Q[k], P[k].x, P[k].y);
+          miller_add_step(T[k + 1], g0, g1, h1, Q[k + 1], P[k + 1].x, P[k + 1].y);
+          fp12_mul_line2(f, a0, a1, ah, g0, g1, h1);
+        } else {
+          miller_add_step(T[k], g0, g1, h1, Q[k], P[k].x, P[k].y);
+          fp12_mul_line(f, g0, g1, h1);
+        }
       }
     }
   }
