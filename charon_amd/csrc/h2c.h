@@ -222,13 +222,17 @@ BLS_HD BLS_CALL void fp_from_be64_words(fp& r, const uint32_t* w) {
   fp_add(r, lo, hi);
 }
 
-BLS_HD BLS_CALL void map_to_curve_sswu(g2a& out, const fp2& u) {
-  fp2 u2, zu2, den, tv1, x1, gx1, t, y, x;
+// SSWU denominator: zu2 = Z u^2, den = zu2^2 + zu2
+BLS_HD BLS_INLINE void sswu_den(fp2& zu2, fp2& den, const fp2& u) {
+  fp2 u2;
   fp2_sqr(u2, u);
   fp2_mul(zu2, SSWU_Z, u2);
   fp2_sqr(den, zu2);
   fp2_add(den, den, zu2);
-  fp2_inv(tv1, den);  // inv0: 0 -> 0
+}
+// SSWU with tv1 = inv0(den) supplied by the caller (so hash_to_g2 can share one inversion)
+BLS_HD BLS_CALL void map_to_curve_sswu_tv(g2a& out, const fp2& u, const fp2& zu2, const fp2& tv1) {
+  fp2 x1, gx1, t, y, x;
   if (fp2_is_zero(tv1)) {
     x1 = SSWU_B_OVER_ZA;
   } else {
@@ -258,6 +262,12 @@ BLS_HD BLS_CALL void map_to_curve_sswu(g2a& out, const fp2& u) {
   if (fp2_sgn0(u) != fp2_sgn0(y)) fp2_neg(y, y);
   out.x = x;
   out.y = y;
+}
+BLS_HD BLS_CALL void map_to_curve_sswu(g2a& out, const fp2& u) {
+  fp2 zu2, den, tv1;
+  sswu_den(zu2, den, u);
+  fp2_inv(tv1, den);  // inv0: 0 -> 0
+  map_to_curve_sswu_tv(out, u, zu2, tv1);
 }
 
 BLS_HD BLS_CALL void iso_map_g2(g2j& out, const g2a& p) {
@@ -302,9 +312,23 @@ BLS_HD BLS_CALL void hash_to_g2(g2j& out, const uint8_t* msg, uint32_t msg_len, 
   fp_from_be64_words(u0.c1, uni + 16);
   fp_from_be64_words(u1.c0, uni + 32);
   fp_from_be64_words(u1.c1, uni + 48);
+  // both SSWU inversions from one (Montgomery's trick); a zero denominator keeps inv0 semantics
+  // through separate inversions (fp2_inv(0) = 0)
+  fp2 zu0, zu1, d0, d1, t0, t1, inv;
+  sswu_den(zu0, d0, u0);
+  sswu_den(zu1, d1, u1);
+  fp2_mul(inv, d0, d1);
+  if (fp2_is_zero(inv)) {
+    fp2_inv(t0, d0);
+    fp2_inv(t1, d1);
+  } else {
+    fp2_inv(inv, inv);
+    fp2_mul(t0, inv, d1);
+    fp2_mul(t1, inv, d0);
+  }
   g2a q0a, q1a;
-  map_to_curve_sswu(q0a, u0);
-  map_to_curve_sswu(q1a, u1);
+  map_to_curve_sswu_tv(q0a, u0, zu0, t0);
+  map_to_curve_sswu_tv(q1a, u1, zu1, t1);
   g2j q0, q1, s;
   iso_map_g2(q0, q0a);
   iso_map_g2(q1, q1a);
