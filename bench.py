@@ -187,6 +187,7 @@ def main():
     from charon_amd.tbls import HipBLS, load_library
     impl = HipBLS(device=local)
     lib = load_library()
+    lib.hipbls_set_timing(1)  # per-kernel HIP events for the roofline (off by default in the library)
 
     rng = random.Random(SEED * 1000003 + rank)  # validator-index shard of this rank
     t0 = time.time()
@@ -282,7 +283,7 @@ def main():
         log("rank %d: C3 data (%d groups) in %.1fs" % (rank, args.tagg_groups, time.time() - t0))
         G = args.tagg_groups
         d_psig = torch.frombuffer(bytearray(b"".join(psigs)), dtype=torch.uint8).to(dev)
-        d_pid = torch.tensor(pids, dtype=torch.int32).to(dev)
+        d_pid = torch.tensor(pids, dtype=torch.int64).to(dev)
         d_poff = torch.tensor(poffs, dtype=torch.int64).to(dev)
         d_agg = torch.zeros(G * 96, dtype=torch.uint8, device=dev)
         d_gst = torch.full((G,), -1, dtype=torch.int32, device=dev)
@@ -293,7 +294,7 @@ def main():
 
         def tstep():
             rc = lib.hipbls_threshold_aggregate_batch_device(d_psig.data_ptr(), d_pid.data_ptr(), d_poff.data_ptr(), G,
-                                                             d_agg.data_ptr(), d_gst.data_ptr(),
+                                                             len(pids), d_agg.data_ptr(), d_gst.data_ptr(),
                                                              ctypes.c_void_p(stream.cuda_stream))
             assert rc == 0
             rc = lib.hipbls_verify_batch_device(d_dpk.data_ptr(), d_dmsg.data_ptr(), d_doff.data_ptr(),

@@ -98,6 +98,24 @@ BLS_HD BLS_INLINE void fr_from_u32(fr& r, uint32_t x) {
   fr_mul(r, t, r2);  // x < r so the product reduces
 }
 
+// A share index as herumi sets it: id.SetDecString(strconv.Itoa(idx)) (/root/reference/tbls/herumi.go:264-271)
+// parses the decimal of a Go int, sign included, as an Fr element: idx mod r, so -k becomes r - k.
+// |idx| < 2^63 < r, so the reduction is one conditional negation.  Result in Montgomery form.
+BLS_HD BLS_INLINE void fr_from_i64(fr& r, int64_t x) {
+  const uint64_t m = x < 0 ? (uint64_t)0 - (uint64_t)x : (uint64_t)x;
+  fr t, r2;
+  for (int i = 0; i < 8; ++i) {
+    t.v[i] = i == 0 ? (uint32_t)m : (i == 1 ? (uint32_t)(m >> 32) : 0u);
+    r2.v[i] = FR_R2[i];
+  }
+  fr_mul(r, t, r2);
+  if (x < 0) {
+    fr z;
+    for (int i = 0; i < 8; ++i) z.v[i] = 0;
+    fr_sub(r, z, r);
+  }
+}
+
 BLS_HD BLS_INLINE void fr_to_plain(fr& r, const fr& a) {
   fr one;
   for (int i = 0; i < 8; ++i) one.v[i] = i == 0 ? 1u : 0u;

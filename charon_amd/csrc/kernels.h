@@ -1,0 +1,526 @@
+// hipbls kernels (gfx950): one lane (or one workgroup) per item; the lane bodies live in ops.h / rlc.h so the
+// same arithmetic is compiled for the host tests.  Included once, by hipbls.hip (the C-ABI host runtime).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ops.h"
+#include "rlc.h"
+
+using namespace bls;
+
+// ============================================================================ kernels
+namespace {
+
+constexpr int kBlock = 64;  // one wave per workgroup: these kernels are register-bound, not LDS-bound
+
+__global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restrict__ pks,
+                                                         const uint8_t* __restrict__ msgs,
+                                                         const uint64_t* __restrict__ offs,
+                                                         const uint8_t* __restrict__ sigs, uint64_t n,
+                                                         int32_t* __restrict__ status) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t o0 = offs[i], o1 = offs[i + 1];
+  status[i] = op_verify(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i);
+}
+
+__global__ void __launch_bounds__(kBlock) k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restrict__ msgs,
+                                                 const uint64_t* __restrict__ offs, uint64_t n,
+                                                 uint8_t* __restrict__ out, int32_t* __restrict__ status) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t o0 = offs[i], o1 = offs[i + 1];
+  uint8_t sig[96];
+  const int st = op_sign(sig, sks + 32 * i, msgs + o0, (uint32_t)(o1 - o0));
+  for (int k = 0; k < 96; ++k) out[96 * i + k] = st == HIPBLS_OK ? sig[k] : (uint8_t)0;
+  status[i] = st;
+}
+
+__global__ void __launch_bounds__(kBlock) k_sk_to_pk(const uint8_t* __restrict__ sks, uint64_t n,
+                                                     uint8_t* __restrict__ out, int32_t* __restrict__ status) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t pk[48];
+  const int st = op_sk_to_pk(pk, sks + 32 * i);
+  for (int k = 0; k < 48; ++k) out[48 * i + k] = st == HIPBLS_OK ? pk[k] : (uint8_t)0;
+  status[i] = st;
+}
+
+// ThresholdAggregate, stage 1: one lane per partial signature k.  Finds its group by binary search
+// over group_offsets, decodes + subgroup-checks sig_k, computes lambda_k(0) from the group's ids and
+// writes lambda_k * sig_k (Jacobian, limb-major SoA: 36 words x n_partials) plus a per-partial code.
+__global__ void __launch_bounds__(kBlock) k_tagg_scale(const uint8_t* __restrict__ sigs,
+                                                       const int64_t* __restrict__ ids,
+                                                       const uint64_t* __restrict__ goffs, uint64_t n_groups,
+                                                       uint64_t n_parts, uint32_t* __restrict__ pts,
+                                                       int32_t* __restrict__ pstat) {
+  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (k >= n_parts) return;
+  uint64_t lo = 0, hi = n_groups;  // find g with goffs[g] <= k < goffs[g+1]
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (goffs[mid] <= k)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  const uint64_t g0 = goffs[lo], g1 = goffs[lo + 1];
+  const int t = (int)(g1 - g0);
+  const int me = (int)(k - g0);
+  g2j acc;
+  jac_set_inf(acc);
+  int st = HIPBLS_OK;
+  // ids must be non-zero and distinct within the group (herumi Recover fails otherwise).  As Fr elements
+  // (idx mod r, fr_from_i64) two int64 ids are equal only when equal as integers: |a - b| < 2^64 < r.
+  for (int a = 0; a < t; ++a) {
+    if (ids[g0 + a] == 0) st = HIPBLS_ERR_COMBINE;
+    for (int b = a + 1; b < t; ++b)
+      if (ids[g0 + a] == ids[g0 + b]) st = HIPBLS_ERR_COMBINE;
+  }
+  g2a s;
+  const int ds = g2_decompress(s, sigs + 96 * k, true);
+  if (ds == DEC_BAD) st = HIPBLS_ERR_SIGNATURE;
+  if (st == HIPBLS_OK && ds == DEC_OK) {
+    fr lam;
+    lagrange_at_zero(lam, ids + g0, t, me);
+    g2j sj;
+    jac_from_aff(sj, s);
+    g2_mul_glv4(acc, sj, lam.v);
+  }
+  const uint32_t* src = &acc.x.c0.v[0];
+  for (int w = 0; w < 72; ++w) pts[(uint64_t)w * n_parts + k] = src[w];
+  pstat[k] = st;
+}
+
+// ThresholdAggregate, stage 2: one lane per group sums its scaled partials and compresses.
+__global__ void __launch_bounds__(kBlock) k_tagg_sum(const uint32_t* __restrict__ pts,
+                                                     const int32_t* __restrict__ pstat,
+                                                     const uint64_t* __restrict__ goffs, uint64_t n_groups,
+                                                     uint64_t n_parts, uint8_t* __restrict__ out,
+                                                     int32_t* __restrict__ status) {
+  const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  const uint64_t g0 = goffs[g], g1 = goffs[g + 1];
+  int st = g1 > g0 ? HIPBLS_OK : HIPBLS_ERR_COMBINE;
+  // the reference reports the first deserialization failure before any combine failure
+  for (uint64_t k = g0; k < g1; ++k)
+    if (pstat[k] == HIPBLS_ERR_SIGNATURE) st = HIPBLS_ERR_SIGNATURE;
+  if (st == HIPBLS_OK)
+    for (uint64_t k = g0; k < g1; ++k)
+      if (pstat[k] != HIPBLS_OK) st = pstat[k];
+  g2j acc;
+  jac_set_inf(acc);
+  if (st == HIPBLS_OK) {
+    for (uint64_t k = g0; k < g1; ++k) {
+      g2j p;
+      uint32_t* dst = &p.x.c0.v[0];
+      for (int w = 0; w < 72; ++w) dst[w] = pts[(uint64_t)w * n_parts + k];
+      jac_add(acc, acc, p);
+    }
+  }
+  uint8_t sig[96];
+  g2_compress(sig, acc);
+  for (int b = 0; b < 96; ++b) out[96 * g + b] = st == HIPBLS_OK ? sig[b] : (uint8_t)0;
+  status[g] = st;
+}
+
+// G1 decode of many public keys (FastAggregateVerify): affine SoA (24 words) + code per key
+__global__ void __launch_bounds__(kBlock) k_g1_decode(const uint8_t* __restrict__ pks, uint64_t n,
+                                                      uint32_t* __restrict__ pts, int32_t* __restrict__ code) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a a;
+  const int st = g1_decompress(a, pks + 48 * i, true);
+  const uint32_t* src = &a.x.v[0];
+  for (int w = 0; w < 24; ++w) pts[(uint64_t)w * n + i] = st == DEC_OK ? src[w] : 0u;
+  code[i] = st;
+}
+
+// FastAggregateVerify (tbls/herumi.go:315-339), one workgroup of two waves per group g over keys
+// [goff[g], goff[g+1]) decoded by k_g1_decode: wave 0 sums the keys (strided, then an LDS tree),
+// wave 1 meanwhile decodes the signature and hashes the message; lane 0 then runs the pairing.
+// Status order follows the reference: signature decode error, then key decode error, then
+// "signature verification failed" (also for an empty key list, an infinity key or signature).
+constexpr int kFavBlock = 128;
+__global__ void __launch_bounds__(kFavBlock) k_fav_batch(const uint32_t* __restrict__ pts,
+                                                         const int32_t* __restrict__ code, uint64_t nkeys,
+                                                         const uint64_t* __restrict__ goff,
+                                                         const uint8_t* __restrict__ sigs,
+                                                         const uint8_t* __restrict__ msgs,
+                                                         const uint64_t* __restrict__ moffs,
+                                                         int32_t* __restrict__ status) {
+  __shared__ uint32_t red[64 * 36];
+  __shared__ uint32_t sh_sig[48], sh_hm[48];
+  __shared__ int sh_ds, sh_bad, sh_inf;
+  const uint64_t g = blockIdx.x;
+  const uint64_t k0 = goff[g], k1 = goff[g + 1];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    sh_bad = 0;
+    sh_inf = 0;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    g1j acc;
+    jac_set_inf(acc);
+    int bad = 0, inf = 0;
+    for (uint64_t k = k0 + tid; k < k1; k += 64) {
+      const int c = code[k];
+      if (c == DEC_BAD) {
+        bad = 1;
+      } else if (c == DEC_INF) {
+        inf = 1;
+      } else {
+        g1a a;
+        soa_load<24>(&a.x.v[0], pts, nkeys, k);
+        jac_add_aff(acc, acc, a);
+      }
+    }
+    if (bad) atomicOr(&sh_bad, 1);
+    if (inf) atomicOr(&sh_inf, 1);
+    for (int w = 0; w < 36; ++w) red[w * 64 + tid] = (&acc.x.v[0])[w];
+  } else if (tid == 64) {
+    g2a sg;
+    const int ds = g2_decompress(sg, sigs + 96 * g, true);
+    sh_ds = ds;
+    g2a hm;
+    if (ds == DEC_OK) {
+      g2j hj;
+      const uint64_t o0 = moffs[g], o1 = moffs[g + 1];
+      hash_to_g2(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43);
+      jac_to_aff(hm, hj);
+    } else {
+      fp2_set_zero(sg.x);
+      fp2_set_zero(sg.y);
+      hm = sg;
+    }
+    for (int w = 0; w < 48; ++w) {
+      sh_sig[w] = (&sg.x.c0.v[0])[w];
+      sh_hm[w] = (&hm.x.c0.v[0])[w];
+    }
+  }
+  __syncthreads();
+  for (int half = 32; half >= 1; half >>= 1) {  // every thread reaches every barrier
+    if (tid < half) {
+      g1j x, y;
+      for (int w = 0; w < 36; ++w) {
+        (&x.x.v[0])[w] = red[w * 64 + tid];
+        (&y.x.v[0])[w] = red[w * 64 + tid + half];
+      }
+      jac_add(x, x, y);
+      for (int w = 0; w < 36; ++w) red[w * 64 + tid] = (&x.x.v[0])[w];
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  int st;
+  if (sh_ds == DEC_BAD) {
+    st = HIPBLS_ERR_SIGNATURE;
+  } else if (sh_bad) {
+    st = HIPBLS_ERR_PUBKEY;
+  } else if (k1 == k0 || sh_ds == DEC_INF || sh_inf) {
+    st = HIPBLS_ERR_VERIFY;  // KeyValidate rejects the identity key; empty set is false [ext]
+  } else {
+    g1j sum;
+    for (int w = 0; w < 36; ++w) (&sum.x.v[0])[w] = red[w * 64];
+    if (jac_is_inf(sum)) {
+      st = HIPBLS_ERR_VERIFY;
+    } else {
+      g1a pk;
+      jac_to_aff(pk, sum);
+      g2a sg, hm;
+      for (int w = 0; w < 48; ++w) {
+        (&sg.x.c0.v[0])[w] = sh_sig[w];
+        (&hm.x.c0.v[0])[w] = sh_hm[w];
+      }
+      st = pairing_check_verify(pk, hm, sg) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+    }
+  }
+  status[g] = st;
+}
+
+// Aggregate (tbls/herumi.go:220-242): sum of n signatures in G2.  Stage 1 decodes every signature in parallel
+// (k_g2_decode: affine SoA + DEC_* code), stage 2 sums: each workgroup of kSumBlock lanes folds a strided
+// slice and reduces it through an LDS tree to one Jacobian partial; stage 3 (one workgroup) sums the partials
+// the same way and compresses.  herumi fails on the first signature that does not deserialize; every other
+// outcome -- including n = 0, where sig.Aggregate leaves the zero point -- serializes the sum, so the empty
+// aggregate is the infinity encoding 0xc0 || 0^95 with no error.
+constexpr int kSumBlock = 256;
+__global__ void __launch_bounds__(kBlock) k_g2_decode(const uint8_t* __restrict__ sigs, uint64_t n,
+                                                      uint32_t* __restrict__ pts, int32_t* __restrict__ code) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2a a;
+  const int st = g2_decompress(a, sigs + 96 * i, true);
+  const uint32_t* src = &a.x.c0.v[0];
+  for (int w = 0; w < 48; ++w) pts[(uint64_t)w * n + i] = st == DEC_OK ? src[w] : 0u;
+  code[i] = st;
+}
+
+// LDS tree over kSumBlock Jacobian points; every thread reaches every barrier.  Returns the sum in thread 0.
+__device__ void g2_block_tree_sum(g2j& acc, uint32_t* red) {
+  const int tid = threadIdx.x;
+  for (int w = 0; w < 72; ++w) red[w * kSumBlock + tid] = (&acc.x.c0.v[0])[w];
+  __syncthreads();
+  for (int half = kSumBlock / 2; half >= 1; half >>= 1) {
+    if (tid < half) {
+      g2j x, y;
+      for (int w = 0; w < 72; ++w) {
+        (&x.x.c0.v[0])[w] = red[w * kSumBlock + tid];
+        (&y.x.c0.v[0])[w] = red[w * kSumBlock + tid + half];
+      }
+      jac_add(x, x, y);
+      for (int w = 0; w < 72; ++w) red[w * kSumBlock + tid] = (&x.x.c0.v[0])[w];
+    }
+    __syncthreads();
+  }
+  for (int w = 0; w < 72; ++w) (&acc.x.c0.v[0])[w] = red[w * kSumBlock];
+}
+
+// Stage 2: workgroup b folds points b, b + stride, ... (stride = gridDim.x * kSumBlock) into partial b
+// (Jacobian, 72 words, SoA over the grid); bad[0] |= 1 when any code is DEC_BAD.
+__global__ void __launch_bounds__(kSumBlock) k_g2_sum_partial(const uint32_t* __restrict__ pts,
+                                                              const int32_t* __restrict__ code, uint64_t n,
+                                                              uint32_t* __restrict__ part, int32_t* __restrict__ bad) {
+  __shared__ uint32_t red[72 * kSumBlock];
+  g2j acc;
+  jac_set_inf(acc);
+  int my_bad = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * kSumBlock;
+  for (uint64_t i = blockIdx.x * (uint64_t)kSumBlock + threadIdx.x; i < n; i += stride) {
+    const int c = code[i];
+    if (c == DEC_BAD) {
+      my_bad = 1;
+    } else if (c == DEC_OK) {
+      g2a a;
+      soa_load<48>(&a.x.c0.v[0], pts, n, i);
+      jac_add_aff(acc, acc, a);
+    }
+  }
+  if (my_bad) atomicOr(bad, 1);
+  g2_block_tree_sum(acc, red);
+  if (threadIdx.x == 0) soa_store<72>(part, gridDim.x, blockIdx.x, &acc.x.c0.v[0]);
+}
+
+// Stage 3: one workgroup sums the np partials and writes the 96-byte encoding + status.
+__global__ void __launch_bounds__(kSumBlock) k_g2_sum_final(const uint32_t* __restrict__ part, uint64_t np,
+                                                            const int32_t* __restrict__ bad, uint8_t* __restrict__ out,
+                                                            int32_t* __restrict__ status) {
+  __shared__ uint32_t red[72 * kSumBlock];
+  g2j acc;
+  jac_set_inf(acc);
+  for (uint64_t i = threadIdx.x; i < np; i += kSumBlock) {
+    g2j p;
+    soa_load<72>(&p.x.c0.v[0], part, np, i);
+    jac_add(acc, acc, p);
+  }
+  g2_block_tree_sum(acc, red);
+  if (threadIdx.x != 0) return;
+  if (*bad) {
+    for (int b = 0; b < 96; ++b) out[b] = 0;
+    *status = HIPBLS_ERR_SIGNATURE;
+    return;
+  }
+  uint8_t sig[96];
+  g2_compress(sig, acc);
+  for (int b = 0; b < 96; ++b) out[b] = sig[b];
+  *status = HIPBLS_OK;
+}
+
+// Shamir shares: lane i-1 evaluates share_i = sum_j poly_j i^j (Horner over Fr)
+__global__ void __launch_bounds__(kBlock) k_threshold_split(const uint8_t* __restrict__ secret, const uint8_t* __restrict__ tail,
+                                  uint32_t total, uint32_t threshold, uint8_t* __restrict__ out,
+                                  int32_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  fr coef, acc, x, r2;
+  for (int w = 0; w < 8; ++w) r2.v[w] = FR_R2[w];
+  fr_from_u32(x, i + 1);
+  bool ok = true;
+  for (int w = 0; w < 8; ++w) acc.v[w] = 0;
+  for (int j = (int)threshold - 1; j >= 0; --j) {
+    const uint8_t* c = j == 0 ? secret : tail + 32 * (j - 1);
+    if (!fr_plain_from_be32(coef, c)) ok = false;
+    fr_mul(coef, coef, r2);  // to Montgomery
+    fr_mul(acc, acc, x);
+    fr_add(acc, acc, coef);
+  }
+  fr plain;
+  fr_to_plain(plain, acc);
+  for (int w = 0; w < 8; ++w)
+    for (int b = 0; b < 4; ++b) out[32 * i + 31 - 4 * w - b] = ok ? (uint8_t)(plain.v[w] >> (8 * b)) : (uint8_t)0;
+  if (i == 0) *status = ok ? HIPBLS_OK : HIPBLS_ERR_SECRET;
+}
+
+__global__ void __launch_bounds__(kBlock) k_recover_secret(const uint8_t* __restrict__ shares, const int64_t* __restrict__ ids, uint32_t n,
+                                 uint8_t* __restrict__ out, int32_t* __restrict__ status) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  int st = n > 0 ? HIPBLS_OK : HIPBLS_ERR_COMBINE;
+  for (uint32_t a = 0; a < n; ++a) {
+    if (ids[a] == 0) st = HIPBLS_ERR_COMBINE;
+    for (uint32_t b = a + 1; b < n; ++b)
+      if (ids[a] == ids[b]) st = HIPBLS_ERR_COMBINE;
+  }
+  fr acc, r2;
+  for (int w = 0; w < 8; ++w) {
+    acc.v[w] = 0;
+    r2.v[w] = FR_R2[w];
+  }
+  for (uint32_t k = 0; k < n && st == HIPBLS_OK; ++k) {
+    fr s, lam;
+    if (!fr_plain_from_be32(s, shares + 32 * k)) {
+      st = HIPBLS_ERR_SECRET;
+      break;
+    }
+    lagrange_at_zero(lam, ids, (int)n, (int)k);  // plain
+    fr_mul(lam, lam, r2);
+    fr_mul(s, s, r2);
+    fr_mul(s, s, lam);
+    fr_add(acc, acc, s);
+  }
+  fr plain;
+  fr_to_plain(plain, acc);
+  for (int w = 0; w < 8; ++w)
+    for (int b = 0; b < 4; ++b)
+      out[31 - 4 * w - b] = st == HIPBLS_OK ? (uint8_t)(plain.v[w] >> (8 * b)) : (uint8_t)0;
+  *status = st;
+}
+
+
+// ---------------------------------------------------------------- RLC BatchVerify (rlc.h)
+// The four stages run per sub-batch (a contiguous, window-aligned item range) so that several
+// sub-batches' stages overlap on separate streams (launch_rlc).
+// Stage 1: one lane per item -> status (final or RLC_PENDING), [r_i] pk_i and [r_i] sig_i in SoA.
+// pks == nullptr: public keys come from the resident pubshare table (key_idx, T, tcode, tab).
+__global__ void __launch_bounds__(kBlock) k_rlc_items(uint64_t i0, uint64_t i1, const uint8_t* __restrict__ pks,
+                                                      const uint8_t* __restrict__ sigs,
+                                                      const uint32_t* __restrict__ msg_idx, uint64_t n,
+                                                      uint64_t n_msgs, rlc_seed seed, uint32_t* __restrict__ rpk,
+                                                      uint32_t* __restrict__ rsig, int32_t* __restrict__ status,
+                                                      const uint32_t* __restrict__ key_idx, uint64_t T,
+                                                      const int32_t* __restrict__ tcode,
+                                                      const uint32_t* __restrict__ tab) {
+  const uint64_t i = i0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < i1) rlc_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk, rsig, status, key_idx, T, tcode, tab);
+}
+
+// Stage 2: one lane per message to hash -> H(m) in affine SoA (48 words) at its table column.  mlist lists the
+// messages to hash (the H(m)-cache misses); nullptr = messages 0 .. n_hash-1.
+__global__ void __launch_bounds__(kBlock) k_rlc_hash(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offs,
+                                                     uint64_t n_hash, const uint32_t* __restrict__ mlist,
+                                                     uint32_t* __restrict__ H, uint64_t hstride,
+                                                     const uint32_t* __restrict__ hslot) {
+  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (j < n_hash) rlc_hash_lane(mlist ? (uint64_t)mlist[j] : j, msgs, offs, H, hstride, hslot);
+}
+
+// Stage 3: one lane per window of RLC_W items -> one multi-pairing check.  The items a failed window
+// leaves pending are appended to this sub-batch's fallback list (one atomic per failed window), so
+// stage 4 runs on a dense list instead of waking a wave for every scattered pending item.
+__global__ void __launch_bounds__(kBlock) k_rlc_window(uint64_t w0, uint64_t w1, uint64_t n,
+                                                       const uint32_t* __restrict__ msg_idx,
+                                                       const uint32_t* __restrict__ rpk,
+                                                       const uint32_t* __restrict__ rsig,
+                                                       const uint32_t* __restrict__ H, uint64_t hstride,
+                                                       const uint32_t* __restrict__ hslot,
+                                                       int32_t* __restrict__ status, int32_t* __restrict__ win_fail,
+                                                       uint32_t* __restrict__ list, uint32_t* __restrict__ list_len) {
+  const uint64_t w = w0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (w >= w1) return;
+  const int left = rlc_window_lane(w, n, msg_idx, rpk, rsig, H, hstride, hslot, status, win_fail);
+  if (left == 0) return;
+  uint32_t at = atomicAdd(list_len, (uint32_t)left);
+  const uint64_t i1 = w * RLC_W + RLC_W < n ? w * RLC_W + RLC_W : n;
+  for (uint64_t i = w * RLC_W; i < i1; ++i)
+    if (status[i] == RLC_PENDING) list[at++] = (uint32_t)i;
+}
+
+// Stage 4: items of failed windows (dense list) are checked one by one (rlc_fallback_lane).
+__global__ void __launch_bounds__(kBlock) k_rlc_fallback(const uint32_t* __restrict__ list,
+                                                         const uint32_t* __restrict__ list_len, uint64_t cap,
+                                                         const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
+                                                         const uint32_t* __restrict__ msg_idx,
+                                                         const uint32_t* __restrict__ H, uint64_t hstride,
+                                                         const uint32_t* __restrict__ hslot,
+                                                         int32_t* __restrict__ status,
+                                                         const uint32_t* __restrict__ key_idx, uint64_t T,
+                                                         const uint32_t* __restrict__ tab) {
+  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t len = *list_len;
+  if (j >= len || j >= cap) return;
+  rlc_fallback_lane(list[j], pks, sigs, msg_idx, H, hstride, hslot, status, key_idx, T, tab);
+}
+
+// ---------------------------------------------------------------- resident pubshare table
+// Load: one lane per pubshare -> decode + subgroup test once (app/app.go:343-381 builds the same set
+// from the cluster lock at startup), keeping the affine key and [x] pk for the RLC scalars.
+__global__ void __launch_bounds__(kBlock) k_pubtab_load(const uint8_t* __restrict__ pks, uint64_t T,
+                                                        int32_t* __restrict__ code, uint32_t* __restrict__ tab,
+                                                        int32_t* __restrict__ status) {
+  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (k < T) status[k] = pubtab_load_lane(k, pks, T, code, tab);
+}
+
+// tbls.Verify with the key from the table: key_idx[i] >= T -> HIPBLS_ERR_ARG for that item.
+__global__ void __launch_bounds__(kBlock) k_verify_keys(const uint32_t* __restrict__ key_idx, uint64_t T,
+                                                        const int32_t* __restrict__ code,
+                                                        const uint32_t* __restrict__ tab,
+                                                        const uint8_t* __restrict__ msgs,
+                                                        const uint64_t* __restrict__ offs,
+                                                        const uint8_t* __restrict__ sigs, uint64_t n,
+                                                        int32_t* __restrict__ status) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = key_idx[i];
+  if (k >= T) {
+    status[i] = HIPBLS_ERR_ARG;
+    return;
+  }
+  g1a pk;
+  g1j xpk;
+  const int dp = pubtab_get(pk, xpk, k, T, code, tab);
+  const uint64_t o0 = offs[i], o1 = offs[i + 1];
+  status[i] = op_verify_decoded_pk(dp, pk, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i);
+}
+
+// ---------------------------------------------------------------- signing roots
+// eth2util/signing.GetDataRoot (/root/reference/eth2util/signing/signing.go:57-69): the signing root is the SSZ
+// hash_tree_root of SigningData{ObjectRoot, Domain}, two 32-byte leaves, i.e. SHA-256(object_root || domain).
+// One lane per item writes the 32-byte message and its offset for the verify kernel.
+__global__ void __launch_bounds__(kBlock) k_signing_roots(const uint8_t* __restrict__ roots,
+                                                          const uint8_t* __restrict__ domains, uint64_t n,
+                                                          uint8_t* __restrict__ out, uint64_t* __restrict__ offs) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i > n) return;
+  offs[i] = 32 * i;
+  if (i == n) return;
+  uint32_t w[16];
+  for (int k = 0; k < 8; ++k) {
+    const uint8_t* r = roots + 32 * i + 4 * k;
+    const uint8_t* d = domains + 32 * i + 4 * k;
+    w[k] = (uint32_t)r[0] << 24 | (uint32_t)r[1] << 16 | (uint32_t)r[2] << 8 | r[3];
+    w[8 + k] = (uint32_t)d[0] << 24 | (uint32_t)d[1] << 16 | (uint32_t)d[2] << 8 | d[3];
+  }
+  sha256_state st;
+  sha256_init(st);
+  sha256_compress(st, w);
+  for (int k = 0; k < 16; ++k) w[k] = 0;
+  w[0] = 0x80000000u;
+  w[15] = 512;
+  sha256_compress(st, w);
+  for (int k = 0; k < 8; ++k)
+    for (int b = 0; b < 4; ++b) out[32 * i + 4 * k + b] = (uint8_t)(st.h[k] >> (24 - 8 * b));
+}
+
+// eth2util/signing.Verify rejects an all-zero signature before tbls.Verify (signing.go:99-102): that item's
+// status becomes HIPBLS_ERR_ZERO_SIG whatever the pairing said.
+__global__ void __launch_bounds__(kBlock) k_zero_sig_status(const uint8_t* __restrict__ sigs, uint64_t n,
+                                                            int32_t* __restrict__ status) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t acc = 0;
+  for (int b = 0; b < 96; ++b) acc |= sigs[96 * i + b];
+  if (acc == 0) status[i] = HIPBLS_ERR_ZERO_SIG;
+}
+
+}  // namespace

@@ -35,15 +35,17 @@ BLS_HD BLS_CALL bool pairing_check_verify(const g1a& pk, const g2a& hm, const g2
 
 // pk = sk * g1; zero secret is an error (GetSafePublicKey, herumi.go:74)
 
-// Lagrange coefficient at 0 for the i-th id of a set (ids small positive integers, distinct)
-BLS_HD BLS_CALL void lagrange_at_zero(fr& out_plain, const uint32_t* ids, int n, int i) {
+// Lagrange coefficient at 0 for the i-th id of a set: lambda_i = prod_{j != i} x_j / (x_j - x_i) over Fr, with
+// x_k = ids[k] mod r (fr_from_i64: herumi's SetDecString(strconv.Itoa(idx)), tbls/herumi.go:264-271).  The ids
+// must be non-zero and pairwise distinct (callers check; herumi's Recover fails otherwise).
+BLS_HD BLS_CALL void lagrange_at_zero(fr& out_plain, const int64_t* ids, int n, int i) {
   fr num, den, t, xi, xj;
   fr_from_u32(num, 1);
   fr_from_u32(den, 1);
-  fr_from_u32(xi, ids[i]);
+  fr_from_i64(xi, ids[i]);
   for (int j = 0; j < n; ++j) {
     if (j == i) continue;
-    fr_from_u32(xj, ids[j]);
+    fr_from_i64(xj, ids[j]);
     fr_mul(num, num, xj);
     fr_sub(t, xj, xi);
     fr_mul(den, den, t);

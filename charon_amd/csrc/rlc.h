@@ -303,28 +303,32 @@ BLS_HD BLS_INLINE void rlc_items_lane(uint64_t i, const uint8_t* pks, const uint
   status[i] = st;
 }
 
-// Stage 2, message m: H(m) in affine SoA (48 words).
-BLS_HD BLS_INLINE void rlc_hash_lane(uint64_t m, const uint8_t* msgs, const uint64_t* offs, uint64_t n_msgs,
-                                     uint32_t* H) {
+// H(m) table addressing: message m lives in column hslot[m] (the resident H(m) cache) or, with hslot == nullptr,
+// in column m of a per-call table; the table has hstride columns of 48 words (affine, SoA).
+BLS_HD BLS_INLINE uint64_t h_col(const uint32_t* hslot, uint64_t m) { return hslot ? (uint64_t)hslot[m] : m; }
+
+// Stage 2, message m: H(m) in affine SoA (48 words) at its column.
+BLS_HD BLS_INLINE void rlc_hash_lane(uint64_t m, const uint8_t* msgs, const uint64_t* offs, uint32_t* H,
+                                     uint64_t hstride, const uint32_t* hslot) {
   const uint64_t o0 = offs[m], o1 = offs[m + 1];
   g2j hj;
   hash_to_g2(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43);
   g2a ha;
   jac_to_aff(ha, hj);
-  soa_store<48>(H, n_msgs, m, &ha.x.c0.v[0]);
+  soa_store<48>(H, hstride, h_col(hslot, m), &ha.x.c0.v[0]);
 }
 
 // Stage 3, window w = items [w*RLC_W, ...): on success every pending item becomes HIPBLS_OK,
 // otherwise they stay pending for stage 4.  Returns (and stores in win_fail[w]) the number of items
 // left pending: 0 when the window passed.
 BLS_HD BLS_INLINE int rlc_window_lane(uint64_t w, uint64_t n, const uint32_t* msg_idx, const uint32_t* rpk,
-                                      const uint32_t* rsig, const uint32_t* H, uint64_t n_msgs, int32_t* status,
-                                      int32_t* win_fail) {
+                                      const uint32_t* rsig, const uint32_t* H, uint64_t hstride, const uint32_t* hslot,
+                                      int32_t* status, int32_t* win_fail) {
   const uint64_t i0 = w * RLC_W;
   const uint64_t i1 = i0 + RLC_W < n ? i0 + RLC_W : n;
   auto load_pk = [&](g1j& q, uint64_t i) { soa_load<36>(&q.x.v[0], rpk, n, i); };
   auto load_sig = [&](g2j& q, uint64_t i) { soa_load<72>(&q.x.c0.v[0], rsig, n, i); };
-  auto load_h = [&](g2a& q, uint32_t m) { soa_load<48>(&q.x.c0.v[0], H, n_msgs, m); };
+  auto load_h = [&](g2a& q, uint32_t m) { soa_load<48>(&q.x.c0.v[0], H, hstride, h_col(hslot, m)); };
   const bool ok = rlc_window(i0, i1, status, msg_idx, load_pk, load_sig, load_h);
   int left = 0;
   for (uint64_t i = i0; i < i1; ++i)
@@ -342,7 +346,7 @@ BLS_HD BLS_INLINE int rlc_window_lane(uint64_t w, uint64_t n, const uint32_t* ms
 // points already passed decoding and the subgroup tests in stage 1 and H(m) is in the table, so this
 // is the bare pairing check: e(pk, H(m)) * e(-g1, sig) == 1 (about half of a full op_verify).
 BLS_HD BLS_INLINE void rlc_fallback_lane(uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
-                                         const uint32_t* H, uint64_t n_msgs, int32_t* status,
+                                         const uint32_t* H, uint64_t hstride, const uint32_t* hslot, int32_t* status,
                                          const uint32_t* key_idx = nullptr, uint64_t T = 0,
                                          const uint32_t* tab = nullptr) {
   if (status[i] != RLC_PENDING) return;
@@ -353,7 +357,7 @@ BLS_HD BLS_INLINE void rlc_fallback_lane(uint64_t i, const uint8_t* pks, const u
   else
     soa_load<24>(&pk.x.v[0], tab, T, key_idx[i]);
   g2_decompress(sig, sigs + 96 * i, false);
-  soa_load<48>(&hm.x.c0.v[0], H, n_msgs, msg_idx[i]);
+  soa_load<48>(&hm.x.c0.v[0], H, hstride, h_col(hslot, msg_idx[i]));
   status[i] = pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }
 

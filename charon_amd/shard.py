@@ -1,10 +1,12 @@
 """Multi-GPU sharding of the verify / aggregate batches.
 
-One process per GPU.  Validators are split into contiguous index ranges, so all partials of one
-distributed validator land on one GPU and ThresholdAggregate needs no exchange.  The only
-collective is one all-gather of the per-rank verify bitmaps (1 bit per item) -- over RCCL/xGMI
-(backend "nccl") on MI355X nodes, over gloo in the CPU tests.  There is no all-reduce on the data
-path.
+One process per GPU.  Validators are split into contiguous index ranges (shard_range), so all partials
+of one distributed validator land on one GPU and ThresholdAggregate needs no exchange.  The only
+collectives are all-gathers of results: the per-rank verify bitmaps (1 bit per item; RLC bitmaps
+too) and the 96-byte aggregate signatures -- over RCCL/xGMI (backend "nccl") on MI355X nodes, over
+gloo in the CPU tests.  There is no all-reduce on the data path.  Shards differ in size by at most one
+item, so every rank pads its block to the largest shard before the all-gather and the receiver cuts
+each row back to that rank's shard_range.
 """
 from __future__ import annotations
 
@@ -47,9 +49,48 @@ def unpack_bitmap(bits: torch.Tensor, n: int) -> torch.Tensor:
     return ((bits.view(-1, 1).to(torch.int32) >> shifts) & 1).view(-1)[:n].bool()
 
 
-def gather_bitmaps(local_bits: torch.Tensor, group=None) -> torch.Tensor:
-    """All-gather equal-sized per-rank bitmaps -> [world, nbytes] on every rank."""
+def _max_shard(n_items: int, world: int) -> int:
+    return (n_items + world - 1) // world
+
+
+def _gather_padded(local: torch.Tensor, width: int, group=None) -> torch.Tensor:
+    """All-gather one uint8 block per rank, each zero-padded to `width` bytes -> [world, width]."""
     world = dist.get_world_size(group)
-    out = torch.empty(world * local_bits.numel(), dtype=local_bits.dtype, device=local_bits.device)
-    dist.all_gather_into_tensor(out, local_bits.contiguous(), group=group)
-    return out.view(world, -1)
+    if local.numel() > width:
+        raise ValueError("local block larger than the padded width")
+    buf = torch.zeros(width, dtype=torch.uint8, device=local.device)
+    buf[:local.numel()] = local.reshape(-1)
+    out = torch.empty(world * width, dtype=torch.uint8, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    return out.view(world, width)
+
+
+def gather_bitmaps(local_bits: torch.Tensor, n_items: int = None, group=None) -> torch.Tensor:
+    """All-gather per-rank bitmaps -> [world, nbytes] on every rank.  With n_items (the node batch) every
+    row is padded to the largest shard's ceil(size/8) bytes, so uneven shards gather too."""
+    world = dist.get_world_size(group)
+    width = local_bits.numel() if n_items is None else (_max_shard(n_items, world) + 7) // 8
+    return _gather_padded(local_bits, width, group)
+
+
+def gather_node_bitmap(local_status: torch.Tensor, n_items: int, group=None) -> torch.Tensor:
+    """Per-rank status of shard_range(n_items, rank, world) -> bool[n_items] ok-bitmap of the whole node batch."""
+    world = dist.get_world_size(group)
+    rows = gather_bitmaps(pack_bitmap(local_status), n_items, group)
+    parts = []
+    for r in range(world):
+        lo, hi = shard_range(n_items, r, world)
+        parts.append(unpack_bitmap(rows[r], hi - lo))
+    return torch.cat(parts)
+
+
+def gather_aggregates(local_sigs: torch.Tensor, n_groups: int, group=None) -> torch.Tensor:
+    """Per-rank aggregate signatures (uint8, 96 bytes per validator of shard_range(n_groups, rank, world)) ->
+    uint8[n_groups * 96] in validator order on every rank."""
+    world = dist.get_world_size(group)
+    rows = _gather_padded(local_sigs, 96 * _max_shard(n_groups, world), group)
+    parts = []
+    for r in range(world):
+        lo, hi = shard_range(n_groups, r, world)
+        parts.append(rows[r, :96 * (hi - lo)])
+    return torch.cat(parts)

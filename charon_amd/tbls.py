@@ -20,7 +20,8 @@ from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 
-OK, ERR_PUBKEY, ERR_SIGNATURE, ERR_VERIFY, ERR_SECRET, ERR_COMBINE = 0, 1, 2, 3, 4, 5
+OK, ERR_PUBKEY, ERR_SIGNATURE, ERR_VERIFY, ERR_SECRET, ERR_COMBINE, ERR_ZERO_SIG = 0, 1, 2, 3, 4, 5, 6
+INFINITY_G2 = b"\xc0" + bytes(95)  # compressed point at infinity (the empty Aggregate, herumi.go:220-242)
 ERR_ARG, ERR_DEVICE = 16, 17
 
 # tbls/herumi.go error strings by status code
@@ -56,22 +57,34 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
     i32p = ctypes.POINTER(ctypes.c_int32)
     u64p = ctypes.POINTER(ctypes.c_uint64)
     u32p = ctypes.POINTER(ctypes.c_uint32)
+    i64p = ctypes.POINTER(ctypes.c_int64)
     vp = ctypes.c_void_p
     sig = {
+        "hipbls_current_device": ([], ctypes.c_int),
+        "hipbls_set_timing": ([ctypes.c_int], ctypes.c_int),
+        "hipbls_verify": ([u8p, u8p, u64, u8p, i32p], ctypes.c_int),
+        "hipbls_verify_submit": ([u8p, u8p, u64, u8p, u64p], ctypes.c_int),
+        "hipbls_verify_wait": ([u64, i32p], ctypes.c_int),
+        "hipbls_queue_config": ([u64, ctypes.c_uint32], ctypes.c_int),
+        "hipbls_queue_stats": ([u64p, u64p], ctypes.c_int),
+        "hipbls_verify_signed_data_batch": ([u8p, u8p, u8p, u8p, u64, i32p], ctypes.c_int),
+        "hipbls_aggregate_device": ([vp, u64, vp, vp, vp], ctypes.c_int),
+        "hipbls_hcache_config": ([u64], ctypes.c_int),
+        "hipbls_hcache_stats": ([u64p, u64p, u64p], ctypes.c_int),
         "hipbls_abi_version": ([], ctypes.c_int),
         "hipbls_init": ([ctypes.c_int], ctypes.c_int),
         "hipbls_device_count": ([], ctypes.c_int),
         "hipbls_last_error": ([], ctypes.c_char_p),
         "hipbls_verify_batch": ([u8p, u8p, u64p, u8p, u64, i32p], ctypes.c_int),
-        "hipbls_threshold_aggregate_batch": ([u8p, u32p, u64p, u64, u8p, i32p], ctypes.c_int),
+        "hipbls_threshold_aggregate_batch": ([u8p, i64p, u64p, u64, u8p, i32p], ctypes.c_int),
         "hipbls_sign_batch": ([u8p, u8p, u64p, u64, u8p, i32p], ctypes.c_int),
         "hipbls_secret_to_public_key_batch": ([u8p, u64, u8p, i32p], ctypes.c_int),
         "hipbls_verify_aggregate": ([u8p, u64, u8p, u8p, u64, i32p], ctypes.c_int),
         "hipbls_aggregate": ([u8p, u64, u8p, i32p], ctypes.c_int),
         "hipbls_threshold_split": ([u8p, u8p, ctypes.c_uint32, ctypes.c_uint32, u8p, i32p], ctypes.c_int),
-        "hipbls_recover_secret": ([u8p, u32p, ctypes.c_uint32, u8p, i32p], ctypes.c_int),
+        "hipbls_recover_secret": ([u8p, i64p, ctypes.c_uint32, u8p, i32p], ctypes.c_int),
         "hipbls_verify_batch_device": ([vp, vp, vp, vp, u64, vp, vp], ctypes.c_int),
-        "hipbls_threshold_aggregate_batch_device": ([vp, vp, vp, u64, vp, vp, vp], ctypes.c_int),
+        "hipbls_threshold_aggregate_batch_device": ([vp, vp, vp, u64, u64, vp, vp, vp], ctypes.c_int),
         "hipbls_sign_batch_device": ([vp, vp, vp, u64, vp, vp, vp], ctypes.c_int),
         "hipbls_secret_to_public_key_batch_device": ([vp, u64, vp, vp, vp], ctypes.c_int),
         "hipbls_batch_verify_rlc": ([u8p, u8p, u32p, u64, u8p, u64p, u64, u8p, i32p], ctypes.c_int),
@@ -108,6 +121,9 @@ def exported_symbols() -> List[str]:
         "hipbls_pubshare_table_load", "hipbls_pubshare_table_size", "hipbls_verify_aggregate_batch",
         "hipbls_verify_aggregate_batch_device", "hipbls_verify_batch_keys",
         "hipbls_batch_verify_rlc_keys", "hipbls_verify_batch_keys_device", "hipbls_batch_verify_rlc_keys_device",
+        "hipbls_current_device", "hipbls_set_timing", "hipbls_verify", "hipbls_verify_submit", "hipbls_verify_wait",
+        "hipbls_queue_config", "hipbls_queue_stats", "hipbls_verify_signed_data_batch", "hipbls_aggregate_device",
+        "hipbls_hcache_config", "hipbls_hcache_stats",
     ]
 
 
@@ -133,6 +149,19 @@ def _offsets(msgs: Sequence[bytes]):
 
 def _status_array(n: int):
     return (ctypes.c_int32 * max(n, 1))()
+
+
+def _go_int(idx) -> int:
+    """A map[int]... key of the Go API: a signed 64-bit integer (herumi.go:264-271 formats it with strconv.Itoa)."""
+    v = int(idx)
+    if not -(1 << 63) <= v < (1 << 63):
+        raise ValueError("share index outside Go's int range")
+    return v
+
+
+def _check_lengths(name: str, items: Sequence[bytes], size: int) -> None:
+    if any(len(x) != size for x in items):
+        raise ValueError("%s must be %d bytes each" % (name, size))
 
 
 class HipBLS:
@@ -171,6 +200,7 @@ class HipBLS:
 
     def secret_to_public_key_batch(self, secrets_: Sequence[bytes]) -> Tuple[List[bytes], List[int]]:
         n = len(secrets_)
+        _check_lengths("secret keys", secrets_, 32)
         out = ctypes.create_string_buffer(48 * max(n, 1))
         st = _status_array(n)
         _check(self.lib.hipbls_secret_to_public_key_batch(b"".join(secrets_), n, out, st), self.lib)
@@ -201,10 +231,11 @@ class HipBLS:
     def recover_secret(self, shares: Mapping[int, bytes], total: int = 0, threshold: int = 0) -> bytes:
         """herumi.go:183-218."""
         ids = list(shares.keys())
+        _check_lengths("shares", [shares[i] for i in ids], 32)
         for i in ids:
             if int.from_bytes(shares[i], "big") >= R:
                 raise TBLSError("cannot unmarshal key with into Herumi secret key")
-        arr = (ctypes.c_uint32 * max(len(ids), 1))(*[int(i) & 0xFFFFFFFF for i in ids])
+        arr = (ctypes.c_int64 * max(len(ids), 1))(*[_go_int(i) for i in ids])
         out = ctypes.create_string_buffer(32)
         st = _status_array(1)
         _check(self.lib.hipbls_recover_secret(b"".join(shares[i] for i in ids), arr, len(ids), out, st), self.lib)
@@ -221,6 +252,9 @@ class HipBLS:
 
     def sign_batch(self, sks: Sequence[bytes], msgs: Sequence[bytes]) -> Tuple[List[bytes], List[int]]:
         n = len(sks)
+        if len(msgs) != n:
+            raise ValueError("mismatching lengths")
+        _check_lengths("secret keys", sks, 32)
         blob, offs = _offsets(msgs)
         out = ctypes.create_string_buffer(96 * max(n, 1))
         st = _status_array(n)
@@ -296,6 +330,7 @@ class HipBLS:
         n = len(key_idx)
         if not (len(msgs) == n == len(sigs)):
             raise ValueError("mismatching lengths")
+        _check_lengths("signatures", sigs, 96)
         blob, offs = _offsets(msgs)
         st = _status_array(n)
         idx = (ctypes.c_uint32 * max(n, 1))(*key_idx)
@@ -308,7 +343,10 @@ class HipBLS:
         n = len(key_idx)
         if not (len(msgs) == n == len(sigs)):
             raise ValueError("mismatching lengths")
+        _check_lengths("signatures", sigs, 96)
         seed = secrets.token_bytes(32) if seed is None else seed
+        if len(seed) != 32:
+            raise ValueError("seed must be 32 bytes")
         pos: Dict[bytes, int] = {}
         table: List[bytes] = []
         midx = (ctypes.c_uint32 * max(n, 1))()
@@ -347,10 +385,12 @@ class HipBLS:
         for g, grp in enumerate(groups):
             offs[g] = len(ids)
             for idx, s in grp.items():
-                ids.append(int(idx) & 0xFFFFFFFF if int(idx) >= 0 else 0)
+                if len(s) != 96:
+                    raise ValueError("bad signature length")
+                ids.append(_go_int(idx))
                 sigs.append(bytes(s))
         offs[n_groups] = len(ids)
-        arr = (ctypes.c_uint32 * max(len(ids), 1))(*ids)
+        arr = (ctypes.c_int64 * max(len(ids), 1))(*ids)
         out = ctypes.create_string_buffer(96 * max(n_groups, 1))
         st = _status_array(n_groups)
         _check(self.lib.hipbls_threshold_aggregate_batch(b"".join(sigs), arr, offs, n_groups, out, st), self.lib)
@@ -367,6 +407,8 @@ class HipBLS:
 
     def verify_aggregate(self, shares: Sequence[bytes], signature: bytes, data: bytes) -> None:
         """herumi.go:315-339 (FastAggregateVerify)."""
+        _check_lengths("public keys", shares, 48)
+        _check_lengths("signature", [signature], 96)
         st = _status_array(1)
         _check(self.lib.hipbls_verify_aggregate(b"".join(shares), len(shares), signature, data, len(data), st),
                self.lib)
@@ -381,6 +423,9 @@ class HipBLS:
         """One FastAggregateVerify per (shares, signature, data) group in one launch; per-group status
         (OK / ERR_SIGNATURE / ERR_PUBKEY / ERR_VERIFY, as verify_aggregate raises)."""
         g = len(groups)
+        for shares, sig, _ in groups:
+            _check_lengths("public keys", shares, 48)
+            _check_lengths("signature", [sig], 96)
         koffs = (ctypes.c_uint64 * (g + 1))()
         keys: List[bytes] = []
         for j, (shares, _, _) in enumerate(groups):
@@ -394,12 +439,71 @@ class HipBLS:
         return list(st)[:g]
 
     def aggregate(self, signs: Sequence[bytes]) -> bytes:
-        """herumi.go:220-242."""
+        """herumi.go:220-242: the G2 sum; the only error is a signature that does not deserialize.  An empty
+        list is not an error: the result is the point at infinity (INFINITY_G2)."""
+        _check_lengths("signatures", signs, 96)
         out = ctypes.create_string_buffer(96)
         st = _status_array(1)
         _check(self.lib.hipbls_aggregate(b"".join(signs), len(signs), out, st), self.lib)
         if st[0] == ERR_SIGNATURE:
             raise TBLSError("cannot unmarshal signature into Herumi signature")
         if st[0] != OK:
-            raise TBLSError("cannot aggregate zero signatures")
+            raise DeviceError("unexpected aggregate status %d" % st[0])
         return out.raw
+
+    # ---------------------------------------------------------------- submission queue (coalesced Verify)
+    def verify_queued(self, compressed_public_key: bytes, data: bytes, signature: bytes) -> int:
+        """One tbls.Verify through the library's submission queue (hipbls_verify): concurrent callers are
+        coalesced into batched launches.  Returns the status code (OK / ERR_*)."""
+        _check_lengths("public key", [compressed_public_key], 48)
+        _check_lengths("signature", [signature], 96)
+        st = ctypes.c_int32(-1)
+        _check(self.lib.hipbls_verify(compressed_public_key, data, len(data), signature, ctypes.byref(st)), self.lib)
+        return st.value
+
+    def verify_submit(self, compressed_public_key: bytes, data: bytes, signature: bytes) -> int:
+        _check_lengths("public key", [compressed_public_key], 48)
+        _check_lengths("signature", [signature], 96)
+        t = ctypes.c_uint64()
+        _check(self.lib.hipbls_verify_submit(compressed_public_key, data, len(data), signature, ctypes.byref(t)),
+               self.lib)
+        return t.value
+
+    def verify_wait(self, ticket: int) -> int:
+        st = ctypes.c_int32(-1)
+        _check(self.lib.hipbls_verify_wait(ticket, ctypes.byref(st)), self.lib)
+        return st.value
+
+    def queue_config(self, max_batch: int = 65536, gather_us: int = 200) -> None:
+        _check(self.lib.hipbls_queue_config(max_batch, gather_us), self.lib)
+
+    def queue_stats(self) -> Tuple[int, int]:
+        b, i = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self.lib.hipbls_queue_stats(ctypes.byref(b), ctypes.byref(i)), self.lib)
+        return b.value, i.value
+
+    # ---------------------------------------------------------------- eth2util/signing.Verify (§8f.3)
+    def verify_signed_data_status(self, pks: Sequence[bytes], object_roots: Sequence[bytes],
+                                  domains: Sequence[bytes], sigs: Sequence[bytes]) -> List[int]:
+        """eth2util/signing/signing.go:88-107 per item: signing root SHA-256(object_root || domain) on the GPU,
+        ERR_ZERO_SIG for an all-zero signature, else the Verify status."""
+        n = len(pks)
+        if not (len(object_roots) == len(domains) == len(sigs) == n):
+            raise ValueError("mismatching lengths")
+        _check_lengths("public keys", pks, 48)
+        _check_lengths("object roots", object_roots, 32)
+        _check_lengths("domains", domains, 32)
+        _check_lengths("signatures", sigs, 96)
+        st = _status_array(n)
+        _check(self.lib.hipbls_verify_signed_data_batch(b"".join(pks), b"".join(object_roots), b"".join(domains),
+                                                        b"".join(sigs), n, st), self.lib)
+        return list(st)[:n]
+
+    # ---------------------------------------------------------------- resident H(m) cache (§8f.2)
+    def hcache_config(self, capacity: int) -> None:
+        _check(self.lib.hipbls_hcache_config(capacity), self.lib)
+
+    def hcache_stats(self) -> Tuple[int, int, int]:
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self.lib.hipbls_hcache_stats(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), self.lib)
+        return a.value, b.value, c.value

@@ -1,288 +1,442 @@
-"""Generate charon_amd/csrc/fp_asm_gfx950.h: the gfx950 Montgomery product as one inline-asm block.
+"""Generate charon_amd/csrc/fp_asm_gfx950.h: the gfx950 Montgomery product as one asm routine.
 
-Why asm: hipcc cannot fuse the carry-out of v_mad_u64_u32 into the next add, so compiled C++
-spends ~4 instructions per 32x32 limb product.  Here every product is exactly
-    v_mad_u64_u32 acc, vcc, x, y, acc      (64-bit accumulate, carry-out -> vcc)
-    v_addc_co_u32 t, vcc, 0, t, vcc        (carry -> third accumulator word)
-in product-scanning (Comba) order with the Montgomery reduction interleaved per column
-(Koc-Acar-Kaliski "FIPS").  Registers are pinned (a = v[0:11] in/out, b = v[12:23]) to match the
-AMDGPU calling convention of a non-inlined function taking/returning 12-dword vectors, so a call
-costs no moves.  Only caller-saved registers are used (v0-v39, vcc, s16-s28).
+SHIPPED (gen_mul): radix 2^32, 12 limbs, product scanning (Comba) with the Montgomery reduction
+interleaved per column.  Every limb product is one v_mad_u64_u32 into a 64-bit column accumulator
+plus one v_addc_co_u32 catching the carry into a third word: 288 mads + 12 v_mul_lo_u32, canonical
+output (final conditional subtraction of p).  Registers are pinned (a = v[0:11] in/out, b = v[12:23])
+and only v24-v39, s16-s28 and vcc are clobbered, so values live across a product stay in registers.
+The final select uses v_cndmask_b32_e64 with an explicit VCC operand: on gfx950 the VOP2 (e32) form that
+reads VCC implicitly issues at ~19 cycles per instruction against ~4.4 for the e64 form and for v_bfi_b32
+(profiles/r02_prod_probe.txt, tools/sel_probe.hip).
 
-Correctness is covered by the GPU parity tests (every curve/pairing result goes through it); the
-host build keeps the C++ CIOS in field.h, which the CPU tests diff against the oracle.
+EXPERIMENT (gen_mul29, not emitted): radix 2^29, 14 limbs, R = 2^406, no carry capture (a column of
+<= 28 terms < 2^58 fits the 64-bit accumulator), two accumulator chains, lazy [0, 2p) output, list
+scheduled.  Measured on MI355X (tools/prod_probe.hip): at one wave per SIMD -- the C2 regime -- it is no
+faster (2,802-2,946 vs 2,754 cycles per product: v_mad_u64_u32 issues at 5 cycles for one wave, so 392
+mads cost what 288 mads + 288 addc cost); at 2 and 4 waves per SIMD it is 10-14 % faster.  Adopting it
+also needs R = 2^406 constants and a weakly reduced value domain everywhere, so it stays an experiment.
+
+Correctness: `emulate()` interprets an emitted stream on the CPU; tests/test_fp_asm.py checks the shipped
+routine (and the experiment) against big-integer Montgomery products before any GPU run.
 
 Run:  python3 charon_amd/tools/gen_fp_asm.py
 """
 import os
+import random
 
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
-N = 12
-PINV = (-pow(P, -1, 1 << 32)) % (1 << 32)
-PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N)]
+N32 = 12
+W = 29
+N = 14
+MASK = (1 << W) - 1
+R_MONT = 1 << (W * N)  # 2^406
+PINV29 = (-pow(P, -1, 1 << W)) % (1 << W)
+P29 = [(P >> (W * i)) & MASK for i in range(N)]
+assert P29[13] == 13 and 4 * P < R_MONT
 
-A = lambda j: "v%d" % j          # a limbs, later the output
-B = lambda j: "v%d" % (12 + j)   # b limbs, later the subtraction temp
-M = lambda j: "v%d" % (24 + j)   # Montgomery quotients
-ACC = "v[36:37]"
-ACC_LO, ACC_HI = "v36", "v37"
-T = "v39"                        # carry word; v38 takes the old hi at a column shift, so that
-SHIFTED, SHIFTED_LO = "v[38:39]", "v38"  # (old hi, T) is an aligned pair the next mad reads
-SP = lambda j: "s%d" % (16 + j)  # p limbs
-SPINV = "s28"
+# ---------------------------------------------------------------- register map
+A = lambda k: "v%d" % k if k < 12 else "v%d" % (24 + k - 12)
+B = lambda k: "v%d" % (12 + k) if k < 12 else "v%d" % (26 + k - 12)
+M = lambda k: "v%d" % (28 + k)
+C0 = (42, 43)
+CB = [(44, 45), (46, 47)]
+VPINV = "v48"
+SP = lambda k: "s%d" % (16 + k) if k < 13 else "13"
+CLOBBER_V = list(range(12, 49))
+CLOBBER_S = list(range(16, 29))
 
 
-def gen_mul(square=False):
+def pair(r):
+    return "v[%d:%d]" % r
+
+
+class Ins:
+    __slots__ = ("text", "defs", "uses", "lat", "salu")
+
+    def __init__(self, text, defs, uses, lat=8, salu=False):
+        self.text, self.defs, self.uses, self.lat, self.salu = text, set(defs), set(uses), lat, salu
+
+
+def regs_of(op):
+    """Register names an operand string touches (v/s, pairs expanded)."""
+    op = op.strip()
+    if op.startswith("v["):
+        lo, hi = op[2:-1].split(":")
+        return ["v%d" % i for i in range(int(lo), int(hi) + 1)]
+    if op.startswith("s[") :
+        lo, hi = op[2:-1].split(":")
+        return ["s%d" % i for i in range(int(lo), int(hi) + 1)]
+    if (op.startswith("v") or op.startswith("s")) and op[1:].isdigit():
+        return [op]
+    return []
+
+
+def I(text, dst, srcs, lat=8):
+    defs = regs_of(dst)
+    uses = [r for s in srcs for r in regs_of(s)]
+    return Ins(text, defs, uses, lat)
+
+
+SDST_POOL = ["vcc"]  # carry-out destinations of the mads (never read); rotated
+_sdst_next = [0]
+
+
+def mad(acc, x, y, src2=None):
+    s2 = pair(acc) if src2 is None else src2
+    srcs = [x, y] + ([s2] if src2 is None else [])
+    sd = SDST_POOL[_sdst_next[0] % len(SDST_POOL)]
+    _sdst_next[0] += 1
+    # the carry-out is never read: not tracked as a dependency
+    return I("v_mad_u64_u32 %s, %s, %s, %s, %s" % (pair(acc), sd, x, y, s2), pair(acc), srcs, lat=8)
+
+
+def gen_mul29(square=False, chains=2):
+    """Returns the list of Ins (unscheduled, in a valid program order)."""
+    out = []
+    for k in range(13):
+        out.append(Ins("s_mov_b32 %s, 0x%08x" % (SP(k), P29[k]), [SP(k)], [], lat=1))
+    out.append(I("v_mov_b32 %s, 0x%08x" % (VPINV, PINV29), VPINV, [], lat=4))
+
+    def convert(R, base):
+        # 12x32 (registers base..base+11) -> 14x29 in R(k), high limb first (in place)
+        for k in range(N - 1, -1, -1):
+            o = W * k
+            w, s = o // 32, o % 32
+            src = lambda j: "v%d" % (base + j)
+            if w + 1 >= N32:  # top limb: the remaining bits of word 11
+                out.append(I("v_lshrrev_b32 %s, %d, %s" % (R(k), s, src(w)), R(k), [src(w)], lat=4))
+            elif s + W <= 32:
+                out.append(I("v_bfe_u32 %s, %s, %d, %d" % (R(k), src(w), s, W), R(k), [src(w)], lat=4))
+            else:
+                out.append(I("v_alignbit_b32 %s, %s, %s, %d" % (R(k), src(w + 1), src(w), s), R(k),
+                             [src(w + 1), src(w)], lat=4))
+                out.append(I("v_and_b32_e32 %s, 0x%08x, %s" % (R(k), MASK, R(k)), R(k), [R(k)], lat=4))
+
+    Bk = A if square else B
+    if not square:
+        convert(B, 12)
+    convert(A, 0)
+
+    started = {C0: False}
+
+    def add_term(acc, x, y):
+        if not started.get(acc, False):
+            out.append(mad(acc, x, y, src2="0"))
+            started[acc] = True
+        else:
+            out.append(mad(acc, x, y))
+
+    for i in range(2 * N - 1):
+        terms = []
+        for j in range(max(0, i - N + 1), min(i, N - 1) + 1):
+            terms.append((A(j), Bk(i - j)))
+        for j in range(max(0, i - N + 1), min(i - 1, N - 1) + 1):
+            terms.append((M(j), SP(i - j)))
+        if i < N:
+            # the quotient term m_i * p_0 comes last; keep a * b_0 in the list
+            pass
+        cb = CB[i % 2]
+        started[cb] = False
+        accs = [C0, cb] if chains >= 2 else [C0]
+        for t, (x, y) in enumerate(terms):
+            add_term(accs[t % len(accs)], x, y)
+        if chains >= 2 and started[cb]:
+            out.append(I("v_lshl_add_u64 %s, %s, 0, %s" % (pair(C0), pair(cb), pair(C0)), pair(C0),
+                         [pair(cb), pair(C0)], lat=8))
+        lo = "v%d" % C0[0]
+        if i < N:
+            out.append(I("v_mul_lo_u32 %s, %s, %s" % (M(i), lo, VPINV), M(i), [lo, VPINV], lat=8))
+            out.append(I("v_and_b32_e32 %s, 0x%08x, %s" % (M(i), MASK, M(i)), M(i), [M(i)], lat=4))
+            out.append(mad(C0, M(i), SP(0)))
+        else:
+            out.append(I("v_and_b32_e32 %s, 0x%08x, %s" % (M(i - N), MASK, lo), M(i - N), [lo], lat=4))
+        out.append(I("v_lshrrev_b64 %s, %d, %s" % (pair(C0), W, pair(C0)), pair(C0), [pair(C0)], lat=8))
+    out.append(I("v_mov_b32 %s, v%d" % (M(N - 1), C0[0]), M(N - 1), ["v%d" % C0[0]], lat=4))
+    # repack r (14 x 29 in M(0..13)) into 12 x 32 words in v0..v11
+    for wd in range(N32):
+        o = 32 * wd
+        k, s = o // W, o % W
+        dst = "v%d" % wd
+        if s == 0:
+            out.append(I("v_lshl_or_b32 %s, %s, %d, %s" % (dst, M(k + 1), W, M(k)), dst, [M(k + 1), M(k)], lat=4))
+        else:
+            out.append(I("v_lshrrev_b32 %s, %d, %s" % (dst, s, M(k)), dst, [M(k)], lat=4))
+            out.append(I("v_lshl_or_b32 %s, %s, %d, %s" % (dst, M(k + 1), W - s, dst), dst, [M(k + 1), dst], lat=4))
+            if W - s + W < 32:
+                out.append(I("v_lshl_or_b32 %s, %s, %d, %s" % (dst, M(k + 2), 2 * W - s, dst), dst,
+                             [M(k + 2), dst], lat=4))
+    return out
+
+
+def schedule(ins, issue=4):
+    """Greedy list scheduler over true/anti/output register dependencies.  Priority = longest
+    latency-weighted path to the end (critical path first).  Returns (ordered ins, modeled cycles)."""
+    n = len(ins)
+    succ = [[] for _ in range(n)]
+    npred = [0] * n
+    last_def, last_uses = {}, {}
+    edges = set()
+
+    def edge(a, b, lat):
+        if (a, b) in edges:
+            return
+        edges.add((a, b))
+        succ[a].append((b, lat))
+        npred[b] += 1
+
+    for i, x in enumerate(ins):
+        for r in x.uses:                   # RAW
+            if r in last_def:
+                edge(last_def[r], i, ins[last_def[r]].lat)
+        for r in x.defs:
+            if r in last_def:              # WAW
+                edge(last_def[r], i, 1)
+            for u in last_uses.get(r, ()):  # WAR
+                if u != i:
+                    edge(u, i, 1)
+        for r in x.uses:
+            last_uses.setdefault(r, []).append(i)
+        for r in x.defs:
+            last_def[r] = i
+            last_uses[r] = []
+    prio = [0] * n
+    for i in range(n - 1, -1, -1):
+        prio[i] = max([l + prio[j] for j, l in succ[i]] + [ins[i].lat])
+    ready_at = [0] * n
+    avail = [i for i in range(n) if npred[i] == 0]
+    order, t = [], 0
+    while avail:
+        # among instructions whose operands are ready at t, the highest priority; else the earliest
+        cands = [i for i in avail if ready_at[i] <= t]
+        if not cands:
+            t = min(ready_at[i] for i in avail)
+            continue
+        i = max(cands, key=lambda j: (prio[j], -j))
+        avail.remove(i)
+        order.append(ins[i])
+        t += 1 if ins[i].salu else issue
+        for j, l in succ[i]:
+            ready_at[j] = max(ready_at[j], t - issue + l if not ins[i].salu else t + l)
+            npred[j] -= 1
+            if npred[j] == 0:
+                avail.append(j)
+    assert len(order) == n
+    return order, t
+
+
+# ---------------------------------------------------------------- old radix-2^32 routine (probe)
+def gen_mul(e64_select=True):
+    """The shipped routine (Comba, radix 2^32, mad + addc carry capture, canonical output, R = 2^384).
+    e64_select=False reproduces the round-1 stream (VOP2 v_cndmask_b32_e32) for the microbenchmark."""
+    PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
+    PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    Aa = lambda j: "v%d" % j
+    Bb = lambda j: "v%d" % (12 + j)
+    Mm = lambda j: "v%d" % (24 + j)
+    Sp = lambda j: "s%d" % (16 + j)
     out = []
     w = out.append
-    for j in range(N):
-        w("s_mov_b32 %s, 0x%08x" % (SP(j), PL[j]))
-    w("s_mov_b32 %s, 0x%08x" % (SPINV, PINV))
-    first_in_col = [True]
-    src2 = [ACC]
+    for j in range(N32):
+        w("s_mov_b32 %s, 0x%08x" % (Sp(j), PL[j]))
+    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    first = [True]
+    src2 = ["v[36:37]"]
 
     def mac(x, y):
-        w("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (ACC, x, y, src2[0]))
-        src2[0] = ACC
-        if first_in_col[0]:
-            w("v_addc_co_u32_e64 %s, vcc, 0, 0, vcc" % T)
-            first_in_col[0] = False
+        w("v_mad_u64_u32 v[36:37], vcc, %s, %s, %s" % (x, y, src2[0]))
+        src2[0] = "v[36:37]"
+        if first[0]:
+            w("v_addc_co_u32_e64 v39, vcc, 0, 0, vcc")
+            first[0] = False
         else:
-            w("v_addc_co_u32_e32 %s, vcc, 0, %s, vcc" % (T, T))
+            w("v_addc_co_u32_e32 v39, vcc, 0, v39, vcc")
 
     def shift():
-        # one move, not two: the next column's first mad reads (old hi, T) as v[38:39] and writes
-        # the fresh accumulator v[36:37] (64-bit VGPR operands must be even-aligned on gfx950)
-        w("v_mov_b32 %s, %s" % (SHIFTED_LO, ACC_HI))
-        src2[0] = SHIFTED
-        first_in_col[0] = True
+        w("v_mov_b32 v38, v37")
+        src2[0] = "v[38:39]"
+        first[0] = True
 
-    # column 0: acc = a0*b0 (no carry possible)
-    w("v_mad_u64_u32 %s, vcc, %s, %s, 0" % (ACC, A(0), B(0)))
-    w("v_mov_b32 %s, 0" % T)
-    first_in_col[0] = False
-    w("v_mul_lo_u32 %s, %s, %s" % (M(0), ACC_LO, SPINV))
-    mac(M(0), SP(0))
+    w("v_mad_u64_u32 v[36:37], vcc, v0, v12, 0")
+    w("v_mov_b32 v39, 0")
+    first[0] = False
+    w("v_mul_lo_u32 v24, v36, s28")
+    mac("v24", "s16")
     shift()
-    for i in range(1, N):
+    for i in range(1, N32):
         for j in range(i):
-            mac(A(j), B(i - j))
-            mac(M(j), SP(i - j))
-        mac(A(i), B(0))
-        w("v_mul_lo_u32 %s, %s, %s" % (M(i), ACC_LO, SPINV))
-        mac(M(i), SP(0))
+            mac(Aa(j), Bb(i - j))
+            mac(Mm(j), Sp(i - j))
+        mac(Aa(i), Bb(0))
+        w("v_mul_lo_u32 %s, v36, s28" % Mm(i))
+        mac(Mm(i), "s16")
         shift()
-    for i in range(N, 2 * N - 1):
-        for j in range(i - N + 1, N):
-            mac(A(j), B(i - j))
-            mac(M(j), SP(i - j))
-        w("v_mov_b32 %s, %s" % (A(i - N), ACC_LO))  # a[i-12] is dead from column i on
+    for i in range(N32, 2 * N32 - 1):
+        for j in range(i - N32 + 1, N32):
+            mac(Aa(j), Bb(i - j))
+            mac(Mm(j), Sp(i - j))
+        w("v_mov_b32 %s, v36" % Aa(i - N32))
         shift()
-    w("v_mov_b32 %s, %s" % (A(N - 1), SHIFTED_LO))
-    # conditional subtraction: d = o - p into b's registers; keep o when it borrows.  p is copied
-    # to the (dead) quotient registers first: a carry-in vcc plus an SGPR operand would exceed the
-    # gfx9 constant-bus limit of one scalar read per VALU instruction.
-    for j in range(N):
-        w("v_mov_b32 %s, %s" % (M(j), SP(j)))
-    w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (B(0), A(0), M(0)))
-    for j in range(1, N):
-        w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (B(j), A(j), M(j)))
-    for j in range(N):
-        w("v_cndmask_b32_e32 %s, %s, %s, vcc" % (A(j), B(j), A(j)))
+    w("v_mov_b32 v11, v38")
+    for j in range(N32):
+        w("v_mov_b32 %s, %s" % (Mm(j), Sp(j)))
+    w("v_sub_co_u32_e32 v12, vcc, v0, v24")
+    for j in range(1, N32):
+        w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (Bb(j), Aa(j), Mm(j)))
+    for j in range(N32):
+        if e64_select:
+            w("v_cndmask_b32_e64 %s, %s, %s, vcc" % (Aa(j), Bb(j), Aa(j)))
+        else:
+            w("v_cndmask_b32_e32 %s, %s, %s, vcc" % (Aa(j), Bb(j), Aa(j)))
     return out
 
 
-# --- two-chain product (experiment, NOT emitted) ----------------------------------------------
-# Measured on MI355X (profiles/r01_fp_product_experiments.txt): bit-exact, but C2 fell from 917k
-# to 841k verifies/s.  The single chain is already ~80 % instruction-issue bound (695 VALU
-# instructions x 4 cycles per wave64 = 2,780 of the ~3,500 cycles a product takes at one wave per
-# SIMD), so the 92 extra instructions cost more than the hidden carry latency saves.  Kept as the
-# record of the experiment; the hypothesis it tested was:
-# the single-chain form above is latency-bound at one wave per SIMD: every v_mad_u64_u32 reads
-# the previous one's accumulator and every v_addc_co_u32 waits ~20 cycles for the carry the mad
-# just wrote to vcc (profiles/r01_lat_probe.txt: 24.8 cycles per mad+addc pair).  Here
-#   * the a*b terms (chain X) and the m*p terms (chain Y) of a column accumulate independently and
-#     are interleaved, so each mad's accumulator dependency is two instructions back;
-#   * every mad writes its carry to the next SGPR pair of a rotating pool and the addc that
-#     consumes it is issued DEFER instructions later, when the carry has landed;
-#   * the columns meet once: Y += lo(X) (a mad by 1), then m_i = lo(Y)*p' and Y += m_i*p0 zeroes
-#     the column (i < 12) or lo(Y) is output word i-12 (i >= 12).
-# The sum X+Y is the same 768-bit value the single chain builds, so results are bit-identical.
-XACC, XL, XH, XT = "v[36:37]", "v36", "v37", "v38"
-YACC, YL, YH, YT = "v[40:41]", "v40", "v41", "v39"
-CARRY_POOL = ["vcc"] + ["s[%d:%d]" % (r, r + 1) for r in range(40, 54, 2)]
-DEFER = 3
+gen_mul32 = gen_mul  # name used by tools/gen_probe_bodies.py
 
 
-def gen_mul2(defer=DEFER):
-    out = []
-    w = out.append
-    for j in range(N):
-        w("s_mov_b32 %s, 0x%08x" % (SP(j), PL[j]))
-    w("s_mov_b32 %s, 0x%08x" % (SPINV, PINV))
-    pool = list(CARRY_POOL)
-    nxt = [0]
-    pending = []          # (T register, carry pair, first-in-column)
-    t_init = {XT: False, YT: False}
-
-    def take():
-        c = pool[nxt[0] % len(pool)]
-        nxt[0] += 1
-        assert all(c != p[1] for p in pending), "carry pool too small for DEFER"
-        return c
-
-    def emit_addc():
-        t, c, first = pending.pop(0)
-        src = "0" if first else t
-        if c == "vcc":
-            if first:
-                w("v_addc_co_u32_e64 %s, vcc, 0, 0, vcc" % t)
-            else:
-                w("v_addc_co_u32_e32 %s, vcc, 0, %s, vcc" % (t, t))
-        else:
-            w("v_addc_co_u32_e64 %s, %s, 0, %s, %s" % (t, c, src, c))
-
-    def mad(acc, t, x, y):
-        c = take()
-        w("v_mad_u64_u32 %s, %s, %s, %s, %s" % (acc, c, x, y, acc))
-        first = not t_init[t]
-        t_init[t] = True
-        pending.append((t, c, first))
-        while len(pending) > defer:
-            emit_addc()
-
-    def flush():
-        while pending:
-            emit_addc()
-
-    def shift():
-        for lo, hi, t in ((XL, XH, XT), (YL, YH, YT)):
-            if t_init[t]:
-                w("v_mov_b32 %s, %s" % (lo, hi))
-                w("v_mov_b32 %s, %s" % (hi, t))
-            else:
-                w("v_mov_b32 %s, %s" % (lo, hi))
-                w("v_mov_b32 %s, 0" % hi)
-            t_init[t] = False
-
-    # column 0 seeds both accumulators without reading them
-    w("v_mad_u64_u32 %s, vcc, %s, %s, 0" % (XACC, A(0), B(0)))
-    w("v_mul_lo_u32 %s, %s, %s" % (M(0), XL, SPINV))
-    w("v_mad_u64_u32 %s, vcc, %s, %s, 0" % (YACC, M(0), SP(0)))
-    # lo(X)+lo(Y) == 0 mod 2^32; the column carries 1 iff lo(X) != 0.  Fold it as Y += lo(X).
-    w("v_mov_b32 %s, 0" % XT)
-    w("v_mov_b32 %s, 0" % YT)
-    t_init[XT] = t_init[YT] = True
-    mad(YACC, YT, XL, "1")
-    flush()
-    shift()
-    for i in range(1, 2 * N - 1):
-        xs = [(A(j), B(i - j)) for j in range(max(0, i - N + 1), min(i, N - 1) + 1)]
-        ys = [(M(j), SP(i - j)) for j in range(max(0, i - N + 1), min(i, N))]
-        for k in range(max(len(xs), len(ys))):
-            if k < len(xs):
-                mad(XACC, XT, *xs[k])
-            if k < len(ys):
-                mad(YACC, YT, *ys[k])
-        mad(YACC, YT, XL, "1")
-        if i < N:
-            flush()  # lo(Y) must be final before the quotient is taken
-            w("v_mul_lo_u32 %s, %s, %s" % (M(i), YL, SPINV))
-            mad(YACC, YT, M(i), SP(0))
-        else:
-            w("v_mov_b32 %s, %s" % (A(i - N), YL))  # a[i-12] is dead from column i on
-        flush()
-        shift()
-    w("v_add_u32_e32 %s, %s, %s" % (A(N - 1), XL, YL))
-    for j in range(N):
-        w("v_mov_b32 %s, %s" % (M(j), SP(j)))
-    w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (B(0), A(0), M(0)))
-    for j in range(1, N):
-        w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (B(j), A(j), M(j)))
-    for j in range(N):
-        w("v_cndmask_b32_e32 %s, %s, %s, vcc" % (A(j), B(j), A(j)))
-    return out
-
-
+# ---------------------------------------------------------------- CPU interpreter
 def emulate(body, a, b):
-    """Tiny interpreter for the instruction subset above (lane-scalar), used to check the
-    generator on the host: returns the 12 output limbs for 12-limb inputs a, b."""
+    """Interprets the instruction subset used above (one lane); a, b: 12 x 32-bit limbs.
+    Returns the 12 output limbs (v0..v11)."""
     v, s = {}, {}
-    for j in range(N):
+    M32, M64 = 0xFFFFFFFF, (1 << 64) - 1
+    for j in range(N32):
         v[j], v[12 + j] = a[j], b[j]
-    M32 = 0xFFFFFFFF
 
     def rd(x):
+        x = x.strip()
         if x.startswith("0x"):
             return int(x, 16)
-        if x.isdigit():
+        if x.lstrip("-").isdigit():
             return int(x)
-        if x.startswith("s["):
-            return s[x]
-        if x.startswith("s"):
-            return s[x]
         if x == "vcc":
-            return s["vcc"]
+            return s.get("vcc", 0)
         if x.startswith("v["):
             lo = int(x[2:x.index(":")])
             return v[lo] | (v[lo + 1] << 32)
+        if x.startswith("s"):
+            return s[x]
         return v[int(x[1:])]
 
-    def wr64(x, val):
-        lo = int(x[2:x.index(":")])
-        v[lo], v[lo + 1] = val & M32, (val >> 32) & M32
+    def wr(x, val):
+        x = x.strip()
+        if x.startswith("v["):
+            lo = int(x[2:x.index(":")])
+            v[lo], v[lo + 1] = val & M32, (val >> 32) & M32
+        elif x.startswith("s") or x == "vcc":
+            s[x] = val
+        else:
+            v[int(x[1:])] = val & M32
 
     for ins in body:
         op, rest = ins.split(" ", 1)
-        ops = [o.strip() for o in rest.split(",")]
+        o = [t.strip() for t in rest.split(",")]
         if op == "s_mov_b32":
-            s[ops[0]] = rd(ops[1])
+            s[o[0]] = rd(o[1])
         elif op == "v_mov_b32":
-            v[int(ops[0][1:])] = rd(ops[1]) & M32
+            wr(o[0], rd(o[1]))
         elif op == "v_mad_u64_u32":
-            r = rd(ops[2]) * rd(ops[3]) + rd(ops[4])
-            wr64(ops[0], r)
-            s[ops[1]] = r >> 64
+            r = (rd(o[2]) & M32) * (rd(o[3]) & M32) + rd(o[4])
+            wr(o[0], r & M64)
+            s[o[1]] = r >> 64
         elif op == "v_mul_lo_u32":
-            v[int(ops[0][1:])] = (rd(ops[1]) * rd(ops[2])) & M32
+            wr(o[0], rd(o[1]) * rd(o[2]))
         elif op.startswith("v_addc_co_u32"):
-            r = rd(ops[2]) + rd(ops[3]) + rd(ops[4])
-            v[int(ops[0][1:])] = r & M32
-            s[ops[1]] = r >> 32
-        elif op == "v_add_u32_e32":
-            v[int(ops[0][1:])] = (rd(ops[1]) + rd(ops[2])) & M32
+            r = rd(o[2]) + rd(o[3]) + rd(o[4])
+            wr(o[0], r)
+            s["vcc"] = r >> 32
         elif op == "v_sub_co_u32_e32":
-            r = rd(ops[2]) - rd(ops[3])
-            v[int(ops[0][1:])] = r & M32
+            r = rd(o[2]) - rd(o[3])
+            wr(o[0], r)
             s["vcc"] = 1 if r < 0 else 0
         elif op == "v_subb_co_u32_e32":
-            r = rd(ops[2]) - rd(ops[3]) - rd(ops[4])
-            v[int(ops[0][1:])] = r & M32
+            r = rd(o[2]) - rd(o[3]) - rd(o[4])
+            wr(o[0], r)
             s["vcc"] = 1 if r < 0 else 0
-        elif op == "v_cndmask_b32_e32":
-            v[int(ops[0][1:])] = rd(ops[2]) if rd(ops[3]) else rd(ops[1])
+        elif op in ("v_cndmask_b32_e32", "v_cndmask_b32_e64"):
+            wr(o[0], rd(o[2]) if rd(o[3]) else rd(o[1]))
+        elif op == "v_lshrrev_b32":
+            wr(o[0], rd(o[2]) >> rd(o[1]))
+        elif op == "v_lshrrev_b64":
+            wr(o[0], rd(o[2]) >> rd(o[1]))
+        elif op == "v_bfe_u32":
+            wr(o[0], (rd(o[1]) >> rd(o[2])) & ((1 << rd(o[3])) - 1))
+        elif op == "v_alignbit_b32":
+            wr(o[0], (((rd(o[1]) << 32) | rd(o[2])) >> rd(o[3])) & M32)
+        elif op == "v_and_b32_e32":
+            wr(o[0], rd(o[1]) & rd(o[2]))
+        elif op == "v_lshl_or_b32":
+            wr(o[0], ((rd(o[1]) << rd(o[2])) | rd(o[3])) & M32)
+        elif op == "v_lshl_add_u64":
+            wr(o[0], ((rd(o[1]) << rd(o[2])) + rd(o[3])) & M64)
         else:
             raise ValueError(ins)
-    return [v[j] for j in range(N)]
+    return [v[j] for j in range(N32)]
+
+
+def limbs(x):
+    return [(x >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+
+
+def value(l):
+    return sum(x << (32 * i) for i, x in enumerate(l))
+
+
+def check(body, square=False, trials=300, seed=1, mont=R_MONT, canonical=False):
+    """Host check of an emitted body: result == a*b/mont mod p, < 2p (or < p when canonical), for inputs
+    < 2^384 (< p for the canonical radix-2^32 routine)."""
+    rng = random.Random(seed)
+    rinv = pow(mont, -1, P)
+    edge = [0, 1, P - 1, P, 2 * P - 1, (1 << 384) - 1, (1 << 383), P + 1]
+    for t in range(trials):
+        if t < len(edge) ** 2:
+            a, b = edge[t % len(edge)], edge[t // len(edge) % len(edge)]
+        else:
+            a, b = rng.randrange(1 << 384), rng.randrange(1 << 384)
+        if canonical:
+            a, b = a % P, b % P
+        if square:
+            b = a
+        got = value(emulate(body, limbs(a), limbs(b)))
+        want = a * b * rinv % P
+        assert got < (P if canonical else 2 * P), (hex(a), hex(b), hex(got))
+        assert got % P == want, (hex(a), hex(b))
+    return True
+
+
+def body_text(square=False, chains=2, sched=True, pool=("vcc",)):
+    SDST_POOL[:] = list(pool)
+    _sdst_next[0] = 0
+    ins = gen_mul29(square=square, chains=chains)
+    if not sched:
+        return [x.text for x in ins], 0
+    order, cyc = schedule(ins)
+    return [x.text for x in order], cyc
+
+
+def emit_header(path, bodies):
+    lines = ["// GENERATED by charon_amd/tools/gen_fp_asm.py -- do not edit.",
+             "// gfx950 Montgomery product r = a*b/2^384 mod p (canonical), product scanning, %d instructions."
+             % len(bodies[0][1]),
+             "#pragma once"]
+    for name, body in bodies:
+        lines.append("// %s: %d instructions" % (name, len(body)))
+        lines.append("#define %s \\" % name)
+        for k, ins in enumerate(body):
+            sep = "\\n\\t" if k + 1 < len(body) else ""
+            lines.append('  "%s%s" \\' % (ins, sep))
+        lines.append("")
+    clob = ", ".join('"v%d"' % r for r in range(24, 40)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
+    lines.append("#define BLS_FP_MUL_ASM_CLOBBERS %s" % clob)
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
 
 
 def main():
-    body = gen_mul()
-    clob = ", ".join('"v%d"' % r for r in range(24, 40)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
-    lines = []
-    lines.append("// GENERATED by charon_amd/tools/gen_fp_asm.py -- do not edit.")
-    lines.append("// gfx950 Montgomery product r = a*b/2^384 mod p, product scanning, %d instructions." % len(body))
-    lines.append("#pragma once")
-    lines.append("#define BLS_FP_MUL_ASM_BODY \\")
-    for k, ins in enumerate(body):
-        sep = "\\n\\t" if k + 1 < len(body) else ""
-        lines.append('  "%s%s" \\' % (ins, sep))
-    lines.append("")
-    lines.append("#define BLS_FP_MUL_ASM_CLOBBERS %s" % clob)
+    mul = gen_mul()
+    check(mul, mont=1 << 384, canonical=True)
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "fp_asm_gfx950.h")
-    with open(path, "w") as f:
-        f.write("\n".join(lines) + "\n")
-    print("wrote", path, len(body), "instructions")
+    emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul)])
+    print("wrote %s: %d instructions" % (path, len(mul)))
 
 
 if __name__ == "__main__":

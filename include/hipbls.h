@@ -3,11 +3,17 @@
  *
  * C-ABI only: plain pointers and sizes, no HIP or torch types.  All buffers are owned by the
  * caller; the library never keeps a caller pointer after a call returns (cgo pointer rules).
- * Every entry point is thread-safe (one internal lock per device context).  A HIP failure is
- * reported as HIPBLS_ERR_DEVICE for the whole call and NEVER as a per-item "verified".
+ * Every entry point is thread-safe and binds the library's device on the calling thread (cgo goroutines move
+ * between OS threads).  Calls that share a device workspace are ordered on the device even when they are issued
+ * on different streams.  A HIP failure is reported as HIPBLS_ERR_DEVICE for the whole call and NEVER as a
+ * per-item "verified".
  *
  * Reference interface each entry point replaces (paths relative to the charon repository):
+ *   hipbls_verify                      tbls.Implementation.Verify (one item, coalesced by the submission queue)
+ *                                      tbls/tbls.go:53-55, tbls/herumi.go:285-301
  *   hipbls_verify_batch                tbls.Implementation.Verify            tbls/tbls.go:53-55, tbls/herumi.go:285-301
+ *   hipbls_verify_signed_data_batch    eth2util/signing.Verify (signing root + zero-signature check + tbls.Verify)
+ *                                      eth2util/signing/signing.go:57-69, 88-107
  *   hipbls_threshold_aggregate_batch   tbls.Implementation.ThresholdAggregate tbls/tbls.go:50-51, tbls/herumi.go:244-283
  *   hipbls_sign_batch                  tbls.Implementation.Sign              tbls/tbls.go:57-59, tbls/herumi.go:303-313
  *   hipbls_secret_to_public_key_batch  tbls.Implementation.SecretToPublicKey tbls/tbls.go:36-38, tbls/herumi.go:67-80
@@ -46,12 +52,13 @@ enum {
   HIPBLS_ERR_VERIFY = 3,    /* "signature not verified" (Verify) / "signature verification failed" (VerifyAggregate) */
   HIPBLS_ERR_SECRET = 4,    /* "cannot unmarshal secret into Herumi secret key" / "cannot obtain public key from secret" */
   HIPBLS_ERR_COMBINE = 5,   /* "cannot combine signatures" (empty set, id 0, duplicate id) */
+  HIPBLS_ERR_ZERO_SIG = 6,  /* eth2util/signing.Verify: "no signature found" (all-zero signature, signing.go:99-102) */
   HIPBLS_ERR_ARG = 16,      /* bad arguments (null pointer, size overflow) */
   HIPBLS_ERR_DEVICE = 17    /* HIP runtime failure; see hipbls_last_error() */
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 4
+#define HIPBLS_ABI_VERSION 5
 int hipbls_abi_version(void);
 
 /* Select the HIP device used by the calling process (one process per GPU); idempotent.
@@ -61,6 +68,24 @@ int hipbls_init(int device);
 int hipbls_device_count(void);
 /* Thread-local text of the last HIPBLS_ERR_DEVICE / HIPBLS_ERR_ARG. */
 const char* hipbls_last_error(void);
+/* Device index the library is bound to (-1 before the first call). */
+int hipbls_current_device(void);
+/* Per-kernel HIP-event timing (hipbls_kernel_timing); off by default, or HIPBLS_TIMING=1 in the environment. */
+int hipbls_set_timing(int enabled);
+
+/* ------------------------------------------------ single-item Verify through the submission queue ---- */
+/* tbls.Verify for one item.  Concurrent callers (any thread) are coalesced into one kernel launch per batch:
+ * while a batch runs on the GPU the next one fills, so the batch size follows the offered load; an idle queue
+ * waits gather_us for company.  *status as hipbls_verify_batch.  The queue has its own stream and buffers and
+ * no lock is held while the GPU runs. */
+int hipbls_verify(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, const uint8_t* sig96, int32_t* status);
+/* Asynchronous form: submit returns a ticket; wait blocks until that item's batch completed (each ticket once). */
+int hipbls_verify_submit(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, const uint8_t* sig96,
+                         uint64_t* ticket);
+int hipbls_verify_wait(uint64_t ticket, int32_t* status);
+/* Queue policy (defaults 65,536 items, 200 us) and counters (batches launched, items verified). */
+int hipbls_queue_config(uint64_t max_batch, uint32_t gather_us);
+int hipbls_queue_stats(uint64_t* batches, uint64_t* items);
 
 /* ---------------------------------------------------------------- batched, host buffers ---- */
 
@@ -70,11 +95,18 @@ const char* hipbls_last_error(void);
 int hipbls_verify_batch(const uint8_t* pks, const uint8_t* msgs, const uint64_t* msg_offsets,
                         const uint8_t* sigs, uint64_t n, int32_t* status);
 
+/* eth2util/signing.Verify for n items: the signing root SHA-256(object_root || domain) (SSZ SigningData) is
+ * computed on the GPU from object_roots[32 i ..] and domains[32 i ..]; status[i] as hipbls_verify_batch, or
+ * HIPBLS_ERR_ZERO_SIG for an all-zero signature. */
+int hipbls_verify_signed_data_batch(const uint8_t* pks, const uint8_t* object_roots, const uint8_t* domains,
+                                    const uint8_t* sigs, uint64_t n, int32_t* status);
+
 /* ThresholdAggregate for n_groups sets: group g holds partials
  * sigs[96 k ..], share_idx[k] for k in [group_offsets[g], group_offsets[g+1]).
- * out_sigs[96 g ..] = sum_k lambda_k(0) * sig_k (Lagrange at 0 over the 1-based share indices).
- * status[g] = HIPBLS_OK | HIPBLS_ERR_SIGNATURE | HIPBLS_ERR_COMBINE. */
-int hipbls_threshold_aggregate_batch(const uint8_t* sigs, const uint32_t* share_idx,
+ * out_sigs[96 g ..] = sum_k lambda_k(0) * sig_k: Lagrange at 0 over the share indices taken as Fr elements the
+ * way herumi parses strconv.Itoa(idx) (tbls/herumi.go:264-271): a signed Go int reduced mod r, so -k is r - k.
+ * status[g] = HIPBLS_OK | HIPBLS_ERR_SIGNATURE | HIPBLS_ERR_COMBINE (empty set, id = 0, duplicate id). */
+int hipbls_threshold_aggregate_batch(const uint8_t* sigs, const int64_t* share_idx,
                                      const uint64_t* group_offsets, uint64_t n_groups,
                                      uint8_t* out_sigs, int32_t* status);
 
@@ -97,7 +129,8 @@ int hipbls_verify_aggregate_batch(const uint8_t* pks, const uint64_t* key_offset
                                   const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_offsets,
                                   int32_t* status);
 
-/* Plain G2 sum of n signatures.  *status = OK | ERR_SIGNATURE | ERR_COMBINE (n == 0). */
+/* Plain G2 sum of n signatures (decoded in parallel, tree-summed).  *status = OK | ERR_SIGNATURE.  As herumi
+ * (tbls/herumi.go:220-242), n == 0 is not an error: the sum is the point at infinity, 0xc0 || 0^95. */
 int hipbls_aggregate(const uint8_t* sigs, uint64_t n, uint8_t* out_sig, int32_t* status);
 
 /* Shamir split: share_i = secret + sum_j poly_tail[j] * i^(j+1) mod r, i = 1..total.
@@ -106,8 +139,9 @@ int hipbls_aggregate(const uint8_t* sigs, uint64_t n, uint8_t* out_sig, int32_t*
 int hipbls_threshold_split(const uint8_t* secret, const uint8_t* poly_tail, uint32_t total, uint32_t threshold,
                            uint8_t* out_shares, int32_t* status);
 
-/* Lagrange recovery of the secret at 0 from n (id, share) pairs.  *status = OK | ERR_SECRET | ERR_COMBINE. */
-int hipbls_recover_secret(const uint8_t* shares, const uint32_t* ids, uint32_t n, uint8_t* out_secret,
+/* Lagrange recovery of the secret at 0 from n (id, share) pairs; ids as in ThresholdAggregate (int mod r).
+ * *status = OK | ERR_SECRET | ERR_COMBINE. */
+int hipbls_recover_secret(const uint8_t* shares, const int64_t* ids, uint32_t n, uint8_t* out_secret,
                           int32_t* status);
 
 /* Random-linear-combination BatchVerify.  Item i is (pks[48 i..], message msg_idx[i], sigs[96 i..]);
@@ -139,14 +173,22 @@ int hipbls_batch_verify_rlc_keys(const uint32_t* key_idx, const uint8_t* sigs, c
  * (synchronizes the device). */
 int hipbls_rlc_stats(uint64_t* windows, uint64_t* windows_failed, uint64_t* items_fallback);
 
+/* Resident H(m) cache used by the host-buffer RLC calls: each distinct message is hashed to G2
+ * once and kept in HBM across calls (FIFO over `capacity` slots, 192 B each); 0 disables it (the default).
+ * Statuses are unchanged by the cache. */
+int hipbls_hcache_config(uint64_t capacity);
+int hipbls_hcache_stats(uint64_t* hits, uint64_t* misses, uint64_t* entries);
+
 /* ------------------------------------------- device-resident variants (inputs already in HBM) ---- */
 /* Same semantics; every pointer is a device pointer; work is enqueued on `stream` (a hipStream_t,
  * NULL = the library's stream) and the call returns without synchronizing. */
 int hipbls_verify_batch_device(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
                                const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream);
-int hipbls_threshold_aggregate_batch_device(const uint8_t* d_sigs, const uint32_t* d_share_idx,
-                                            const uint64_t* d_group_offsets, uint64_t n_groups,
+/* n_parts = group_offsets[n_groups], passed explicitly so the call never reads device memory. */
+int hipbls_threshold_aggregate_batch_device(const uint8_t* d_sigs, const int64_t* d_share_idx,
+                                            const uint64_t* d_group_offsets, uint64_t n_groups, uint64_t n_parts,
                                             uint8_t* d_out_sigs, int32_t* d_status, void* stream);
+int hipbls_aggregate_device(const uint8_t* d_sigs, uint64_t n, uint8_t* d_out_sig, int32_t* d_status, void* stream);
 int hipbls_sign_batch_device(const uint8_t* d_sks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
                              uint64_t n, uint8_t* d_out_sigs, int32_t* d_status, void* stream);
 int hipbls_secret_to_public_key_batch_device(const uint8_t* d_sks, uint64_t n, uint8_t* d_out_pks,
@@ -172,8 +214,9 @@ int hipbls_batch_verify_rlc_keys_device(const uint32_t* d_key_idx, const uint8_t
                                         uint64_t n_msgs, const uint8_t* seed32, int32_t* d_status, void* stream);
 
 /* Average duration (ms) per launch of a kernel over the calls since the last reset, measured with HIP
- * events on the stream it runs on (bench.py roofline).  Names: "verify" (k_verify_fused), "verify_keys",
- * "rlc_items", "rlc_hash", "rlc_window", "rlc_fallback". */
+ * events on the stream it runs on (bench.py roofline; enable with hipbls_set_timing).  Names: "verify"
+ * (k_verify_fused), "verify_keys", "rlc_items", "rlc_hash", "rlc_window", "rlc_fallback", "tagg_scale",
+ * "tagg_sum", "fav". */
 int hipbls_kernel_timing(const char* name, double* avg_ms, uint64_t* launches);
 int hipbls_kernel_timing_reset(void);
 

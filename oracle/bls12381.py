@@ -62,7 +62,10 @@ EDGE_POLICY = {
     "recover_id_zero_or_duplicate": "error 'cannot combine signatures'",
     "recover_single_share": "returns that share's point re-serialized",
     "fast_aggregate_verify_empty": "fails",
-    "aggregate_empty": "error",
+    "aggregate_empty": "no error: the sum of nothing is the point at infinity, 0xc0 || 0^95 "
+                       "(herumi.go:220-242 has no empty check; sig.Aggregate leaves the zero point)",
+    "share_id": "a Go int parsed as Fr (strconv.Itoa -> SetDecString, herumi.go:264-271): id mod r, so "
+                "-k is r - k; id = 0 and duplicate ids fail to combine",
     "secret_zero": "SecretToPublicKey error; secret >= r is a deserialize error",
 }
 
@@ -775,9 +778,7 @@ def threshold_aggregate(partials: Dict[int, bytes]) -> bytes:
 
 
 def aggregate(sigs: Sequence[bytes]) -> bytes:
-    """herumi.go:220-242."""
-    if len(sigs) == 0:
-        raise BLSError("cannot aggregate zero signatures")
+    """herumi.go:220-242: the only error path is deserialization; an empty list sums to infinity."""
     acc = None
     for s in sigs:
         try:

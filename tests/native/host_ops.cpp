@@ -186,7 +186,7 @@ void ht_fp12_op(int op, const uint8_t* a576, const uint8_t* b576, uint8_t* out57
   for (int i = 0; i < 12; ++i) fp_out(out576 + 48 * i, d[i]);
 }
 
-int ht_threshold_aggregate(const uint8_t* sigs, const uint32_t* ids, int n, uint8_t* out96) {
+int ht_threshold_aggregate(const uint8_t* sigs, const int64_t* ids, int n, uint8_t* out96) {
   g2j acc;
   jac_set_inf(acc);
   for (int i = 0; i < n; ++i) {
@@ -273,15 +273,15 @@ extern "C" int ht_rlc_verify(const uint8_t* pks, const uint8_t* sigs, const uint
   c0 = g_fp_mul_count + g_fp_sqr_count;
   for (uint64_t i = 0; i < n; ++i) rlc_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk.data(), rsig.data(), status);
   mark(0);
-  for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, n_msgs, H.data());
+  for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, H.data(), n_msgs, nullptr);
   mark(1);
   std::vector<uint32_t> list;
   for (uint64_t w = 0; w < n_win; ++w)
-    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, status, win.data()))
+    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
   mark(2);
-  for (uint32_t i : list) rlc_fallback_lane(i, pks, sigs, msg_idx, H.data(), n_msgs, status);
+  for (uint32_t i : list) rlc_fallback_lane(i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status);
   mark(3);
   stats3[0] = n_win;
   stats3[1] = stats3[2] = 0;
@@ -311,13 +311,13 @@ extern "C" int ht_rlc_verify_keys(const uint8_t* tab_pks, uint64_t T, const uint
   for (uint64_t i = 0; i < n; ++i)
     rlc_items_lane(i, nullptr, sigs, msg_idx, n, n_msgs, seed, rpk.data(), rsig.data(), status, key_idx, T,
                    code.data(), tab.data());
-  for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, n_msgs, H.data());
+  for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, H.data(), n_msgs, nullptr);
   std::vector<uint32_t> list;
   for (uint64_t w = 0; w < n_win; ++w)
-    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, status, win.data()))
+    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
-  for (uint32_t i : list) rlc_fallback_lane(i, nullptr, sigs, msg_idx, H.data(), n_msgs, status, key_idx, T, tab.data());
+  for (uint32_t i : list) rlc_fallback_lane(i, nullptr, sigs, msg_idx, H.data(), n_msgs, nullptr, status, key_idx, T, tab.data());
   stats3[0] = n_win;
   stats3[1] = stats3[2] = 0;
   for (int32_t x : win)

@@ -200,7 +200,7 @@ def test_threshold_aggregate_host(L):
     ids = [2, 3, 5, 7]
     sigs = b"".join(bls.sign(shares[i], msg) for i in ids)
     import ctypes
-    arr = (ctypes.c_uint32 * 4)(*ids)
+    arr = (ctypes.c_int64 * 4)(*ids)
     out = buf(96)
     assert L.ht_threshold_aggregate(sigs, arr, 4, out) == 0
     assert out.raw == bls.sign(bls.sk_serialize(secret), msg)

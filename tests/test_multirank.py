@@ -8,7 +8,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from charon_amd.shard import gather_bitmaps, pack_bitmap, shard_range, unpack_bitmap
+from charon_amd.shard import (gather_aggregates, gather_bitmaps, gather_node_bitmap, pack_bitmap, shard_range,
+                              unpack_bitmap)
 
 
 def test_shard_range_partitions():
@@ -48,9 +49,16 @@ def _worker(rank, world, port, n_items, q):
         full = torch.randint(0, 4, (n_items,), generator=g, dtype=torch.int32)
         lo, hi = shard_range(n_items, rank, world)
         local = full[lo:hi]
-        bits = gather_bitmaps(pack_bitmap(local))
-        got = torch.cat([unpack_bitmap(bits[r], hi - lo) for r in range(world)])
+        bits = gather_bitmaps(pack_bitmap(local), n_items)
+        got = torch.cat([unpack_bitmap(bits[r], shard_range(n_items, r, world)[1] - shard_range(n_items, r, world)[0])
+                         for r in range(world)])
         q.put((rank, bool(torch.equal(got, full == 0))))
+        q.put((rank, bool(torch.equal(gather_node_bitmap(local, n_items), full == 0))))
+        # aggregate signatures: each rank owns a contiguous validator range (uneven when n_groups % world != 0)
+        n_groups = n_items // 3 + 1
+        allsig = torch.randint(0, 256, (n_groups * 96,), generator=g, dtype=torch.uint8)
+        glo, ghi = shard_range(n_groups, rank, world)
+        q.put((rank, bool(torch.equal(gather_aggregates(allsig[96 * glo:96 * ghi], n_groups), allsig))))
         # max-over-ranks timing reduce used by bench.py
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -59,9 +67,9 @@ def _worker(rank, world, port, n_items, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gloo_bitmap_gather(world):
-    n_items = 4096 * world  # equal shards, as in the weak-scaling bench
+@pytest.mark.parametrize("world,n_items", [(2, 4096 * 2), (2, 4097 * 2 + 1), (3, 1001)])
+def test_gloo_bitmap_gather(world, n_items):
+    """Equal shards (the weak-scaling bench) and uneven ones (a node batch that does not divide by world)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -71,5 +79,5 @@ def test_gloo_bitmap_gather(world):
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    results = [q.get(timeout=5) for _ in range(2 * world)]
+    results = [q.get(timeout=5) for _ in range(4 * world)]
     assert all(ok for _, ok in results), results
