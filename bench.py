@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--n", type=int, default=65536, help="verifies per GPU per step (C2: 65,536)")
     ap.add_argument("--tagg-groups", type=int, default=10000, help="C3 validators per GPU (0 = skip)")
     ap.add_argument("--tagg-steps", type=int, default=2)
-    ap.add_argument("--cpu-sample", type=int, default=16, help="oracle verifies for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=4096,
+                    help="C2 items verified by the C++ CPU baseline, one thread per core (0 = skip)")
     ap.add_argument("--rlc-validators", type=int, default=32768,
                     help="C4 validators per GPU (x4 partials; 32,768 = the 1M-partial node batch / 8 GPUs; 0 = skip)")
     ap.add_argument("--rlc-steps", type=int, default=3)
@@ -152,22 +153,90 @@ def traffic_from_pmc(path=os.path.join(ROOT, "profiles", "r01_pmc_verify.json"))
         return None
 
 
-def cpu_baseline(n_sample, rng):
-    """Oracle (oracle/bls12381.py, pure Python, 1 core) timed on this host: kind 'port'."""
-    from oracle import bls12381 as bls
-    sks = [rng.randrange(1, R_ORDER).to_bytes(32, "big") for _ in range(4)]
-    items = []
-    for i in range(n_sample):
-        sk = sks[i % 4]
-        m = rng.randbytes(32)
-        items.append((bls.secret_to_public_key(sk), m, bls.sign(sk, m)))
-    t0 = time.perf_counter()
-    ok = sum(bls.verify_status(pk, m, s) == 0 for pk, m, s in items)
-    dt = time.perf_counter() - t0
-    assert ok == n_sample
-    return {"value": round(n_sample / dt, 3), "unit": "verifies/s", "cores": 1, "kind": "port",
-            "sample": "%d tbls.Verify calls of C2 items (32-byte roots) through oracle/bls12381.py, "
-                      "single-threaded CPython; not herumi (no Go toolchain / herumi module on the box)" % n_sample}
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    """One thread per host core this job may use: the box exports OMP_NUM_THREADS = its CPU share."""
+    n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return n
+
+
+def cpu_baseline(impl, c2, n_sample, rng):
+    """SURVEY.md §8d(2) / BASELINE.md: the repo's C++ restatement of the same per-item operations
+    (tests/native/cpu_baseline.cpp over charon_amd/csrc/ops.h, -O3, 6 x 64-bit Montgomery product), one
+    thread per host core, timed on this box.  kind 'port' -- NOT herumi (no Go toolchain or herumi module
+    here).  Two samples: (1) n_sample C2 items (the bench's own inputs) -> verifies/s, the `value`; (2) the
+    C1 workload (BASELINE configs[0]): 250 DVs x 4-of-6 -> 1,000 partial Verify + 250 ThresholdAggregate +
+    250 Verify of the aggregates, inputs made by the GPU engine, statuses checked."""
+    from tests.hostlib import cpu_baseline_lib
+    cb = cpu_baseline_lib()
+    threads = cpu_threads()
+    pks, roots, sigs, bad = c2
+    n = min(n_sample, len(pks))
+    offs = (ctypes.c_uint64 * (n + 1))(*[32 * i for i in range(n + 1)])
+    st = (ctypes.c_int32 * n)()
+    dt = cb.cb_verify_batch(b"".join(pks[:n]), b"".join(roots[:n]), offs, b"".join(sigs[:n]), n, st, threads)
+    assert {i for i in range(n) if st[i] != 0} == {i for i in bad if i < n}, "CPU baseline bitmap mismatch"
+    # C1: 250 DVs x 4-of-6
+    G, t, nsh = 250, 4, 6
+    secrets_ = [rng.randrange(1, R_ORDER) for _ in range(G)]
+    droots = [rng.randbytes(32) for _ in range(G)]
+    psks, pmsg, pids, poffs = [], [], [], [0]
+    for g in range(G):
+        poly = [secrets_[g]] + [rng.randrange(R_ORDER) for _ in range(t - 1)]
+        for i in sorted(rng.sample(range(1, nsh + 1), t)):
+            acc = 0
+            for c in reversed(poly):
+                acc = (acc * i + c) % R_ORDER
+            psks.append(acc.to_bytes(32, "big"))
+            pmsg.append(droots[g])
+            pids.append(i)
+        poffs.append(len(pids))
+    ppks, _ = impl.secret_to_public_key_batch(psks)
+    psig, _ = impl.sign_batch(psks, pmsg)
+    dpk, _ = impl.secret_to_public_key_batch([s.to_bytes(32, "big") for s in secrets_])
+    np_ = len(psks)
+    o1 = (ctypes.c_uint64 * (np_ + 1))(*[32 * i for i in range(np_ + 1)])
+    s1 = (ctypes.c_int32 * np_)()
+    t_ver = cb.cb_verify_batch(b"".join(ppks), b"".join(pmsg), o1, b"".join(psig), np_, s1, threads)
+    ids = (ctypes.c_int64 * np_)(*pids)
+    go = (ctypes.c_uint64 * (G + 1))(*poffs)
+    agg = ctypes.create_string_buffer(96 * G)
+    s2 = (ctypes.c_int32 * G)()
+    t_agg = cb.cb_threshold_aggregate_batch(b"".join(psig), ids, go, G, agg, s2, threads)
+    aggs = [agg.raw[96 * g:96 * g + 96] for g in range(G)]
+    o3 = (ctypes.c_uint64 * (G + 1))(*[32 * i for i in range(G + 1)])
+    s3 = (ctypes.c_int32 * G)()
+    t_aver = cb.cb_verify_batch(b"".join(dpk), b"".join(droots), o3, b"".join(aggs), G, s3, threads)
+    assert set(s1) == {0} and set(s2) == {0} and set(s3) == {0}, "CPU baseline C1 statuses"
+    gpu_aggs = impl.batch_threshold_aggregate([dict(zip(pids[poffs[g]:poffs[g + 1]], psig[poffs[g]:poffs[g + 1]]))
+                                               for g in range(G)])
+    assert gpu_aggs == aggs, "CPU and GPU threshold aggregates differ"
+    c1 = t_ver + t_agg + t_aver
+    return {"value": round(n / dt, 1), "unit": "verified partial sigs/s", "cores": threads, "kind": "port",
+            "label": "cpu-restatement, not herumi",
+            "cpu_model": _cpu_model(),
+            "sample": "%d C2 items (the bench's own 32-byte-root inputs, 1%% corrupted) through "
+                      "tests/native/cpu_baseline.cpp (charon_amd/csrc/ops.h compiled -O3 for x86-64, 6x64-bit "
+                      "Montgomery product), %d threads; herumi/Go absent on the box (SURVEY.md 8c)" % (n, threads),
+            "c1_workload": {"config": "BASELINE configs[0]: 250 DVs x 4-of-6: 1,000 Verify + 250 ThresholdAggregate "
+                                      "+ 250 Verify of the aggregates",
+                            "seconds": round(c1, 4), "verify_s": round(t_ver, 4), "threshold_aggregate_s": round(t_agg, 4),
+                            "aggregate_verify_s": round(t_aver, 4),
+                            "verified_partial_sigs_per_s": round(np_ / t_ver, 1),
+                            "threshold_aggregates_per_s": round(G / t_agg, 1)}}
 
 
 def main():
@@ -533,7 +602,7 @@ def main():
                 "kernel_launches": int(launches.value),
             }
         if world == 1 and args.cpu_sample > 0:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_sample, random.Random(SEED))
+            out["cpu_baseline"] = cpu_baseline(impl, (pks, roots, sigs, bad), args.cpu_sample, random.Random(SEED))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

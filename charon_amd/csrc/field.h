@@ -229,16 +229,59 @@ BLS_HD BLS_INLINE void fp_sqr(fp& r, const fp& a) {
   fp_from_vec(r, fp_mul_dev(v, v));
 }
 #else
+#if defined(BLS_HOST_FAST_MUL)
+// Host CPU baseline build (tests/native/cpu_baseline.cpp): the same Montgomery product (R = 2^384) on 6 x 64-bit
+// limbs with 64x64->128 multiplies -- x86-64's native width -- instead of the 12 x 32-bit form the GPU uses.
+// Little-endian: the 12 32-bit limbs ARE the 6 64-bit limbs.  p's top limb < 2^63: no-carry CIOS.
+static inline void fp_mul_impl64(fp& r, const fp& a, const fp& b) {
+  typedef unsigned __int128 u128;
+  static const uint64_t P64[6] = {0xb9feffffffffaaabull, 0x1eabfffeb153ffffull, 0x6730d2a0f6b0f624ull,
+                                  0x64774b84f38512bfull, 0x4b1ba7b6434bacd7ull, 0x1a0111ea397fe69aull};
+  const uint64_t PINV64 = 0x89f3fffcfffcfffdull;
+  uint64_t A[6], B[6], t[6] = {0, 0, 0, 0, 0, 0};
+  __builtin_memcpy(A, a.v, 48);
+  __builtin_memcpy(B, b.v, 48);
+  for (int i = 0; i < 6; ++i) {
+    u128 x = (u128)A[0] * B[i] + t[0];
+    t[0] = (uint64_t)x;
+    const uint64_t m = t[0] * PINV64;
+    u128 y = (u128)m * P64[0] + t[0];
+    for (int j = 1; j < 6; ++j) {
+      x = (u128)A[j] * B[i] + t[j] + (uint64_t)(x >> 64);
+      t[j] = (uint64_t)x;
+      y = (u128)m * P64[j] + t[j] + (uint64_t)(y >> 64);
+      t[j - 1] = (uint64_t)y;
+    }
+    t[5] = (uint64_t)(y >> 64) + (uint64_t)(x >> 64);
+  }
+  uint64_t d[6];
+  unsigned char br = 0;
+  for (int i = 0; i < 6; ++i) {
+    const u128 s = (u128)t[i] - P64[i] - br;
+    d[i] = (uint64_t)s;
+    br = (unsigned char)((s >> 64) != 0);
+  }
+  __builtin_memcpy(r.v, br ? t : d, 48);
+}
+#endif
 BLS_HD BLS_NOINLINE fp fp_mul_v(fp a, fp b) {
   BLS_COUNT_MUL();
   fp r;
+#if defined(BLS_HOST_FAST_MUL)
+  fp_mul_impl64(r, a, b);
+#else
   fp_mul_impl(r, a, b);
+#endif
   return r;
 }
 BLS_HD BLS_NOINLINE fp fp_sqr_v(fp a) {
   BLS_COUNT_SQR();
   fp r;
+#if defined(BLS_HOST_FAST_MUL)
+  fp_mul_impl64(r, a, a);
+#else
   fp_mul_impl(r, a, a);
+#endif
   return r;
 }
 BLS_HD BLS_INLINE void fp_mul(fp& r, const fp& a, const fp& b) { r = fp_mul_v(a, b); }

@@ -18,9 +18,31 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+CB_SRC = os.path.join(HERE, "native", "cpu_baseline.cpp")
+CB_LIB = os.path.join(HERE, "native", "libcpu_baseline.so")
+
+
 def build():
     if _stale():
         subprocess.check_call(["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-o", LIB, SRC])
+    build_cpu_baseline()
+
+
+def build_cpu_baseline():
+    """-O3, portable x86-64 (the .so built here runs on the GPU box's host CPU), one thread per core at run time."""
+    deps = [CB_SRC] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    if not os.path.exists(CB_LIB) or any(os.path.getmtime(d) > os.path.getmtime(CB_LIB) for d in deps):
+        subprocess.check_call(["g++", "-std=c++17", "-O3", "-fPIC", "-shared", "-pthread", "-o", CB_LIB, CB_SRC])
+
+
+def cpu_baseline_lib():
+    """ctypes handle on tests/native/libcpu_baseline.so (bench.py's cpu_baseline leg only)."""
+    if not os.path.exists(CB_LIB):
+        build_cpu_baseline()
+    lib = ctypes.CDLL(CB_LIB)
+    lib.cb_verify_batch.restype = ctypes.c_double
+    lib.cb_threshold_aggregate_batch.restype = ctypes.c_double
+    return lib
 
 
 _lib = None
