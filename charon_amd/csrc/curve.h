@@ -70,7 +70,8 @@ BLS_HD BLS_INLINE void jac_neg(jac<F>& r, const jac<F>& a) {
 
 // dbl-2009-l (a = 0)
 template <class F>
-BLS_HD BLS_CALL void jac_dbl(jac<F>& r, const jac<F>& p) {
+BLS_HD BLS_CALL void jac_dbl(jac<F>& r, const jac<F>& p_in) {
+  const jac<F> p = p_in;
   F A, B, C, D, E, Fv, t;
   f_sqr(A, p.x);
   f_sqr(B, p.y);
@@ -100,7 +101,9 @@ BLS_HD BLS_CALL void jac_dbl(jac<F>& r, const jac<F>& p) {
 
 // add-2007-bl with the exceptional cases handled (P = Q doubles, P = -Q gives infinity)
 template <class F>
-BLS_HD BLS_CALL void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
+BLS_HD BLS_CALL void jac_add(jac<F>& r, const jac<F>& p_in, const jac<F>& q_in) {
+  const jac<F> p = p_in;
+  const jac<F> q = q_in;
   if (jac_is_inf(p)) {
     r = q;
     return;
@@ -155,7 +158,9 @@ BLS_HD BLS_CALL void jac_add(jac<F>& r, const jac<F>& p, const jac<F>& q) {
 
 // mixed addition r = p + q with q affine (madd-2007-bl), exceptional cases handled
 template <class F>
-BLS_HD BLS_CALL void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) {
+BLS_HD BLS_CALL void jac_add_aff(jac<F>& r, const jac<F>& p_in, const aff<F>& q_in) {
+  const jac<F> p = p_in;
+  const aff<F> q = q_in;
   if (jac_is_inf(p)) {
     jac_from_aff(r, q);
     return;
@@ -202,7 +207,8 @@ BLS_HD BLS_CALL void jac_add_aff(jac<F>& r, const jac<F>& p, const aff<F>& q) {
 
 // r = [k] p for a 64-bit scalar k (uniform across lanes when k is a constant)
 template <class F>
-BLS_HD BLS_CALL void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
+BLS_HD BLS_CALL void jac_mul_u64(jac<F>& r, const jac<F>& p_in, uint64_t k) {
+  const jac<F> p = p_in;
   jac<F> acc;
   jac_set_inf(acc);
   for (int i = 63; i >= 0; --i) {
@@ -214,7 +220,8 @@ BLS_HD BLS_CALL void jac_mul_u64(jac<F>& r, const jac<F>& p, uint64_t k) {
 
 // r = [k] p for a scalar given as nlimbs little-endian 32-bit limbs
 template <class F>
-BLS_HD BLS_CALL void jac_mul_limbs(jac<F>& r, const jac<F>& p, const uint32_t* k, int nlimbs) {
+BLS_HD BLS_CALL void jac_mul_limbs(jac<F>& r, const jac<F>& p_in, const uint32_t* k, int nlimbs) {
+  const jac<F> p = p_in;
   jac<F> acc;
   jac_set_inf(acc);
   for (int i = nlimbs * 32 - 1; i >= 0; --i) {
@@ -226,7 +233,9 @@ BLS_HD BLS_CALL void jac_mul_limbs(jac<F>& r, const jac<F>& p, const uint32_t* k
 
 // Jacobian equality without normalization
 template <class F>
-BLS_HD BLS_CALL bool jac_eq(const jac<F>& p, const jac<F>& q) {
+BLS_HD BLS_CALL bool jac_eq(const jac<F>& p_in, const jac<F>& q_in) {
+  const jac<F> p = p_in;
+  const jac<F> q = q_in;
   const bool pi = jac_is_inf(p), qi = jac_is_inf(q);
   if (pi || qi) return pi && qi;
   F z1z1, z2z2, a, b;
@@ -243,7 +252,8 @@ BLS_HD BLS_CALL bool jac_eq(const jac<F>& p, const jac<F>& q) {
 }
 
 template <class F>
-BLS_HD BLS_CALL void jac_to_aff(aff<F>& r, const jac<F>& p) {
+BLS_HD BLS_CALL void jac_to_aff(aff<F>& r, const jac<F>& p_in) {
+  const jac<F> p = p_in;
   F zi, zi2;
   f_inv(zi, p.z);
   f_sqr(zi2, zi);
@@ -312,7 +322,8 @@ BLS_HD BLS_INLINE bool fp2_is_lex_largest(const fp2& y) {
 
 // 48-byte compressed G1 -> affine; returns DEC_OK / DEC_BAD / DEC_INF.  Subgroup test included.
 
-BLS_HD BLS_CALL bool g1_in_subgroup(const g1j& p) {
+BLS_HD BLS_CALL bool g1_in_subgroup(const g1j& p_in) {
+  const g1j p = p_in;
   if (jac_is_inf(p)) return true;
   g1j q;
   jac_mul_u64(q, p, X_ABS);
@@ -323,7 +334,8 @@ BLS_HD BLS_CALL bool g1_in_subgroup(const g1j& p) {
   phi.z = p.z;
   return jac_eq(q, phi);
 }
-BLS_HD BLS_CALL bool g2_in_subgroup(const g2j& p) {
+BLS_HD BLS_CALL bool g2_in_subgroup(const g2j& p_in) {
+  const g2j p = p_in;
   if (jac_is_inf(p)) return true;
   g2j q, ps;
   jac_mul_u64(q, p, X_ABS);
@@ -331,7 +343,8 @@ BLS_HD BLS_CALL bool g2_in_subgroup(const g2j& p) {
   g2_psi(ps, p);
   return jac_eq(q, ps);
 }
-BLS_HD BLS_CALL void g2_clear_cofactor(g2j& r, const g2j& p) {
+BLS_HD BLS_CALL void g2_clear_cofactor(g2j& r, const g2j& p_in) {
+  const g2j p = p_in;
   g2j t1, t2, t3, np;
   jac_mul_u64(t1, p, X_ABS);
   jac_neg(t1, t1);  // t1 = [x] P
@@ -376,7 +389,8 @@ BLS_HD BLS_INLINE uint64_t u256_divmod_xabs(uint32_t* k) {
 // On G2, psi = [x] and x = -|x|, so with k = e0 + e1|x| + e2|x|^2 + e3|x|^3 (base-|x| digits,
 // r < |x|^4) [k]P = sum_i e_i (-psi)^i(P): 64 doublings and <= 64 additions over a 16-entry
 // subset-sum table instead of a 255-bit double-and-add.
-BLS_HD BLS_CALL void g2_mul_glv4(g2j& r, const g2j& p, const uint32_t* k_plain) {
+BLS_HD BLS_CALL void g2_mul_glv4(g2j& r, const g2j& p_in, const uint32_t* k_plain) {
+  const g2j p = p_in;
   uint32_t k[8];
   for (int i = 0; i < 8; ++i) k[i] = k_plain[i];
   uint64_t e[4];
@@ -405,7 +419,8 @@ BLS_HD BLS_CALL void g2_mul_glv4(g2j& r, const g2j& p, const uint32_t* k_plain) 
   r = acc;
 }
 
-BLS_HD BLS_CALL bool fp2_sqrt(fp2& r, const fp2& a) {
+BLS_HD BLS_CALL bool fp2_sqrt(fp2& r, const fp2& a_in) {
+  const fp2 a = a_in;
   // a = a0 + a1 u: s = sqrt(a0^2 + a1^2), t = (a0 + s)/2, then sqrt(a) = x0 + a1/(2 x0) u with
   // x0^2 = t, or a1/(2 x0) + x0 u with x0^2 = -t when t is not a square.  One power
   // z = t^((p-3)/4) gives both x0 = t z and 1/x0 = z (t square) or -z (t^((p-1)/2) = -1).

@@ -76,27 +76,32 @@ BLS_HD BLS_INLINE bool fp_eq(const fp& a, const fp& b) {
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
-// Device: explicit 32-bit carry chains (__builtin_addc/__builtin_subc lower to v_add_co/v_addc_co and
-// v_sub_co/v_subb_co), ~43 VALU per add or sub; the generic 64-bit form below compiles to ~110.
+}  // namespace bls
+#include "fp_asm_gfx950.h"
+namespace bls {
+// Device: each modular add / sub / negation is ONE asm block (tools/gen_fp_asm.py gen_add / gen_sub): a single
+// VCC carry chain, the borrow turned into a VGPR lane mask, and v_bfi_b32 / v_and_b32 selects -- 37 VALU, no
+// s_nop padding (compiled C++ interleaves two carry chains on VCC and an SGPR pair and pays an s_nop per step)
+// and no VOP2 v_cndmask_b32_e32 (~19 cycles on gfx950).  Measured: profiles/r02_op_probe.txt.
+#define BLS_FP12_OUT(x) "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), \
+                        "=&v"(x[7]), "=&v"(x[8]), "=&v"(x[9]), "=&v"(x[10]), "=&v"(x[11])
+#define BLS_FP12_IN(x) "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), \
+                       "v"(x[8]), "v"(x[9]), "v"(x[10]), "v"(x[11])
 // r = a + b mod p
 BLS_HD BLS_INLINE void fp_add(fp& r, const fp& a, const fp& b) {
-  uint32_t s[12], d[12], c = 0, br = 0;
+  uint32_t o[12], t[12], m;
+  asm volatile(BLS_FP_ADD_ASM : BLS_FP12_OUT(o), BLS_FP12_OUT(t), "=&v"(m)
+               : BLS_FP12_IN(a.v), BLS_FP12_IN(b.v), BLS_FP12_IN(P_LIMBS) : "vcc");
 #pragma unroll
-  for (int i = 0; i < 12; ++i) s[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
-  // s < 2p < 2^384: subtract p, keep s on borrow
-#pragma unroll
-  for (int i = 0; i < 12; ++i) d[i] = __builtin_subc(s[i], P_LIMBS[i], br, &br);
-#pragma unroll
-  for (int i = 0; i < 12; ++i) r.v[i] = br ? s[i] : d[i];
+  for (int i = 0; i < 12; ++i) r.v[i] = o[i];
 }
 // r = a - b mod p
 BLS_HD BLS_INLINE void fp_sub(fp& r, const fp& a, const fp& b) {
-  uint32_t d[12], c = 0, br = 0;
+  uint32_t o[12], t[12], m;
+  asm volatile(BLS_FP_SUB_ASM : BLS_FP12_OUT(o), BLS_FP12_OUT(t), "=&v"(m)
+               : BLS_FP12_IN(a.v), BLS_FP12_IN(b.v), BLS_FP12_IN(P_LIMBS) : "vcc");
 #pragma unroll
-  for (int i = 0; i < 12; ++i) d[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
-  const uint32_t m = 0u - br;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) r.v[i] = __builtin_addc(d[i], P_LIMBS[i] & m, c, &c);
+  for (int i = 0; i < 12; ++i) r.v[i] = o[i];
 }
 #else
 // r = a + b mod p
@@ -145,11 +150,21 @@ BLS_HD BLS_INLINE void fp_sub(fp& r, const fp& a, const fp& b) {
 
 #endif
 
+#if defined(__HIP_DEVICE_COMPILE__)
+BLS_HD BLS_INLINE void fp_neg(fp& r, const fp& a) {
+  uint32_t o[12], t[12], m;
+  asm volatile(BLS_FP_NEG_ASM : BLS_FP12_OUT(o), BLS_FP12_OUT(t), "=&v"(m) : BLS_FP12_IN(a.v), BLS_FP12_IN(P_LIMBS)
+               : "vcc");
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = o[i];
+}
+#else
 BLS_HD BLS_INLINE void fp_neg(fp& r, const fp& a) {
   fp z;
   fp_set_zero(z);
   fp_sub(r, z, a);
 }
+#endif
 
 BLS_HD BLS_INLINE void fp_dbl(fp& r, const fp& a) { fp_add(r, a, a); }
 
@@ -197,9 +212,6 @@ BLS_HD BLS_INLINE void fp_mul_impl(fp& r, const fp& a, const fp& b) {
 // Operands are pinned: a in v[0:11] (result out), b in v[12:23].
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef uint32_t u32x12 __attribute__((ext_vector_type(12)));
-}  // namespace bls
-#include "fp_asm_gfx950.h"
-namespace bls {
 // Never called: hosts the routine's code (entered only at the local label).
 __device__ __attribute__((used, noinline)) static void bls_fp_asm_routines() {
   asm volatile("s_endpgm\n.p2align 6\n.type bls_fp_mul_rt,@function\nbls_fp_mul_rt:\n\t" BLS_FP_MUL_ASM_BODY

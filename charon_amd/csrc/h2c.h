@@ -231,7 +231,10 @@ BLS_HD BLS_INLINE void sswu_den(fp2& zu2, fp2& den, const fp2& u) {
   fp2_add(den, den, zu2);
 }
 // SSWU with tv1 = inv0(den) supplied by the caller (so hash_to_g2 can share one inversion)
-BLS_HD BLS_CALL void map_to_curve_sswu_tv(g2a& out, const fp2& u, const fp2& zu2, const fp2& tv1) {
+BLS_HD BLS_CALL void map_to_curve_sswu_tv(g2a& out, const fp2& u_in, const fp2& zu2_in, const fp2& tv1_in) {
+  const fp2 u = u_in;
+  const fp2 zu2 = zu2_in;
+  const fp2 tv1 = tv1_in;
   fp2 x1, gx1, t, y, x;
   if (fp2_is_zero(tv1)) {
     x1 = SSWU_B_OVER_ZA;
@@ -270,7 +273,8 @@ BLS_HD BLS_CALL void map_to_curve_sswu(g2a& out, const fp2& u) {
   map_to_curve_sswu_tv(out, u, zu2, tv1);
 }
 
-BLS_HD BLS_CALL void iso_map_g2(g2j& out, const g2a& p) {
+BLS_HD BLS_CALL void iso_map_g2(g2j& out, const g2a& p_in) {
+  const g2a p = p_in;
   // x = xn/xd, y = y * yn/yd  ->  Jacobian (xn xd yd^2, y yn xd^3 yd^2, xd yd)
   const fp2& x = p.x;
   fp2 xn, xd, yn, yd, t;

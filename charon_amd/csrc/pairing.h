@@ -23,7 +23,10 @@ struct g1_pair_in {  // P in affine coordinates, or is_inf
 
 // r = f^((p^12-1)/r * 3)
 
-BLS_HD BLS_CALL void miller_dbl_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const fp& xp, const fp& yp) {
+BLS_HD BLS_CALL void miller_dbl_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const fp& xp_in, const fp& yp_in) {
+  const fp xp = xp_in;
+  const fp yp = yp_in;
+  g2j T = T_in;
   // Homogeneous coordinates (x = X/Z, y = Y/Z).  Note: T.z here is the projective Z, not Jacobian.
   fp2 A, B, C, E, F, G, H, J, t;
   fp2_mul(A, T.x, T.y);
@@ -60,10 +63,15 @@ BLS_HD BLS_CALL void miller_dbl_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const fp
   T.x = X3;
   T.y = Y3;
   T.z = Z3;
+  T_in = T;
 }
 
-BLS_HD BLS_CALL void miller_add_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const g2a& Q, const fp& xp,
-                                         const fp& yp) {
+BLS_HD BLS_CALL void miller_add_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const g2a& Q_in, const fp& xp_in,
+                                         const fp& yp_in) {
+  const g2a Q = Q_in;
+  const fp xp = xp_in;
+  const fp yp = yp_in;
+  g2j T = T_in;
   fp2 theta, lambda, C, D, E, F, G, H, t;
   fp2_mul(t, Q.y, T.z);
   fp2_sub(theta, T.y, t);
@@ -96,6 +104,7 @@ BLS_HD BLS_CALL void miller_add_step(g2j& T, fp2& g0, fp2& g1, fp2& h1, const g2
   T.x = X3;
   T.y = Y3;
   T.z = Z3;
+  T_in = T;
 }
 
 BLS_HD BLS_CALL void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bool* skip, int n) {
@@ -139,7 +148,8 @@ BLS_HD BLS_CALL void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bo
 }
 
 // r = a^|x| for a in the cyclotomic subgroup
-BLS_HD BLS_CALL void fp12_cyc_exp_xabs(fp12& r, const fp12& a) {
+BLS_HD BLS_CALL void fp12_cyc_exp_xabs(fp12& r, const fp12& a_in) {
+  const fp12 a = a_in;
   fp12 acc = a;
   for (int bit = 62; bit >= 0; --bit) {
     fp12_cyclotomic_sqr(acc, acc);
@@ -148,7 +158,8 @@ BLS_HD BLS_CALL void fp12_cyc_exp_xabs(fp12& r, const fp12& a) {
   r = acc;
 }
 
-BLS_HD BLS_CALL void final_exponentiation(fp12& r, const fp12& f) {
+BLS_HD BLS_CALL void final_exponentiation(fp12& r, const fp12& f_in) {
+  const fp12 f = f_in;
   // easy part: f^((p^6-1)(p^2+1))
   fp12 t, fi, m;
   fp12_conj(t, f);

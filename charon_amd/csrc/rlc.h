@@ -57,7 +57,9 @@ BLS_HD BLS_INLINE void soa_load(uint32_t* dst, const uint32_t* base, uint64_t st
 
 // [a] P + [b] Q with one shared doubling chain (Shamir's trick), 32-bit a, b
 template <class F>
-BLS_HD BLS_CALL void jac_mul2_u32(jac<F>& r, const jac<F>& P, const jac<F>& Q, uint32_t a, uint32_t b) {
+BLS_HD BLS_CALL void jac_mul2_u32(jac<F>& r, const jac<F>& P_in, const jac<F>& Q_in, uint32_t a, uint32_t b) {
+  const jac<F> P = P_in;
+  const jac<F> Q = Q_in;
   jac<F> PQ, acc, addend;
   jac_add(PQ, P, Q);
   jac_set_inf(acc);

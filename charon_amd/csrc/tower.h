@@ -138,7 +138,8 @@ BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
   fp_mul(r.c0, s, d);
   fp_add(r.c1, m, m);
 }
-BLS_HD BLS_CALL void fp2_inv(fp2& r, const fp2& a) {
+BLS_HD BLS_CALL void fp2_inv(fp2& r, const fp2& a_in) {
+  const fp2 a = a_in;
   fp t0, t1;
   fp_sqr(t0, a.c0);
   fp_sqr(t1, a.c1);
@@ -149,8 +150,10 @@ BLS_HD BLS_CALL void fp2_inv(fp2& r, const fp2& a) {
   fp_neg(r.c1, t0);
 }
 
-BLS_HD BLS_CALL void fp6_mul(fp6& r, const fp6& a, const fp6& b) {
-  // Karatsuba over Fp2 (6 Fp2 products)
+BLS_HD BLS_CALL void fp6_mul(fp6& r, const fp6& a_in, const fp6& b_in) {
+  // Karatsuba over Fp2 (6 Fp2 products).  Operands are copied in once: referenced operands live in the
+  // caller's frame, and re-reading them around every product exposes a flat-load round trip each time.
+  const fp6 a = a_in, b = b_in;
   fp2 t0, t1, t2, s0, s1, u0, u1, u2;
   fp2_mul(t0, a.c0, b.c0);
   fp2_mul(t1, a.c1, b.c1);
@@ -183,7 +186,8 @@ BLS_HD BLS_CALL void fp6_mul(fp6& r, const fp6& a, const fp6& b) {
   r.c1 = u1;
   r.c2 = u2;
 }
-BLS_HD BLS_CALL void fp6_sqr(fp6& r, const fp6& a) {
+BLS_HD BLS_CALL void fp6_sqr(fp6& r, const fp6& a_in) {
+  const fp6 a = a_in;
   // Chung-Hasan SQR2
   fp2 s0, s1, s2, s3, s4, t;
   fp2_sqr(s0, a.c0);
@@ -208,7 +212,8 @@ BLS_HD BLS_CALL void fp6_sqr(fp6& r, const fp6& a) {
   r.c1 = c1;
   r.c2 = c2;
 }
-BLS_HD BLS_CALL void fp6_inv(fp6& r, const fp6& a) {
+BLS_HD BLS_CALL void fp6_inv(fp6& r, const fp6& a_in) {
+  const fp6 a = a_in;
   fp2 c0, c1, c2, t, s;
   fp2_sqr(c0, a.c0);
   fp2_mul(t, a.c1, a.c2);
@@ -232,7 +237,10 @@ BLS_HD BLS_CALL void fp6_inv(fp6& r, const fp6& a) {
   fp2_mul(r.c1, c1, t);
   fp2_mul(r.c2, c2, t);
 }
-BLS_HD BLS_CALL void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& b1) {
+BLS_HD BLS_CALL void fp6_mul_01(fp6& r, const fp6& a_in, const fp2& b0_in, const fp2& b1_in) {
+  const fp6 a = a_in;
+  const fp2 b0 = b0_in;
+  const fp2 b1 = b1_in;
   // (a0 + a1 v + a2 v^2)(b0 + b1 v): 5 Fp2 products
   fp2 t0, t1, s0, s1, u;
   fp2_mul(t0, a.c0, b0);
@@ -255,7 +263,9 @@ BLS_HD BLS_CALL void fp6_mul_01(fp6& r, const fp6& a, const fp2& b0, const fp2& 
   r.c1 = c1;
   r.c2 = c2;
 }
-BLS_HD BLS_CALL void fp6_mul_1(fp6& r, const fp6& a, const fp2& b1) {
+BLS_HD BLS_CALL void fp6_mul_1(fp6& r, const fp6& a_in, const fp2& b1_in) {
+  const fp6 a = a_in;
+  const fp2 b1 = b1_in;
   // (a0 + a1 v + a2 v^2) b1 v = xi a2 b1 + a0 b1 v + a1 b1 v^2
   fp2 c0, c1, c2;
   fp2_mul(c0, a.c2, b1);
@@ -267,7 +277,9 @@ BLS_HD BLS_CALL void fp6_mul_1(fp6& r, const fp6& a, const fp2& b1) {
   r.c2 = c2;
 }
 
-BLS_HD BLS_CALL void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
+BLS_HD BLS_CALL void fp12_mul(fp12& r, const fp12& a_in, const fp12& b_in) {
+  const fp12 a = a_in;
+  const fp12 b = b_in;
   fp6 t0, t1, s0, s1;
   fp6_mul(t0, a.c0, b.c0);
   fp6_mul(t1, a.c1, b.c1);
@@ -281,8 +293,9 @@ BLS_HD BLS_CALL void fp12_mul(fp12& r, const fp12& a, const fp12& b) {
   fp6_add(r.c0, t0, t1);
   r.c1 = c1;
 }
-BLS_HD BLS_CALL void fp12_sqr(fp12& r, const fp12& a) {
+BLS_HD BLS_CALL void fp12_sqr(fp12& r, const fp12& a_in) {
   // complex squaring: c0 = (a0+a1)(a0+v a1) - t - v t, c1 = 2t, t = a0 a1
+  const fp12 a = a_in;
   fp6 t, s0, s1, vt;
   fp6_mul(t, a.c0, a.c1);
   fp6_add(s0, a.c0, a.c1);
@@ -294,7 +307,8 @@ BLS_HD BLS_CALL void fp12_sqr(fp12& r, const fp12& a) {
   fp6_sub(r.c0, s0, vt);
   fp6_add(r.c1, t, t);
 }
-BLS_HD BLS_CALL void fp12_inv(fp12& r, const fp12& a) {
+BLS_HD BLS_CALL void fp12_inv(fp12& r, const fp12& a_in) {
+  const fp12 a = a_in;
   fp6 t0, t1;
   fp6_sqr(t0, a.c0);
   fp6_sqr(t1, a.c1);
@@ -305,7 +319,11 @@ BLS_HD BLS_CALL void fp12_inv(fp12& r, const fp12& a) {
   fp6_mul(t1, a.c1, t0);
   fp6_neg(r.c1, t1);
 }
-BLS_HD BLS_CALL void fp12_mul_line(fp12& f, const fp2& g0, const fp2& g1, const fp2& h1) {
+BLS_HD BLS_CALL void fp12_mul_line(fp12& f_in, const fp2& g0_in, const fp2& g1_in, const fp2& h1_in) {
+  const fp2 g0 = g0_in;
+  const fp2 g1 = g1_in;
+  const fp2 h1 = h1_in;
+  fp12 f = f_in;
   // f = (a0 + a1 w)(G + H w), G = g0 + g1 v, H = h1 v:
   //   c0 = a0 G + v (a1 H),  c1 = (a0 + a1)(G + H) - a0 G - a1 H
   fp6 t0, t1, s;
@@ -319,12 +337,20 @@ BLS_HD BLS_CALL void fp12_mul_line(fp12& f, const fp2& g0, const fp2& g1, const 
   fp6_sub(f.c1, s, t1);
   fp6_mul_v(t1, t1);
   fp6_add(f.c0, t0, t1);
+  f_in = f;
 }
 // f *= la * lb for two M-twist lines l = (g0 + g1 v) + (h1 v) w.  The line product is
 // (c0 dense) + (x v + y v^2) w with w^2 = v, v^3 = xi (6 Fp2 products); multiplying it into f
 // costs 17 more, 23 in all instead of 26 for two fp12_mul_line calls.
-BLS_HD BLS_CALL void fp12_mul_line2(fp12& f, const fp2& ga0, const fp2& ga1, const fp2& ha1, const fp2& gb0,
-                                    const fp2& gb1, const fp2& hb1) {
+BLS_HD BLS_CALL void fp12_mul_line2(fp12& f_in, const fp2& ga0_in, const fp2& ga1_in, const fp2& ha1_in, const fp2& gb0_in,
+                                    const fp2& gb1_in, const fp2& hb1_in) {
+  const fp2 ga0 = ga0_in;
+  const fp2 ga1 = ga1_in;
+  const fp2 ha1 = ha1_in;
+  const fp2 gb0 = gb0_in;
+  const fp2 gb1 = gb1_in;
+  const fp2 hb1 = hb1_in;
+  fp12 f = f_in;
   fp2 p00, p11, phh, sa, sb, t;
   fp6 L0;
   fp2 x, y;
@@ -378,8 +404,10 @@ BLS_HD BLS_CALL void fp12_mul_line2(fp12& f, const fp2& ga0, const fp2& ga1, con
   fp6_sub(f.c1, s, t1);
   fp6_mul_v(t1, t1);
   fp6_add(f.c0, t0, t1);
+  f_in = f;
 }
-BLS_HD BLS_CALL void fp12_frobenius(fp12& r, const fp12& a, int j) {
+BLS_HD BLS_CALL void fp12_frobenius(fp12& r, const fp12& a_in, int j) {
+  const fp12 a = a_in;
   // coefficient of w^k (k = 2i + h for a.c_h.c_i) is conj^j(c) * gamma_{j,k}
   const fp2* g = j == 1 ? FROB1 : (j == 2 ? FROB2 : FROB3);
   const fp2* src[6] = {&a.c0.c0, &a.c1.c0, &a.c0.c1, &a.c1.c1, &a.c0.c2, &a.c1.c2};

@@ -293,6 +293,92 @@ def gen_mul(e64_select=True):
 gen_mul32 = gen_mul  # name used by tools/gen_probe_bodies.py
 
 
+# ---------------------------------------------------------------- modular add / sub / neg
+# One asm block each, operands allocated by the compiler (positional: outputs r = %0-%11, t = %12-%23,
+# m = %24; inputs a = %25-%36, then b = %37-%48 and p = %49-%60, or p = %37-%48 for neg).  One VCC carry chain
+# per block: compiled C++ interleaves the chains of independent adds on VCC and an SGPR pair, which costs an
+# s_nop per step (VALU-written carry read back two instructions later), and selects with the VOP2
+# v_cndmask_b32_e32 (~19 cycles on gfx950).  Here the borrow becomes a lane mask m = -borrow in a VGPR
+# (v_subb_co_u32_e64 m, vcc, 0, 0, vcc) and the select is v_bfi_b32 / v_and_b32.  p must sit in VGPRs: a
+# carry-in VCC plus a literal or SGPR operand exceeds the gfx9 constant-bus limit of one.
+def gen_add():
+    """r = a + b mod p for a, b < p: s = a + b, d = s - p, keep s when d borrows."""
+    w = []
+    w.append("v_add_co_u32_e32 %0, vcc, %25, %37")
+    for i in range(1, 12):
+        w.append("v_addc_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (i, 25 + i, 37 + i))
+    w.append("v_sub_co_u32_e32 %12, vcc, %0, %49")
+    for i in range(1, 12):
+        w.append("v_subb_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (12 + i, i, 49 + i))
+    w.append("v_subb_co_u32_e64 %24, vcc, 0, 0, vcc")
+    for i in range(12):
+        w.append("v_bfi_b32 %%%d, %%24, %%%d, %%%d" % (i, i, 12 + i))
+    return w
+
+
+def gen_sub(neg=False):
+    """r = a - b mod p (neg: r = 0 - a): d = a - b, then d + (p & -borrow)."""
+    pb = 37 if neg else 49
+    w = []
+    if neg:
+        w.append("v_sub_co_u32_e32 %0, vcc, 0, %25")
+        for i in range(1, 12):
+            w.append("v_subb_co_u32_e32 %%%d, vcc, 0, %%%d, vcc" % (i, 25 + i))
+    else:
+        w.append("v_sub_co_u32_e32 %0, vcc, %25, %37")
+        for i in range(1, 12):
+            w.append("v_subb_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (i, 25 + i, 37 + i))
+    w.append("v_subb_co_u32_e64 %24, vcc, 0, 0, vcc")
+    for i in range(12):
+        w.append("v_and_b32_e32 %%%d, %%24, %%%d" % (12 + i, pb + i))
+    w.append("v_add_co_u32_e32 %0, vcc, %0, %12")
+    for i in range(1, 12):
+        w.append("v_addc_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (i, i, 12 + i))
+    return w
+
+
+def emulate_positional(body, outs, ins):
+    """Interprets an add/sub/neg block: ins = list of input values by operand number (25..)."""
+    reg = {}
+    for k, v in ins.items():
+        reg[k] = v
+    s = {"vcc": 0}
+    M32 = 0xFFFFFFFF
+
+    def rd(x):
+        x = x.strip()
+        if x == "vcc":
+            return s["vcc"]
+        if x.startswith("%"):
+            return reg[int(x[1:])]
+        return int(x, 0)
+
+    for ins_ in body:
+        op, rest = ins_.split(" ", 1)
+        o = [t.strip() for t in rest.split(",")]
+        d = int(o[0][1:])
+        if op == "v_add_co_u32_e32":
+            r = rd(o[2]) + rd(o[3])
+            reg[d], s["vcc"] = r & M32, r >> 32
+        elif op == "v_addc_co_u32_e32":
+            r = rd(o[2]) + rd(o[3]) + rd(o[4])
+            reg[d], s["vcc"] = r & M32, r >> 32
+        elif op == "v_sub_co_u32_e32":
+            r = rd(o[2]) - rd(o[3])
+            reg[d], s["vcc"] = r & M32, 1 if r < 0 else 0
+        elif op in ("v_subb_co_u32_e32", "v_subb_co_u32_e64"):
+            r = rd(o[2]) - rd(o[3]) - rd(o[4])
+            reg[d], s["vcc"] = r & M32, 1 if r < 0 else 0
+        elif op == "v_bfi_b32":
+            m = rd(o[1])
+            reg[d] = (m & rd(o[2])) | (~m & M32 & rd(o[3]))
+        elif op == "v_and_b32_e32":
+            reg[d] = rd(o[1]) & rd(o[2])
+        else:
+            raise ValueError(ins_)
+    return [reg[k] for k in outs]
+
+
 # ---------------------------------------------------------------- CPU interpreter
 def emulate(body, a, b):
     """Interprets the instruction subset used above (one lane); a, b: 12 x 32-bit limbs.
@@ -413,7 +499,7 @@ def body_text(square=False, chains=2, sched=True, pool=("vcc",)):
     return [x.text for x in order], cyc
 
 
-def emit_header(path, bodies):
+def emit_header(path, bodies, extra=()):
     lines = ["// GENERATED by charon_amd/tools/gen_fp_asm.py -- do not edit.",
              "// gfx950 Montgomery product r = a*b/2^384 mod p (canonical), product scanning, %d instructions."
              % len(bodies[0][1]),
@@ -427,6 +513,14 @@ def emit_header(path, bodies):
         lines.append("")
     clob = ", ".join('"v%d"' % r for r in range(24, 40)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
     lines.append("#define BLS_FP_MUL_ASM_CLOBBERS %s" % clob)
+    for name, body in extra:
+        lines.append("")
+        lines.append("// %s: %d instructions, positional operands (see tools/gen_fp_asm.py)" % (name, len(body)))
+        lines.append("#define %s \\" % name)
+        for k, ins in enumerate(body):
+            sep = "\\n\\t" if k + 1 < len(body) else ""
+            lines.append('  "%s%s" \\' % (ins, sep))
+        lines.append("")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
 
@@ -435,7 +529,8 @@ def main():
     mul = gen_mul()
     check(mul, mont=1 << 384, canonical=True)
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "fp_asm_gfx950.h")
-    emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul)])
+    emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul)],
+                extra=[("BLS_FP_ADD_ASM", gen_add()), ("BLS_FP_SUB_ASM", gen_sub()), ("BLS_FP_NEG_ASM", gen_sub(neg=True))])
     print("wrote %s: %d instructions" % (path, len(mul)))
 
 

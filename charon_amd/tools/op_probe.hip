@@ -1,0 +1,88 @@
+// Microbenchmark: cycles per tower / curve operation at one wave per SIMD (the C2 regime), against the
+// cost of the Fp products each one performs (profiles/r02_op_probe.txt).  Each lane runs a dependent chain of
+// one operation; s_memtime around the loop; median over waves.  Shows how much of an operation's time is
+// products and how much is operand traffic (scratch/flat loads), adds and selects.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "../csrc/pairing.h"
+
+using namespace bls;
+
+template <int K>
+__global__ void __launch_bounds__(64) k_op(const uint32_t* in, uint32_t* out, uint64_t* cyc, int iters) {
+  const int lane = threadIdx.x;
+  fp12 f;
+  uint32_t* fw = &f.c0.c0.c0.v[0];
+  for (int w = 0; w < 144; ++w) fw[w] = in[(lane * 144 + w) % 4096] & 0x0fffffffu;
+  fp2 g0 = f.c0.c0, g1 = f.c0.c1, h1 = f.c0.c2;
+  g2j T;
+  T.x = f.c1.c0;
+  T.y = f.c1.c1;
+  T.z = f.c1.c2;
+  g1a P;
+  P.x = f.c0.c0.c0;
+  P.y = f.c0.c0.c1;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    if (K == 0) fp_mul(f.c0.c0.c0, f.c0.c0.c0, f.c0.c0.c1);
+    if (K == 1) fp_add(f.c0.c0.c0, f.c0.c0.c0, f.c0.c0.c1);
+    if (K == 2) fp2_mul(f.c0.c0, f.c0.c0, f.c0.c1);
+    if (K == 3) fp6_mul(f.c0, f.c0, f.c1);
+    if (K == 4) fp12_sqr(f, f);
+    if (K == 5) fp12_mul(f, f, f);
+    if (K == 6) fp12_mul_line2(f, g0, g1, h1, g1, h1, g0);
+    if (K == 7) fp12_cyclotomic_sqr(f, f);
+    if (K == 8) miller_dbl_step(T, g0, g1, h1, P.x, P.y);
+    if (K == 9) jac_dbl(T, T);
+    if (K == 10) fp_sub(f.c0.c0.c0, f.c0.c0.c0, f.c0.c0.c1);
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  uint32_t acc = 0;
+  for (int w = 0; w < 144; ++w) acc ^= fw[w];
+  acc ^= g0.c0.v[0] ^ T.x.c0.v[1] ^ T.z.c1.v[2];
+  out[blockIdx.x * 64 + lane] = acc;
+  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+static double median(uint64_t* h, int n) {
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && h[j - 1] > h[j]; --j) {
+      const uint64_t t = h[j];
+      h[j] = h[j - 1];
+      h[j - 1] = t;
+    }
+  return (double)h[n / 2];
+}
+
+int main() {
+  const char* names[11] = {"fp_mul", "fp_add", "fp2_mul", "fp6_mul", "fp12_sqr", "fp12_mul", "fp12_mul_line2",
+                           "fp12_cyclotomic_sqr", "miller_dbl_step", "jac_dbl<fp2>", "fp_sub"};
+  const int products[11] = {1, 0, 3, 18, 36, 54, 69, 18, 32, 16, 0};
+  const int iters[11] = {400, 400, 200, 40, 20, 20, 20, 40, 40, 40, 400};
+  uint32_t *d_in, *d_out;
+  uint64_t* d_cyc;
+  uint32_t h_in[4096];
+  for (int i = 0; i < 4096; ++i) h_in[i] = 0x9E3779B9u * (i + 7);
+  if (hipMalloc(&d_in, sizeof(h_in)) || hipMalloc(&d_out, 1024 * 64 * 4) || hipMalloc(&d_cyc, 1024 * 8)) return 1;
+  (void)hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice);
+  uint64_t h_cyc[1024];
+  double per_product = 0;
+  for (int k = 0; k < 11; ++k) {
+    for (int rep = 0; rep < 2; ++rep) {
+      switch (k) {
+#define L(K) case K: hipLaunchKernelGGL(k_op<K>, dim3(1024), dim3(64), 0, 0, d_in, d_out, d_cyc, iters[K]); break;
+        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10)
+      }
+      if (hipDeviceSynchronize() != hipSuccess) return 2;
+    }
+    (void)hipMemcpy(h_cyc, d_cyc, sizeof(h_cyc), hipMemcpyDeviceToHost);
+    const double c = median(h_cyc, 1024) / iters[k];
+    if (k == 0) per_product = c;
+    printf("%-22s %9.0f cycles/op  products %3d  = %5.2f products-worth  (overhead %5.1f %%)\n", names[k], c,
+           products[k], c / per_product, products[k] ? 100.0 * (c / per_product - products[k]) / (c / per_product) : 100.0);
+  }
+  return 0;
+}

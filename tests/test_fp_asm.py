@@ -26,8 +26,7 @@ def _val(limbs):
 
 
 def _header_body():
-    text = open(os.path.join(ROOT, "charon_amd", "csrc", "fp_asm_gfx950.h")).read()
-    return [s.replace("\\n\\t", "") for s in re.findall(r'^\s+"([^"]*)"', text, re.M)]
+    return _macro_body("BLS_FP_MUL_ASM_BODY")
 
 
 def _cases(n, seed):
@@ -56,3 +55,33 @@ def test_radix29_experiment_is_montgomery(chains, square):
     docstring and profiles/r02_prod_probe.txt): scheduled stream == a*b/2^406 mod p, < 2p, for any 384-bit input."""
     body, _ = g.body_text(square=square, chains=chains, pool=("s[40:41]", "s[42:43]"))
     g.check(body, square=square, trials=120, seed=chains)
+
+
+def _macro_body(name):
+    text = open(os.path.join(ROOT, "charon_amd", "csrc", "fp_asm_gfx950.h")).read()
+    block = text.split("#define %s \\" % name, 1)[1].split("\n\n", 1)[0]
+    return [s.replace("\\n\\t", "") for s in re.findall(r'^\s+"([^"]*)"', block, re.M)]
+
+
+@pytest.mark.parametrize("kind", ["add", "sub", "neg"])
+def test_modular_add_sub_neg_blocks(kind):
+    """The device fp_add / fp_sub / fp_neg asm blocks (field.h): emitted text == generator, and the interpreted
+    stream equals (a +- b) mod p / -a mod p on canonical operands, edge values included."""
+    name = {"add": "BLS_FP_ADD_ASM", "sub": "BLS_FP_SUB_ASM", "neg": "BLS_FP_NEG_ASM"}[kind]
+    body = _macro_body(name)
+    assert body == {"add": g.gen_add(), "sub": g.gen_sub(), "neg": g.gen_sub(neg=True)}[kind]
+    cases = _cases(150, 21)
+    rnd = random.Random(22)
+    pl = _limbs(g.P)
+    for a in cases:
+        b = rnd.choice(cases)
+        ins = {25 + i: v for i, v in enumerate(_limbs(a))}
+        if kind == "neg":
+            ins.update({37 + i: v for i, v in enumerate(pl)})
+            want = (-a) % g.P
+        else:
+            ins.update({37 + i: v for i, v in enumerate(_limbs(b))})
+            ins.update({49 + i: v for i, v in enumerate(pl)})
+            want = (a + b) % g.P if kind == "add" else (a - b) % g.P
+        got = _val(g.emulate_positional(body, list(range(12)), ins))
+        assert got == want, (kind, hex(a), hex(b))
