@@ -151,6 +151,21 @@ BLS_HD BLS_INLINE void fp_sub(fp& r, const fp& a, const fp& b) {
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
+// Product operands only (see gen_fp_asm.py gen_add_lazy / gen_sub_lazy): a + b and a + (p - b) left unreduced in
+// [0, 2p).  The Montgomery product reduces any operands with a*b < p*2^384 to a canonical result.
+BLS_HD BLS_INLINE void fp_add_lazy(fp& r, const fp& a, const fp& b) {
+  uint32_t o[12];
+  asm volatile(BLS_FP_ADD_LAZY_ASM : BLS_FP12_OUT(o) : BLS_FP12_IN(a.v), BLS_FP12_IN(b.v) : "vcc");
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = o[i];
+}
+BLS_HD BLS_INLINE void fp_sub_lazy(fp& r, const fp& a, const fp& b) {
+  uint32_t o[12], t[12];
+  asm volatile(BLS_FP_SUB_LAZY_ASM : BLS_FP12_OUT(o), BLS_FP12_OUT(t)
+               : BLS_FP12_IN(a.v), BLS_FP12_IN(b.v), BLS_FP12_IN(P_LIMBS) : "vcc");
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = o[i];
+}
 BLS_HD BLS_INLINE void fp_neg(fp& r, const fp& a) {
   uint32_t o[12], t[12], m;
   asm volatile(BLS_FP_NEG_ASM : BLS_FP12_OUT(o), BLS_FP12_OUT(t), "=&v"(m) : BLS_FP12_IN(a.v), BLS_FP12_IN(P_LIMBS)
@@ -164,7 +179,26 @@ BLS_HD BLS_INLINE void fp_neg(fp& r, const fp& a) {
   fp_set_zero(z);
   fp_sub(r, z, a);
 }
+// host builds keep every value canonical
+BLS_HD BLS_INLINE void fp_add_lazy(fp& r, const fp& a, const fp& b) { fp_add(r, a, b); }
+BLS_HD BLS_INLINE void fp_sub_lazy(fp& r, const fp& a, const fp& b) { fp_sub(r, a, b); }
 #endif
+
+// r = a / 2 mod p (Montgomery form is preserved: (aR)/2 = (a/2)R): a + p when a is odd, then one right shift.
+BLS_HD BLS_INLINE void fp_half(fp& r, const fp& a) {
+  const uint32_t m = 0u - (a.v[0] & 1u);
+  uint32_t t[12];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)a.v[i] + (P_LIMBS[i] & m);
+    t[i] = (uint32_t)c;
+    c >>= 32;
+  }
+#pragma unroll
+  for (int i = 0; i < 11; ++i) r.v[i] = (t[i] >> 1) | (t[i + 1] << 31);
+  r.v[11] = t[11] >> 1;
+}
 
 BLS_HD BLS_INLINE void fp_dbl(fp& r, const fp& a) { fp_add(r, a, a); }
 

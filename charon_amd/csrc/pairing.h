@@ -30,14 +30,14 @@ BLS_HD BLS_CALL void miller_dbl_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const
   // Homogeneous coordinates (x = X/Z, y = Y/Z).  Note: T.z here is the projective Z, not Jacobian.
   fp2 A, B, C, E, F, G, H, J, t;
   fp2_mul(A, T.x, T.y);
-  fp2_mul_fp(A, A, FP_HALF);  // A = XY/2
+  fp2_half(A, A);             // A = XY/2
   fp2_sqr(B, T.y);
   fp2_sqr(C, T.z);
-  fp2_mul(E, C, FP2_B2_3);    // E = 3b' Z^2
+  fp2_mul_3b2(E, C);          // E = 3b' Z^2 (additions, not a product)
   fp2_add(F, E, E);
   fp2_add(F, F, E);           // F = 3E
   fp2_add(G, B, F);
-  fp2_mul_fp(G, G, FP_HALF);  // G = (B+F)/2
+  fp2_half(G, G);             // G = (B+F)/2
   fp2_add(H, T.y, T.z);
   fp2_sqr(H, H);
   fp2_sub(H, H, B);
@@ -152,7 +152,9 @@ BLS_HD BLS_CALL void fp12_cyc_exp_xabs(fp12& r, const fp12& a_in) {
   const fp12 a = a_in;
   fp12 acc = a;
   for (int bit = 62; bit >= 0; --bit) {
-    fp12_cyclotomic_sqr(acc, acc);
+    fp12 t;
+    fp12_cyclotomic_sqr_body(t, acc);  // inlined: acc stays in registers between squarings
+    acc = t;
     if ((X_ABS >> bit) & 1ull) fp12_mul(acc, acc, a);
   }
   r = acc;

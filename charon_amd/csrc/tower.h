@@ -52,6 +52,19 @@ BLS_HD BLS_INLINE void fp2_mul_xi(fp2& r, const fp2& a) {
   fp_add(r.c1, a.c0, a.c1);
   r.c0 = t;
 }
+BLS_HD BLS_INLINE void fp2_half(fp2& r, const fp2& a) {
+  fp_half(r.c0, a.c0);
+  fp_half(r.c1, a.c1);
+}
+// r = a * 3b' = a * 12 (1 + u) (the twist's 3b, b' = 4(1 + u)): additions only
+BLS_HD BLS_INLINE void fp2_mul_3b2(fp2& r, const fp2& a) {
+  fp2 t, t4;
+  fp2_mul_xi(t, a);
+  fp2_add(t, t, t);    // 2 xi a
+  fp2_add(t4, t, t);   // 4 xi a
+  fp2_add(t, t4, t4);  // 8 xi a
+  fp2_add(r, t, t4);   // 12 xi a
+}
 BLS_HD BLS_INLINE void fp2_mul_small(fp2& r, const fp2& a, uint32_t k) {
   fp_mul_small(r.c0, a.c0, k);
   fp_mul_small(r.c1, a.c1, k);
@@ -118,22 +131,22 @@ BLS_HD BLS_INLINE void fp12_conj(fp12& r, const fp12& a) {
 // Granger-Scott squaring for elements of the cyclotomic subgroup
 
 BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
-  // Karatsuba: 3 Fp products
+  // Karatsuba: 3 Fp products; the two sums only feed the third product, so they stay unreduced (fp_add_lazy)
   fp t0, t1, t2, s0, s1;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
-  fp_add(s0, a.c0, a.c1);
-  fp_add(s1, b.c0, b.c1);
+  fp_add_lazy(s0, a.c0, a.c1);
+  fp_add_lazy(s1, b.c0, b.c1);
   fp_mul(t2, s0, s1);
   fp_sub(r.c0, t0, t1);
   fp_sub(t2, t2, t0);
   fp_sub(r.c1, t2, t1);
 }
 BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
-  // (a0+a1)(a0-a1) + 2 a0 a1 u
+  // (a0+a1)(a0-a1) + 2 a0 a1 u; the sum and difference only feed the product: unreduced
   fp s, d, m;
-  fp_add(s, a.c0, a.c1);
-  fp_sub(d, a.c0, a.c1);
+  fp_add_lazy(s, a.c0, a.c1);
+  fp_sub_lazy(d, a.c0, a.c1);
   fp_mul(m, a.c0, a.c1);
   fp_mul(r.c0, s, d);
   fp_add(r.c1, m, m);
@@ -423,7 +436,9 @@ BLS_HD BLS_CALL void fp12_frobenius(fp12& r, const fp12& a_in, int j) {
   }
   for (int k = 0; k < 6; ++k) *dst[k] = tmp[k];
 }
-BLS_HD BLS_CALL void fp12_cyclotomic_sqr(fp12& r, const fp12& a) {
+// Body force-inlined into the exponentiation loop (pairing.h fp12_cyc_exp_xabs) so the Fp12 state stays in
+// registers across the 63 squarings instead of round-tripping through the stack at every call.
+BLS_HD BLS_INLINE void fp12_cyclotomic_sqr_body(fp12& r, const fp12& a) {
   // Granger-Scott: view a in Fp4^3 with Fp4 = Fp2[s]/(s^2 - xi), s = w^3... pairs
   // (g0,g1) := (c0.c0, c1.c1), (g2,g3) := (c1.c0, c0.c2), (g4,g5) := (c0.c1, c1.c2)
   fp2 z0 = a.c0.c0, z4 = a.c0.c1, z3 = a.c0.c2;
@@ -485,6 +500,13 @@ BLS_HD BLS_CALL void fp12_cyclotomic_sqr(fp12& r, const fp12& a) {
   r.c1.c0 = z2;
   r.c1.c1 = z1;
   r.c1.c2 = z5;
+}
+
+BLS_HD BLS_CALL void fp12_cyclotomic_sqr(fp12& r, const fp12& a_in) {
+  const fp12 a = a_in;
+  fp12 t;
+  fp12_cyclotomic_sqr_body(t, a);
+  r = t;
 }
 
 }  // namespace bls

@@ -337,6 +337,28 @@ def gen_sub(neg=False):
     return w
 
 
+def gen_add_lazy():
+    """r = a + b WITHOUT reduction (a, b < p -> r < 2p): only ever a product operand.  The product reduces any
+    operands with a*b < p*2^384, which 2p*2p satisfies (4p < 2^384).  Operands: r = %0-%11, a = %12-%23,
+    b = %24-%35."""
+    w = ["v_add_co_u32_e32 %0, vcc, %12, %24"]
+    for i in range(1, 12):
+        w.append("v_addc_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (i, 12 + i, 24 + i))
+    return w
+
+
+def gen_sub_lazy():
+    """r = a + (p - b) WITHOUT reduction (a, b < p -> 0 < r < 2p): a product operand standing for a - b.
+    Operands: r = %0-%11, t = %12-%23 (p - b), a = %24-%35, b = %36-%47, p = %48-%59."""
+    w = ["v_sub_co_u32_e32 %12, vcc, %48, %36"]
+    for i in range(1, 12):
+        w.append("v_subb_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (12 + i, 48 + i, 36 + i))
+    w.append("v_add_co_u32_e32 %0, vcc, %24, %12")
+    for i in range(1, 12):
+        w.append("v_addc_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (i, 24 + i, 12 + i))
+    return w
+
+
 def emulate_positional(body, outs, ins):
     """Interprets an add/sub/neg block: ins = list of input values by operand number (25..)."""
     reg = {}
@@ -530,7 +552,8 @@ def main():
     check(mul, mont=1 << 384, canonical=True)
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "fp_asm_gfx950.h")
     emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul)],
-                extra=[("BLS_FP_ADD_ASM", gen_add()), ("BLS_FP_SUB_ASM", gen_sub()), ("BLS_FP_NEG_ASM", gen_sub(neg=True))])
+                extra=[("BLS_FP_ADD_ASM", gen_add()), ("BLS_FP_SUB_ASM", gen_sub()), ("BLS_FP_NEG_ASM", gen_sub(neg=True)),
+                       ("BLS_FP_ADD_LAZY_ASM", gen_add_lazy()), ("BLS_FP_SUB_LAZY_ASM", gen_sub_lazy())])
     print("wrote %s: %d instructions" % (path, len(mul)))
 
 

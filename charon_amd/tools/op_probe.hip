@@ -7,7 +7,7 @@
 #include <cstdint>
 #include <cstdio>
 
-#include "../csrc/pairing.h"
+#include "../csrc/ops.h"
 
 using namespace bls;
 
@@ -38,6 +38,36 @@ __global__ void __launch_bounds__(64) k_op(const uint32_t* in, uint32_t* out, ui
     if (K == 8) miller_dbl_step(T, g0, g1, h1, P.x, P.y);
     if (K == 9) jac_dbl(T, T);
     if (K == 10) fp_sub(f.c0.c0.c0, f.c0.c0.c0, f.c0.c0.c1);
+    if (K == 11) final_exponentiation(f, f);
+    if (K == 12) fp12_cyc_exp_xabs(f, f);
+    if (K == 13) {
+      g1a Ps[2];
+      g2a Qs[2];
+      bool skip[2] = {false, false};
+      Ps[0] = P;
+      Ps[1] = P;
+      Qs[0].x = T.x;
+      Qs[0].y = T.y;
+      Qs[1].x = T.y;
+      Qs[1].y = T.x;
+      miller_loop_n(f, Ps, Qs, skip, 2);
+    }
+    if (K == 14) {
+      uint8_t m[32];
+      for (int b = 0; b < 32; ++b) m[b] = (uint8_t)(f.c0.c0.c0.v[b & 7] >> (b & 24));
+      g2j hj;
+      hash_to_g2(hj, m, 32, DST_POP, 43);
+      f.c0.c0 = hj.x;
+    }
+    if (K == 15) {
+      uint8_t b[96];
+      b[0] = 0xa0;
+      for (int k = 1; k < 96; ++k) b[k] = (uint8_t)(f.c0.c0.c0.v[k % 12] >> (k & 24));
+      g2a a;
+      const int st = g2_decompress(a, b, true);
+      f.c0.c0 = a.x;
+      f.c0.c1.c0.v[0] ^= (uint32_t)st;
+    }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   uint32_t acc = 0;
@@ -58,10 +88,13 @@ static double median(uint64_t* h, int n) {
 }
 
 int main() {
-  const char* names[11] = {"fp_mul", "fp_add", "fp2_mul", "fp6_mul", "fp12_sqr", "fp12_mul", "fp12_mul_line2",
-                           "fp12_cyclotomic_sqr", "miller_dbl_step", "jac_dbl<fp2>", "fp_sub"};
-  const int products[11] = {1, 0, 3, 18, 36, 54, 69, 18, 32, 16, 0};
-  const int iters[11] = {400, 400, 200, 40, 20, 20, 20, 40, 40, 40, 400};
+  const char* names[16] = {"fp_mul", "fp_add", "fp2_mul", "fp6_mul", "fp12_sqr", "fp12_mul", "fp12_mul_line2",
+                           "fp12_cyclotomic_sqr", "miller_dbl_step", "jac_dbl<fp2>", "fp_sub",
+                           "final_exponentiation", "fp12_cyc_exp_xabs", "miller_loop_n(2)", "hash_to_g2",
+                           "g2_decompress+subgroup"};
+  // Fp products per op (host instrumented build: tests/test_work_counts.py); 0 = not a product count
+  const int products[16] = {1, 0, 3, 18, 36, 54, 69, 18, 25, 16, 0, 8150, 1404, 10700, 6645, 2203};
+  const int iters[16] = {400, 400, 200, 40, 20, 20, 20, 40, 40, 40, 400, 1, 2, 1, 2, 4};
   uint32_t *d_in, *d_out;
   uint64_t* d_cyc;
   uint32_t h_in[4096];
@@ -70,11 +103,11 @@ int main() {
   (void)hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice);
   uint64_t h_cyc[1024];
   double per_product = 0;
-  for (int k = 0; k < 11; ++k) {
+  for (int k = 0; k < 16; ++k) {
     for (int rep = 0; rep < 2; ++rep) {
       switch (k) {
 #define L(K) case K: hipLaunchKernelGGL(k_op<K>, dim3(1024), dim3(64), 0, 0, d_in, d_out, d_cyc, iters[K]); break;
-        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10)
+        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15)
       }
       if (hipDeviceSynchronize() != hipSuccess) return 2;
     }

@@ -85,3 +85,32 @@ def test_modular_add_sub_neg_blocks(kind):
             want = (a + b) % g.P if kind == "add" else (a - b) % g.P
         got = _val(g.emulate_positional(body, list(range(12)), ins))
         assert got == want, (kind, hex(a), hex(b))
+
+
+@pytest.mark.parametrize("kind", ["add_lazy", "sub_lazy"])
+def test_lazy_add_sub_blocks(kind):
+    """Unreduced product operands: a + b and a + (p - b), both in [0, 2p) for canonical a, b; and the product
+    routine maps such operands (a*b < p*2^384) to the canonical Montgomery product."""
+    name = {"add_lazy": "BLS_FP_ADD_LAZY_ASM", "sub_lazy": "BLS_FP_SUB_LAZY_ASM"}[kind]
+    body = _macro_body(name)
+    assert body == (g.gen_add_lazy() if kind == "add_lazy" else g.gen_sub_lazy())
+    mul = _header_body()
+    cases = _cases(120, 31)
+    rnd = random.Random(32)
+    pl = _limbs(g.P)
+    for a in cases:
+        b = rnd.choice(cases)
+        if kind == "add_lazy":
+            ins = {12 + i: v for i, v in enumerate(_limbs(a))}
+            ins.update({24 + i: v for i, v in enumerate(_limbs(b))})
+            want = a + b
+        else:
+            ins = {24 + i: v for i, v in enumerate(_limbs(a))}
+            ins.update({36 + i: v for i, v in enumerate(_limbs(b))})
+            ins.update({48 + i: v for i, v in enumerate(pl)})
+            want = a + g.P - b
+        got = _val(g.emulate_positional(body, list(range(12)), ins))
+        assert got == want and got < 2 * g.P
+        c = rnd.choice(cases)
+        for x, y in ((got, got), (got, c), (c, got)):
+            assert _val(g.emulate(mul, _limbs(x), _limbs(y))) == x * y * R_INV % g.P
