@@ -431,11 +431,12 @@ def main():
             fb = ctypes.c_uint64()
             lib.hipbls_rlc_stats(ctypes.byref(w), ctypes.byref(wf), ctypes.byref(fb))
             kms = {}
-            for k in ("rlc_items", "rlc_hash", "rlc_window", "rlc_fallback"):
+            for k in ("rlc_items", "rlc_hash", "rlc_window", "rlc_window_lg2", "rlc_fallback", "rlc_fallback_lg2"):
                 a = ctypes.c_double()
                 c = ctypes.c_uint64()
                 lib.hipbls_kernel_timing(k.encode(), ctypes.byref(a), ctypes.byref(c))
-                kms[k] = round(a.value, 3)
+                if c.value:  # lane-pair (_lg2) or one-lane kernels, whichever HIPBLS_PAIR_AUTO picked
+                    kms[k] = round(a.value, 3)
             tt = torch.tensor([tel], dtype=torch.float64, device=dev)
             if world > 1:
                 dist.all_reduce(tt, op=dist.ReduceOp.MAX)

@@ -81,6 +81,7 @@ struct Context {
   DevBuf b_pk, b_msg, b_off, b_sig, b_st, b_out, b_ids, b_pts, b_pst, b_aux, b_part, b_bad;
   DevBuf r_pk, r_sig, r_h, r_win, r_midx, r_list, r_cnt, r_slot, r_mlist;  // RLC BatchVerify workspaces
   DevBuf t_code, t_tab, b_kidx;                                            // resident pubshare table + key indices
+  DevBuf v_ws;                                                             // lane-pair Verify points (SoA)
   uint64_t t_size = 0;
   // RLC sub-batches in flight.  The process gets GPU_MAX_HW_QUEUES = 4 hardware queues, shared by the caller's
   // stream (which also hashes the messages), the library stream and these; a kernel trace
@@ -207,12 +208,46 @@ int timed(const char* name, hipStream_t s, Launch launch) {
   return HIPBLS_OK;
 }
 
+// Pairing-check layout (hipbls_set_pair_mode): one lane per check (the fused kernels), or a lane pair per check
+// (lg2.h: the two Miller loops side by side, split final exponentiation).  A pair halves a check's latency but
+// uses two lanes, so it wins while the batch leaves lanes idle: one wave per SIMD is 64 x 1024 lanes on MI355X.
+int initial_pair_mode() {
+  const char* pm = getenv("HIPBLS_PAIR_MODE");
+  if (pm && pm[0] >= '0' && pm[0] <= '2' && pm[1] == 0) return pm[0] - '0';
+  return HIPBLS_PAIR_AUTO;
+}
+std::atomic<int> g_pair_mode{initial_pair_mode()};
+// Crossovers measured on MI355X (profiles/r02_pair_sweep.txt): lane pairs win up to 32,768 Verify items (742k vs
+// 634k verifies/s there) and lose from 49,152 (731k vs 919k).
+constexpr uint64_t kLg2MaxVerify = 32768;    // auto: Verify batches up to this many items take lane pairs
+constexpr uint64_t kLg2MaxWindows = 32768;   // auto: RLC sub-batches up to this many windows take lane pairs
+
+bool use_pairs(uint64_t units, uint64_t auto_max) {
+  const int mode = g_pair_mode.load();
+  if (mode == HIPBLS_PAIR_SINGLE) return false;
+  if (mode == HIPBLS_PAIR_LANES) return true;
+  return units <= auto_max;
+}
+
+// Verify: fused (one lane per item) or prep + lane-pair check; `ws` is the caller's SoA workspace for the latter
+// (120 words per item), so the library stream and the queue worker never share one.
 int launch_verify(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_offs, const uint8_t* d_sigs,
-                  uint64_t n, int32_t* d_status, hipStream_t s) {
+                  uint64_t n, int32_t* d_status, hipStream_t s, DevBuf& ws) {
   if (n == 0) return HIPBLS_OK;
-  return timed("verify", s, [&] {
-    hipLaunchKernelGGL(k_verify_fused, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs,
-                       n, d_status);
+  if (!use_pairs(n, kLg2MaxVerify))
+    return timed("verify", s, [&] {
+      hipLaunchKernelGGL(k_verify_fused, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs,
+                         d_sigs, n, d_status);
+    });
+  HIP_TRY(ws.ensure(n * 120 * 4));
+  int rc = timed("verify_prep", s, [&] {
+    hipLaunchKernelGGL(k_verify_prep, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs,
+                       n, (uint32_t*)ws.p, d_status);
+  });
+  if (rc) return rc;
+  return timed("verify_pair_lg2", s, [&] {
+    hipLaunchKernelGGL(k_verify_pair_lg2, dim3((unsigned)grid_for(2 * n)), dim3(kBlock), 0, s,
+                       (const uint32_t*)ws.p, n, d_status);
   });
 }
 
@@ -301,18 +336,33 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
     });
     if (rc) return rc;
     HIP_TRY(hipStreamWaitEvent(ss, c.ev_hash, 0));
-    rc = timed("rlc_window", ss, [&] {
-      hipLaunchKernelGGL(k_rlc_window, dim3((unsigned)grid_for(w1 - w0)), dim3(kBlock), 0, ss, w0, w1, n, d_midx,
-                         (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
-                         d_status, win, list + i0, cnt + k);
-    });
+    if (use_pairs(w1 - w0, kLg2MaxWindows))
+      rc = timed("rlc_window_lg2", ss, [&] {
+        hipLaunchKernelGGL(k_rlc_window_lg2, dim3((unsigned)grid_for(2 * (w1 - w0))), dim3(kBlock), 0, ss, w0, w1, n,
+                           d_midx, (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
+                           d_status, win, list + i0, cnt + k);
+      });
+    else
+      rc = timed("rlc_window", ss, [&] {
+        hipLaunchKernelGGL(k_rlc_window, dim3((unsigned)grid_for(w1 - w0)), dim3(kBlock), 0, ss, w0, w1, n, d_midx,
+                           (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
+                           d_status, win, list + i0, cnt + k);
+      });
     if (rc) return rc;
-    // the list length is only known on the device: launch for the worst case, idle lanes exit
-    rc = timed("rlc_fallback", ss, [&] {
-      hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(i1 - i0)), dim3(kBlock), 0, ss,
-                         (const uint32_t*)(list + i0), (const uint32_t*)(cnt + k), i1 - i0, d_pks, d_sigs, d_midx,
-                         (const uint32_t*)d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
-    });
+    // The list length is only known on the device: launch for the worst case, idle lanes exit.  The list is short
+    // (failed windows only) and latency-bound, so lane pairs unless the caller forced single lanes.
+    if (g_pair_mode.load() != HIPBLS_PAIR_SINGLE)
+      rc = timed("rlc_fallback_lg2", ss, [&] {
+        hipLaunchKernelGGL(k_rlc_fallback_lg2, dim3((unsigned)grid_for(2 * (i1 - i0))), dim3(kBlock), 0, ss,
+                           (const uint32_t*)(list + i0), (const uint32_t*)(cnt + k), i1 - i0, d_pks, d_sigs, d_midx,
+                           (const uint32_t*)d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
+      });
+    else
+      rc = timed("rlc_fallback", ss, [&] {
+        hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(i1 - i0)), dim3(kBlock), 0, ss,
+                           (const uint32_t*)(list + i0), (const uint32_t*)(cnt + k), i1 - i0, d_pks, d_sigs, d_midx,
+                           (const uint32_t*)d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
+      });
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c.ev_join[k], ss));
     HIP_TRY(hipStreamWaitEvent(s, c.ev_join[k], 0));
@@ -425,7 +475,7 @@ struct VerifyQueue {
   uint32_t gather_us = 200;
   uint64_t batches = 0, items = 0;
   hipStream_t stream = nullptr;
-  DevBuf d_pk, d_sig, d_msg, d_off, d_st;
+  DevBuf d_pk, d_sig, d_msg, d_off, d_st, d_ws;
 };
 VerifyQueue g_q;
 
@@ -443,7 +493,7 @@ int run_batch(VBatch& b) {
   if (b.msg.size()) HIP_TRY(hipMemcpyAsync(q.d_msg.p, b.msg.data(), b.msg.size(), hipMemcpyHostToDevice, q.stream));
   HIP_TRY(hipMemcpyAsync(q.d_off.p, b.off.data(), (n + 1) * 8, hipMemcpyHostToDevice, q.stream));
   int rc = launch_verify((const uint8_t*)q.d_pk.p, (const uint8_t*)q.d_msg.p, (const uint64_t*)q.d_off.p,
-                         (const uint8_t*)q.d_sig.p, n, (int32_t*)q.d_st.p, q.stream);
+                         (const uint8_t*)q.d_sig.p, n, (int32_t*)q.d_st.p, q.stream, q.d_ws);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(b.status.data(), q.d_st.p, n * 4, hipMemcpyDeviceToHost, q.stream));
   HIP_TRY(hipStreamSynchronize(q.stream));
@@ -661,6 +711,12 @@ int hipbls_set_timing(int enabled) {
   return HIPBLS_OK;
 }
 
+int hipbls_set_pair_mode(int mode) {
+  if (mode != HIPBLS_PAIR_AUTO && mode != HIPBLS_PAIR_SINGLE && mode != HIPBLS_PAIR_LANES)
+    return arg_err("unknown pair mode");
+  return g_pair_mode.exchange(mode);
+}
+
 int hipbls_verify_batch(const uint8_t* pks, const uint8_t* msgs, const uint64_t* msg_offsets, const uint8_t* sigs,
                         uint64_t n, int32_t* status) {
   if (n == 0) return HIPBLS_OK;
@@ -679,8 +735,12 @@ int hipbls_verify_batch(const uint8_t* pks, const uint8_t* msgs, const uint64_t*
   HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
   if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
   HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  int rc = launch_verify((const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p,
-                         (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p, c.stream);
+  int rc = ws_begin(c.stream);
+  if (rc) return rc;
+  rc = launch_verify((const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p,
+                     (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p, c.stream, c.v_ws);
+  if (rc) return rc;
+  rc = ws_end(c.stream);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
   HIP_TRY(hipStreamSynchronize(c.stream));
@@ -690,7 +750,12 @@ int hipbls_verify_batch(const uint8_t* pks, const uint8_t* msgs, const uint64_t*
 int hipbls_verify_batch_device(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
                                const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream) {
   ENTER();
-  return launch_verify(d_pks, d_msgs, d_msg_offsets, d_sigs, n, d_status, pick(stream));
+  const hipStream_t s = pick(stream);
+  int rc = ws_begin(s);
+  if (rc) return rc;
+  rc = launch_verify(d_pks, d_msgs, d_msg_offsets, d_sigs, n, d_status, s, g_ctx.v_ws);
+  if (rc) return rc;
+  return ws_end(s);
 }
 
 int hipbls_verify(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, const uint8_t* sig96, int32_t* status) {
@@ -742,8 +807,12 @@ int hipbls_verify_signed_data_batch(const uint8_t* pks, const uint8_t* object_ro
   hipLaunchKernelGGL(k_signing_roots, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_aux.p,
                      (const uint8_t*)c.b_aux.p + n * 32, n, (uint8_t*)c.b_msg.p, (uint64_t*)c.b_off.p);
   HIP_TRY(hipGetLastError());
-  int rc = launch_verify((const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p,
-                         (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p, c.stream);
+  int rc = ws_begin(c.stream);
+  if (rc) return rc;
+  rc = launch_verify((const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p,
+                     (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p, c.stream, c.v_ws);
+  if (rc) return rc;
+  rc = ws_end(c.stream);
   if (rc) return rc;
   hipLaunchKernelGGL(k_zero_sig_status, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream,
                      (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p);

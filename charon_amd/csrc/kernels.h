@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "lg2.h"
 #include "ops.h"
 #include "rlc.h"
 
@@ -22,6 +23,64 @@ __global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restri
   if (i >= n) return;
   const uint64_t o0 = offs[i], o1 = offs[i + 1];
   status[i] = op_verify(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i);
+}
+
+// ---------------------------------------------------------------- lane-pair Verify (lg2.h)
+// Stage 1, one lane per item: decode + subgroup-check pk and sig, hash the message; the points go to SoA
+// (pk 24 words, H(m) 48, sig 48 per item: `ws` holds 120 words x n) and the status is final or RLC_PENDING.
+// Status order is op_verify's.
+__global__ void __launch_bounds__(kBlock) k_verify_prep(const uint8_t* __restrict__ pks,
+                                                        const uint8_t* __restrict__ msgs,
+                                                        const uint64_t* __restrict__ offs,
+                                                        const uint8_t* __restrict__ sigs, uint64_t n,
+                                                        uint32_t* __restrict__ ws, int32_t* __restrict__ status) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a pk;
+  g2a sig;
+  int st = RLC_PENDING;
+  const int dp = g1_decompress(pk, pks + 48 * i, true);
+  if (dp == DEC_BAD) {
+    st = HIPBLS_ERR_PUBKEY;
+  } else {
+    const int ds = g2_decompress(sig, sigs + 96 * i, true);
+    if (ds == DEC_BAD)
+      st = HIPBLS_ERR_SIGNATURE;
+    else if (dp == DEC_INF || ds == DEC_INF)
+      st = HIPBLS_ERR_VERIFY;  // KeyValidate / e(pk,H) != 1
+  }
+  if (st == RLC_PENDING) {
+    const uint64_t o0 = offs[i], o1 = offs[i + 1];
+    g2j hj;
+    hash_to_g2(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43);
+    g2a hm;
+    jac_to_aff(hm, hj);
+    soa_store<24>(ws, n, i, &pk.x.v[0]);
+    soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);
+    soa_store<48>(ws + 72 * n, n, i, &sig.x.c0.v[0]);
+  }
+  status[i] = st;
+}
+
+// Stage 2, lanes 2i and 2i+1 per item: e(pk, H(m)) * e(-g1, sig) == 1 with the two Miller loops side by side
+// and the final exponentiation split across the pair.
+__global__ void __launch_bounds__(kBlock) k_verify_pair_lg2(const uint32_t* __restrict__ ws, uint64_t n,
+                                                            int32_t* __restrict__ status) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t i = t >> 1;
+  const uint32_t m = (t & 1) ? ~0u : 0u;
+  if (i >= n || status[i] != RLC_PENDING) return;  // same decision on both lanes of the pair
+  const bool ok = pairing_check_lg2<1>(2, m, [&](int k, g1a& P, g2a& Q) {
+    if (k == 0) {
+      soa_load<24>(&P.x.v[0], ws, n, i);
+      soa_load<48>(&Q.x.c0.v[0], ws + 24 * n, n, i);
+    } else {
+      P.x = G1_GEN_X;
+      P.y = G1_NEG_GEN_Y;
+      soa_load<48>(&Q.x.c0.v[0], ws + 72 * n, n, i);
+    }
+  });
+  if (!m) status[i] = ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }
 
 __global__ void __launch_bounds__(kBlock) k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restrict__ msgs,
@@ -212,7 +271,10 @@ __global__ void __launch_bounds__(kFavBlock) k_fav_batch(const uint32_t* __restr
     }
     __syncthreads();
   }
-  if (tid != 0) return;
+  // lanes 0 and 1 finish as a pair (lg2.h): e(pk, H(m)) on lane 0 and e(-g1, sig) on lane 1, split final
+  // exponentiation; every branch below depends on shared values only, so the pair stays together
+  if (tid >= 2) return;
+  const uint32_t lm = tid ? ~0u : 0u;
   int st;
   if (sh_ds == DEC_BAD) {
     st = HIPBLS_ERR_SIGNATURE;
@@ -233,10 +295,20 @@ __global__ void __launch_bounds__(kFavBlock) k_fav_batch(const uint32_t* __restr
         (&sg.x.c0.v[0])[w] = sh_sig[w];
         (&hm.x.c0.v[0])[w] = sh_hm[w];
       }
-      st = pairing_check_verify(pk, hm, sg) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+      const bool ok = pairing_check_lg2<1>(2, lm, [&](int k, g1a& P, g2a& Q) {
+        if (k == 0) {
+          P = pk;
+          Q = hm;
+        } else {
+          P.x = G1_GEN_X;
+          P.y = G1_NEG_GEN_Y;
+          Q = sg;
+        }
+      });
+      st = ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
     }
   }
-  status[g] = st;
+  if (tid == 0) status[g] = st;
 }
 
 // Aggregate (tbls/herumi.go:220-242): sum of n signatures in G2.  Stage 1 decodes every signature in parallel
@@ -435,6 +507,42 @@ __global__ void __launch_bounds__(kBlock) k_rlc_window(uint64_t w0, uint64_t w1,
     if (status[i] == RLC_PENDING) list[at++] = (uint32_t)i;
 }
 
+// Stage 3 on lane pairs (lg2.h rlc_window_lg2): lanes 2v and 2v+1 share window w0 + v; the even lane records
+// the verdict.
+__global__ void __launch_bounds__(kBlock) k_rlc_window_lg2(uint64_t w0, uint64_t w1, uint64_t n,
+                                                           const uint32_t* __restrict__ msg_idx,
+                                                           const uint32_t* __restrict__ rpk,
+                                                           const uint32_t* __restrict__ rsig,
+                                                           const uint32_t* __restrict__ H, uint64_t hstride,
+                                                           const uint32_t* __restrict__ hslot,
+                                                           int32_t* __restrict__ status, int32_t* __restrict__ win_fail,
+                                                           uint32_t* __restrict__ list, uint32_t* __restrict__ list_len) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t w = w0 + (t >> 1);
+  const uint32_t m = (t & 1) ? ~0u : 0u;
+  if (w >= w1) return;
+  const uint64_t i0 = w * RLC_W;
+  const uint64_t i1 = i0 + RLC_W < n ? i0 + RLC_W : n;
+  auto load_pk = [&](g1j& q, uint64_t i) { soa_load<36>(&q.x.v[0], rpk, n, i); };
+  auto load_sig = [&](g2j& q, uint64_t i) { soa_load<72>(&q.x.c0.v[0], rsig, n, i); };
+  auto load_h = [&](g2a& q, uint32_t mi) { soa_load<48>(&q.x.c0.v[0], H, hstride, h_col(hslot, mi)); };
+  const bool ok = rlc_window_lg2(i0, i1, status, msg_idx, load_pk, load_sig, load_h, m);
+  if (m) return;
+  int left = 0;
+  for (uint64_t i = i0; i < i1; ++i)
+    if (status[i] == RLC_PENDING) {
+      if (ok)
+        status[i] = HIPBLS_OK;
+      else
+        ++left;
+    }
+  win_fail[w] = left;
+  if (left == 0) return;
+  uint32_t at = atomicAdd(list_len, (uint32_t)left);
+  for (uint64_t i = i0; i < i1; ++i)
+    if (status[i] == RLC_PENDING) list[at++] = (uint32_t)i;
+}
+
 // Stage 4: items of failed windows (dense list) are checked one by one (rlc_fallback_lane).
 __global__ void __launch_bounds__(kBlock) k_rlc_fallback(const uint32_t* __restrict__ list,
                                                          const uint32_t* __restrict__ list_len, uint64_t cap,
@@ -449,6 +557,41 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback(const uint32_t* __restr
   const uint64_t len = *list_len;
   if (j >= len || j >= cap) return;
   rlc_fallback_lane(list[j], pks, sigs, msg_idx, H, hstride, hslot, status, key_idx, T, tab);
+}
+
+// Stage 4 on lane pairs (lg2.h): the even lane decodes the key and takes e(pk, H(m)), the odd lane decodes the
+// signature and takes e(-g1, sig); the final exponentiation is split.  Same verdicts as k_rlc_fallback.
+__global__ void __launch_bounds__(kBlock) k_rlc_fallback_lg2(const uint32_t* __restrict__ list,
+                                                             const uint32_t* __restrict__ list_len, uint64_t cap,
+                                                             const uint8_t* __restrict__ pks,
+                                                             const uint8_t* __restrict__ sigs,
+                                                             const uint32_t* __restrict__ msg_idx,
+                                                             const uint32_t* __restrict__ H, uint64_t hstride,
+                                                             const uint32_t* __restrict__ hslot,
+                                                             int32_t* __restrict__ status,
+                                                             const uint32_t* __restrict__ key_idx, uint64_t T,
+                                                             const uint32_t* __restrict__ tab) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t j = t >> 1;
+  const uint32_t m = (t & 1) ? ~0u : 0u;
+  const uint64_t len = *list_len;
+  if (j >= len || j >= cap) return;
+  const uint64_t i = list[j];
+  if (status[i] != RLC_PENDING) return;
+  const bool ok = pairing_check_lg2<1>(2, m, [&](int k, g1a& P, g2a& Q) {
+    if (k == 0) {
+      if (pks)
+        g1_decompress(P, pks + 48 * i, false);
+      else
+        soa_load<24>(&P.x.v[0], tab, T, key_idx[i]);
+      soa_load<48>(&Q.x.c0.v[0], H, hstride, h_col(hslot, msg_idx[i]));
+    } else {
+      P.x = G1_GEN_X;
+      P.y = G1_NEG_GEN_Y;
+      g2_decompress(Q, sigs + 96 * i, false);
+    }
+  });
+  if (!m) status[i] = ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }
 
 // ---------------------------------------------------------------- resident pubshare table

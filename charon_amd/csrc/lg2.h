@@ -1,0 +1,340 @@
+// Two-lane groups for the pairing check (BASELINE.json north star: "one lane-group per pairing with
+// wavefront-level reductions").  Lanes 2i and 2i+1 of a wave cooperate on one pairing-product check:
+//
+//   * Miller loop: each lane runs the Miller loop of its own pairs (lane 0: e(pk, H(m)), lane 1: e(-g1, sig) for a
+//     Verify; pairs of equal parity for a multi-pairing), so the two loops run side by side instead of one after
+//     the other.  Same instruction stream on both lanes, different data (SIMT-uniform).
+//   * The two Miller values are combined into ONE Fp12 held split across the pair: the even lane owns c0, the odd
+//     lane owns c1 (Fp12 = Fp6[w]).  Halves are exchanged with DPP quad_perm [1,0,3,2] moves (one VALU instruction
+//     per dword, no LDS), which need both lanes of a pair active: every exchange sits in pair-uniform control flow.
+//   * The final exponentiation runs on the split value: each lane computes its own half of every product
+//     (Fp12 products: two Fp6 products per lane, schoolbook; cyclotomic squarings: five Fp2 squarings per lane
+//     instead of nine), so its latency is roughly halved.  The inversion of the easy part is computed redundantly
+//     on both lanes from the gathered value.
+//
+// Semantics are those of pairing_check_verify / the RLC checks (ops.h, rlc.h): the same formulas, the same e^3
+// final exponentiation, so a split check and a single-lane check accept exactly the same inputs.  Device-only
+// (DPP); parity is covered by the GPU tests against the single-lane kernels and the oracle.
+#pragma once
+#include "rlc.h"
+
+namespace bls {
+
+#if defined(__HIPCC__)
+
+// Partner lane's value (lane ^ 1).  Both lanes of the pair must be active.
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1 /* quad_perm [1,0,3,2] */, 0xF, 0xF, false);
+#else
+  return v;  // host pass of a device function: never executed
+#endif
+}
+template <int N>
+__device__ __forceinline__ void pair_swap_words(uint32_t* d, const uint32_t* s) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i] = pair_swap(s[i]);
+}
+__device__ __forceinline__ void pair_swap(fp2& d, const fp2& s) { pair_swap_words<24>(&d.c0.v[0], &s.c0.v[0]); }
+__device__ __forceinline__ void pair_swap(fp6& d, const fp6& s) { pair_swap_words<72>(&d.c0.c0.v[0], &s.c0.c0.v[0]); }
+
+// Lane-parity selects: m = ~0 on the odd lane, 0 on the even one.  Bitwise (v_bfi_b32), never a VOP2 cndmask.
+template <int N>
+__device__ __forceinline__ void sel_words(uint32_t* d, uint32_t m, const uint32_t* if_odd, const uint32_t* if_even) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i] = (m & if_odd[i]) | (~m & if_even[i]);
+}
+__device__ __forceinline__ fp2 sel(uint32_t m, const fp2& if_odd, const fp2& if_even) {
+  fp2 r;
+  sel_words<24>(&r.c0.v[0], m, &if_odd.c0.v[0], &if_even.c0.v[0]);
+  return r;
+}
+__device__ __forceinline__ fp6 sel(uint32_t m, const fp6& if_odd, const fp6& if_even) {
+  fp6 r;
+  sel_words<72>(&r.c0.c0.v[0], m, &if_odd.c0.c0.v[0], &if_even.c0.c0.v[0]);
+  return r;
+}
+
+// ---------------------------------------------------------------- split Fp12 (own half h)
+// Own half of the product of two FULL Fp12 values a, b (both known to the lane): even lane c0 = a0 b0 + v a1 b1,
+// odd lane c1 = a0 b1 + a1 b0.  Two Fp6 products per lane.
+BLS_CALL __device__ void fp12h_mul_full(fp6& r, const fp12& a_in, const fp12& b_in, uint32_t m) {
+  const fp12 a = a_in, b = b_in;
+  const fp6 y1 = sel(m, b.c1, b.c0), y2 = sel(m, b.c0, b.c1);
+  fp6 p1, p2, vp2;
+  fp6_mul(p1, a.c0, y1);
+  fp6_mul(p2, a.c1, y2);
+  fp6_mul_v(vp2, p2);
+  const fp6 q = sel(m, p2, vp2);
+  fp6_add(r, p1, q);
+}
+
+// Own half of a*b for split a, b.
+BLS_CALL __device__ void fp12h_mul(fp6& r, const fp6& ah_in, const fp6& bh_in, uint32_t m) {
+  const fp6 ah = ah_in, bh = bh_in;
+  fp6 ao, bo;
+  pair_swap(ao, ah);
+  pair_swap(bo, bh);
+  // even: (a0 b0) + v (a1 b1) with a0 = ah, a1 = ao; odd: (a0 b1) + (a1 b0) with a0 = ao, a1 = ah
+  const fp6 x1 = sel(m, ao, ah), x2 = sel(m, ah, ao);
+  fp6 p1, p2, vp2;
+  fp6_mul(p1, x1, bh);
+  fp6_mul(p2, x2, bo);
+  fp6_mul_v(vp2, p2);
+  const fp6 q = sel(m, p2, vp2);
+  fp6_add(r, p1, q);
+}
+
+// conj: c1 -> -c1 (odd lane negates)
+__device__ __forceinline__ void fp12h_conj(fp6& r, const fp6& h, uint32_t m) {
+  fp6 n;
+  fp6_neg(n, h);
+  r = sel(m, n, h);
+}
+
+// x -> x^(p^j): coefficient k = 2i + h (h = lane parity) of w^k is conj^j(c) * gamma_{j,k}
+BLS_CALL __device__ void fp12h_frobenius(fp6& r, const fp6& h_in, int j, uint32_t m) {
+  const fp6 h = h_in;
+  const fp2* g = j == 1 ? FROB1 : (j == 2 ? FROB2 : FROB3);
+  const fp2* src[3] = {&h.c0, &h.c1, &h.c2};
+  fp2 out[3];
+  for (int i = 0; i < 3; ++i) {
+    fp2 c = *src[i];
+    if (j & 1) fp2_conj(c, c);
+    const fp2 gk = sel(m, g[2 * i + 1], g[2 * i]);
+    fp2_mul(out[i], c, gk);
+  }
+  r.c0 = out[0];
+  r.c1 = out[1];
+  r.c2 = out[2];
+}
+
+// Granger-Scott cyclotomic squaring on the split value: five Fp2 squarings per lane (nine on one lane).
+// Even lane holds (z0, z4, z3) = (c0.c0, c0.c1, c0.c2), odd lane (z2, z1, z5) = (c1.c0, c1.c1, c1.c2); the Fp4 pairs
+// are (z0, z1), (z2, z3), (z4, z5).  The even lane squares pair (z0, z1) and z4, z4 + z5; the odd lane pair (z2, z3)
+// and z5.  Outputs as fp12_cyclotomic_sqr: z0' = 3 t0 - 2 z0, z1' = 3 t1 + 2 z1, z2' = 3 xi t5 + 2 z2,
+// z3' = 3 t4 - 2 z3, z4' = 3 t2 - 2 z4, z5' = 3 t3 + 2 z5.
+BLS_CALL __device__ void fp12h_cyc_sqr(fp6& r, const fp6& h_in, uint32_t m) {
+  const fp6 h = h_in;
+  fp6 o;
+  pair_swap(o, h);  // even: (z2, z1, z5); odd: (z0, z4, z3)
+  const fp2 x = h.c0;                // even z0 | odd z2
+  const fp2 y = sel(m, o.c2, o.c1);  // even z1 | odd z3
+  const fp2 w = sel(m, h.c2, h.c1);  // even z4 | odd z5
+  fp2 v, xy;
+  fp2_add(v, h.c1, o.c2);            // even z4 + z5 (odd: unused)
+  fp2_add(xy, x, y);
+  fp2 S1, S2, S3, S4, S5;
+  fp2_sqr(S1, x);
+  fp2_sqr(S2, y);
+  fp2_sqr(S3, xy);
+  fp2_sqr(S4, w);
+  fp2_sqr(S5, v);
+  fp2 te, to, t;
+  fp2_mul_xi(te, S2);
+  fp2_add(te, te, S1);  // even t0 | odd t2
+  fp2_sub(to, S3, S1);
+  fp2_sub(to, to, S2);  // even t1 | odd t3
+  fp2 S4o;
+  pair_swap(S4o, S4);   // even z5^2 | odd z4^2
+  fp2 t4, t5;
+  fp2_mul_xi(t4, S4o);
+  fp2_add(t4, t4, S4);  // even: t4 = z4^2 + xi z5^2
+  fp2_sub(t5, S5, S4);
+  fp2_sub(t5, t5, S4o);  // even: t5 = (z4 + z5)^2 - z4^2 - z5^2
+  const fp2 p1 = sel(m, te, to);  // even sends t1, odd sends t2
+  fp2 q1, q2;
+  pair_swap(q1, p1);  // even receives t2 | odd receives t1
+  pair_swap(q2, t5);  // odd receives t5
+  fp2 xq2;
+  fp2_mul_xi(xq2, q2);
+  const fp2 u0 = sel(m, xq2, te), u1 = q1, u2 = sel(m, to, t4);
+  fp6 nh;
+  fp6_neg(nh, h);
+  const fp6 zs = sel(m, h, nh);  // -z on the even lane, +z on the odd lane
+  const fp2* us[3] = {&u0, &u1, &u2};
+  const fp2* zz[3] = {&zs.c0, &zs.c1, &zs.c2};
+  fp2 out[3];
+  for (int k = 0; k < 3; ++k) {
+    fp2 a;
+    fp2_add(a, *us[k], *zz[k]);
+    fp2_dbl(a, a);
+    fp2_add(out[k], a, *us[k]);
+  }
+  r.c0 = out[0];
+  r.c1 = out[1];
+  r.c2 = out[2];
+}
+
+// Gathers the full value on both lanes.
+__device__ __forceinline__ void fp12h_gather(fp12& full, const fp6& h, uint32_t m) {
+  fp6 o;
+  pair_swap(o, h);
+  full.c0 = sel(m, o, h);
+  full.c1 = sel(m, h, o);
+}
+
+// r = a^|x| for a in the cyclotomic subgroup (split)
+BLS_CALL __device__ void fp12h_exp_xabs(fp6& r, const fp6& a_in, uint32_t m) {
+  const fp6 a = a_in;
+  fp6 acc = a;
+  for (int bit = 62; bit >= 0; --bit) {
+    fp6 t;
+    fp12h_cyc_sqr(t, acc, m);
+    acc = t;
+    if ((X_ABS >> bit) & 1ull) fp12h_mul(acc, acc, a, m);
+  }
+  r = acc;
+}
+
+// final_exponentiation (pairing.h) on a split value: same formula, split operations.
+BLS_CALL __device__ void final_exponentiation_split(fp6& r, const fp6& f_in, uint32_t m) {
+  const fp6 f = f_in;
+  fp6 t, mm, t0, t1, t2, u;
+  // easy part: f^((p^6-1)(p^2+1)); the inverse is computed on both lanes from the gathered value
+  fp12 full, inv;
+  fp12h_gather(full, f, m);
+  fp12_inv(inv, full);
+  const fp6 fi = sel(m, inv.c1, inv.c0);
+  fp12h_conj(t, f, m);
+  fp12h_mul(mm, t, fi, m);
+  fp12h_frobenius(t, mm, 2, m);
+  fp12h_mul(mm, t, mm, m);
+  // hard part
+  fp12h_exp_xabs(t0, mm, m);
+  fp12h_mul(t0, t0, mm, m);
+  fp12h_conj(t0, t0, m);
+  fp12h_exp_xabs(u, t0, m);
+  fp12h_mul(u, u, t0, m);
+  fp12h_conj(t0, u, m);
+  fp12h_exp_xabs(u, t0, m);
+  fp12h_conj(u, u, m);
+  fp12h_frobenius(t1, t0, 1, m);
+  fp12h_mul(t1, t1, u, m);
+  fp12h_exp_xabs(u, t1, m);
+  fp12h_exp_xabs(u, u, m);
+  fp12h_frobenius(t2, t1, 2, m);
+  fp12h_mul(t2, t2, u, m);
+  fp12h_conj(u, t1, m);
+  fp12h_mul(t2, t2, u, m);
+  fp12h_cyc_sqr(u, mm, m);
+  fp12h_mul(u, u, mm, m);
+  fp12h_mul(r, t2, u, m);
+}
+
+// Is the split value 1?  Even half must be (1, 0, 0), odd half 0; both lanes get the answer.
+__device__ __forceinline__ bool fp12h_is_one(const fp6& h, uint32_t m) {
+  fp6 one6;
+  fp6_set_one(one6);
+  fp6 zero6;
+  fp6_set_zero(zero6);
+  const fp6 want = sel(m, zero6, one6);
+  uint32_t acc = 0;
+  const uint32_t* a = &h.c0.c0.v[0];
+  const uint32_t* b = &want.c0.c0.v[0];
+  for (int i = 0; i < 72; ++i) acc |= a[i] ^ b[i];
+  const uint32_t mine = acc == 0 ? 1u : 0u;
+  return (mine & pair_swap(mine)) != 0;
+}
+
+// Pairing-product check over n pairs split across a lane pair: this lane takes pairs i with i % 2 == parity
+// (at most MAXN of them).  Both lanes must call it together with the same n.  Returns prod e(P_i, Q_i) == 1 on
+// both lanes.  P_i / Q_i are read through callables so the caller decides where the pairs come from.
+template <int MAXN>
+__device__ bool lg2_check_pairs(const g1a* P, const g2a* Q, int k, uint32_t m) {
+  fp12 f;
+  if (k > 0)
+    miller_loop_multi<MAXN>(f, P, Q, k);
+  else
+    fp12_set_one(f);
+  fp12 g;
+  fp12 mine = f;
+  // combine the two lanes' Miller values: own half of f_even * f_odd
+  pair_swap(g.c0, mine.c0);
+  pair_swap(g.c1, mine.c1);
+  fp12 fe, fo;
+  fe.c0 = sel(m, g.c0, mine.c0);
+  fe.c1 = sel(m, g.c1, mine.c1);
+  fo.c0 = sel(m, mine.c0, g.c0);
+  fo.c1 = sel(m, mine.c1, g.c1);
+  fp6 h, e;
+  fp12h_mul_full(h, fe, fo, m);
+  final_exponentiation_split(e, h, m);
+  return fp12h_is_one(e, m);
+}
+
+template <int MAXN, class GetPair>
+__device__ bool pairing_check_lg2(int n, uint32_t m, GetPair get_pair) {
+  const int par = m ? 1 : 0;
+  g1a P[MAXN];
+  g2a Q[MAXN];
+  int k = 0;
+  for (int i = par; i < n && k < MAXN; i += 2, ++k) get_pair(i, P[k], Q[k]);
+  return lg2_check_pairs<MAXN>(P, Q, k, m);
+}
+
+// rlc_window (rlc.h) on a lane pair: both lanes form the same runs (sums of scaled keys per message run, the sum of
+// scaled signatures), each converts to affine and Miller-loops only the pairs of its parity, then the split
+// final exponentiation.  Same verdict as rlc_window.
+template <class LoadPk, class LoadSig, class LoadH>
+__device__ bool rlc_window_lg2(uint64_t i0, uint64_t i1, const int32_t* status, const uint32_t* msg_idx,
+                               LoadPk load_pk, LoadSig load_sig, LoadH load_h, uint32_t m) {
+  constexpr int MAXN = (RLC_W + 2) / 2;
+  const int par = m ? 1 : 0;
+  g1a P[MAXN];
+  g2a Q[MAXN];
+  int np = 0, k = 0;
+  g2j S;
+  jac_set_inf(S);
+  g1j run;
+  uint32_t run_msg = 0xffffffffu;
+  bool any = false;
+  for (uint64_t i = i0; i < i1; ++i) {
+    if (status[i] != RLC_PENDING) continue;
+    any = true;
+    g1j qp;
+    g2j qs;
+    load_pk(qp, i);
+    load_sig(qs, i);
+    jac_add(S, S, qs);
+    const uint32_t mi = msg_idx[i];
+    if (mi != run_msg) {
+      if (run_msg != 0xffffffffu && !jac_is_inf(run)) {
+        if ((np & 1) == par) {
+          jac_to_aff(P[k], run);
+          load_h(Q[k], run_msg);
+          ++k;
+        }
+        ++np;
+      }
+      run = qp;
+      run_msg = mi;
+    } else {
+      jac_add(run, run, qp);
+    }
+  }
+  if (!any) return true;
+  if (!jac_is_inf(run)) {
+    if ((np & 1) == par) {
+      jac_to_aff(P[k], run);
+      load_h(Q[k], run_msg);
+      ++k;
+    }
+    ++np;
+  }
+  if (!jac_is_inf(S)) {
+    if ((np & 1) == par) {
+      P[k].x = G1_GEN_X;
+      P[k].y = G1_NEG_GEN_Y;
+      jac_to_aff(Q[k], S);
+      ++k;
+    }
+    ++np;
+  }
+  if (np == 0) return true;  // np, any: same on both lanes
+  return lg2_check_pairs<MAXN>(P, Q, k, m);
+}
+
+#endif  // __HIPCC__
+
+}  // namespace bls

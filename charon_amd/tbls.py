@@ -23,6 +23,7 @@ R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 OK, ERR_PUBKEY, ERR_SIGNATURE, ERR_VERIFY, ERR_SECRET, ERR_COMBINE, ERR_ZERO_SIG = 0, 1, 2, 3, 4, 5, 6
 INFINITY_G2 = b"\xc0" + bytes(95)  # compressed point at infinity (the empty Aggregate, herumi.go:220-242)
 ERR_ARG, ERR_DEVICE = 16, 17
+PAIR_AUTO, PAIR_SINGLE, PAIR_LANES = 0, 1, 2  # hipbls_set_pair_mode: pairing-check layout (include/hipbls.h)
 
 # tbls/herumi.go error strings by status code
 VERIFY_ERRORS = {
@@ -62,6 +63,7 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
     sig = {
         "hipbls_current_device": ([], ctypes.c_int),
         "hipbls_set_timing": ([ctypes.c_int], ctypes.c_int),
+        "hipbls_set_pair_mode": ([ctypes.c_int], ctypes.c_int),
         "hipbls_verify": ([u8p, u8p, u64, u8p, i32p], ctypes.c_int),
         "hipbls_verify_submit": ([u8p, u8p, u64, u8p, u64p], ctypes.c_int),
         "hipbls_verify_wait": ([u64, i32p], ctypes.c_int),
@@ -123,7 +125,7 @@ def exported_symbols() -> List[str]:
         "hipbls_batch_verify_rlc_keys", "hipbls_verify_batch_keys_device", "hipbls_batch_verify_rlc_keys_device",
         "hipbls_current_device", "hipbls_set_timing", "hipbls_verify", "hipbls_verify_submit", "hipbls_verify_wait",
         "hipbls_queue_config", "hipbls_queue_stats", "hipbls_verify_signed_data_batch", "hipbls_aggregate_device",
-        "hipbls_hcache_config", "hipbls_hcache_stats",
+        "hipbls_hcache_config", "hipbls_hcache_stats", "hipbls_set_pair_mode",
     ]
 
 
@@ -507,3 +509,12 @@ class HipBLS:
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         _check(self.lib.hipbls_hcache_stats(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), self.lib)
         return a.value, b.value, c.value
+
+    # ---------------------------------------------------------------- pairing-check layout
+    def set_pair_mode(self, mode: int) -> int:
+        """PAIR_AUTO / PAIR_SINGLE (one lane per check) / PAIR_LANES (a lane pair per check); returns the
+        previous mode.  Results are identical in every mode; only latency and lane use differ."""
+        rc = self.lib.hipbls_set_pair_mode(mode)
+        if rc not in (PAIR_AUTO, PAIR_SINGLE, PAIR_LANES):
+            _check(rc, self.lib)
+        return rc

@@ -58,7 +58,7 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 5
+#define HIPBLS_ABI_VERSION 6
 int hipbls_abi_version(void);
 
 /* Select the HIP device used by the calling process (one process per GPU); idempotent.
@@ -72,6 +72,14 @@ const char* hipbls_last_error(void);
 int hipbls_current_device(void);
 /* Per-kernel HIP-event timing (hipbls_kernel_timing); off by default, or HIPBLS_TIMING=1 in the environment. */
 int hipbls_set_timing(int enabled);
+/* Pairing-check layout.  HIPBLS_PAIR_SINGLE: one lane per check.  HIPBLS_PAIR_LANES: a lane pair per check (the
+ * two Miller loops side by side, the final exponentiation split across the pair; about half the latency, twice
+ * the lanes).  HIPBLS_PAIR_AUTO (default): lane pairs for batches that leave lanes idle (Verify up to 32,768
+ * items, RLC sub-batches up to 32,768 windows, every RLC fallback list and FastAggregateVerify).  Results are
+ * identical in every mode.  Returns the previous mode, or HIPBLS_ERR_ARG for an unknown one.  The environment
+ * variable HIPBLS_PAIR_MODE (0/1/2) sets the initial mode. */
+enum { HIPBLS_PAIR_AUTO = 0, HIPBLS_PAIR_SINGLE = 1, HIPBLS_PAIR_LANES = 2 };
+int hipbls_set_pair_mode(int mode);
 
 /* ------------------------------------------------ single-item Verify through the submission queue ---- */
 /* tbls.Verify for one item.  Concurrent callers (any thread) are coalesced into one kernel launch per batch:
@@ -215,8 +223,9 @@ int hipbls_batch_verify_rlc_keys_device(const uint32_t* d_key_idx, const uint8_t
 
 /* Average duration (ms) per launch of a kernel over the calls since the last reset, measured with HIP
  * events on the stream it runs on (bench.py roofline; enable with hipbls_set_timing).  Names: "verify"
- * (k_verify_fused), "verify_keys", "rlc_items", "rlc_hash", "rlc_window", "rlc_fallback", "tagg_scale",
- * "tagg_sum", "fav". */
+ * (k_verify_fused), "verify_prep" + "verify_pair_lg2" (lane-pair Verify), "verify_keys", "rlc_items",
+ * "rlc_hash", "rlc_window" / "rlc_window_lg2", "rlc_fallback" / "rlc_fallback_lg2", "tagg_scale", "tagg_sum",
+ * "fav". */
 int hipbls_kernel_timing(const char* name, double* avg_ms, uint64_t* launches);
 int hipbls_kernel_timing_reset(void);
 
