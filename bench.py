@@ -13,6 +13,7 @@ an extra field.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
 import random
@@ -46,18 +47,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=65536, help="verifies per GPU per step (C2: 65,536)")
-    ap.add_argument("--tagg-groups", type=int, default=10000, help="C3 validators per GPU (0 = skip)")
+    ap.add_argument("--c2-items", dest="n", type=int, default=65536,
+                    help="C2 verifies per GPU per step (65,536); node batch = items x world")
+    ap.add_argument("--tagg-groups", type=int, default=10000,
+                    help="C3 validators per GPU (0 = skip); node batch = groups x world")
     ap.add_argument("--tagg-steps", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=4096,
                     help="C2 items verified by the C++ CPU baseline, one thread per core (0 = skip)")
-    ap.add_argument("--rlc-validators", type=int, default=32768,
-                    help="C4 validators per GPU (x4 partials; 32,768 = the 1M-partial node batch / 8 GPUs; 0 = skip)")
+    ap.add_argument("--rlc-node-validators", type=int, default=262144,
+                    help="C4 node batch in validators (x4 partials; 262,144 = 1M partials), sliced over the ranks "
+                         "with shard_range (0 = skip)")
     ap.add_argument("--rlc-steps", type=int, default=3)
     ap.add_argument("--c5", type=int, default=1, help="time the C5 full-slot mix (0 = skip)")
     ap.add_argument("--keys", type=int, default=1, help="also time C2 / C4 with the resident pubshare table (0 = skip)")
-    ap.add_argument("--rlc-big-validators", type=int, default=262144,
-                    help="also time one GPU on the whole C4 node batch (262,144 x 4 = 1M partials; 0 = skip)")
     return ap.parse_args()
 
 
@@ -65,92 +67,145 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def make_c2(impl, n, rng):
-    """n partial signatures by 4,096 share keys over distinct roots; 1% corrupted at seeded spots."""
-    nkeys = min(4096, n)
-    sks = [rng.randrange(1, R_ORDER).to_bytes(32, "big") for _ in range(nkeys)]
+# ---------------------------------------------------------------- synthetic node batches
+# Every item of a node batch is a pure function of (SEED, config tag, global index), so each rank builds exactly its
+# shard_range slice of the same node batch and can recompute the node-wide expected bitmap after the all-gather.
+def _hb(*parts) -> bytes:
+    return hashlib.sha256(("%x|" % SEED + "|".join(str(p) for p in parts)).encode()).digest()
+
+
+def _hi(*parts) -> int:
+    return int.from_bytes(_hb(*parts)[:8], "big")
+
+
+def _scalar(*parts) -> int:
+    """Uniform-ish secret in [1, r)."""
+    return int.from_bytes(_hb(*parts), "big") % (R_ORDER - 1) + 1
+
+
+def share_keys(impl, nkeys, tag):
+    sks = [_scalar(tag, "sk", k).to_bytes(32, "big") for k in range(nkeys)]
     pks, st = impl.secret_to_public_key_batch(sks)
     assert set(st) == {0}
-    roots = [rng.randbytes(32) for _ in range(n)]
-    owner = [i % nkeys for i in range(n)]
+    return sks, pks
+
+
+def c2_is_bad(i):
+    r = _hi("c2", "bad", i)
+    return r % 100 == 0, (r >> 32) % 3
+
+
+def make_c2(impl, keys, lo, hi):
+    """Items [lo, hi) of the C2 node batch: partial signatures by 4,096 share keys over distinct roots, ~1% corrupted
+    (wrong root / swapped share / flipped signature bit).  Returns local lists + the set of local bad indices."""
+    sks, pks = keys
+    nk = len(sks)
+    idx = range(lo, hi)
+    roots = [_hb("c2", "root", i) for i in idx]
+    owner = [i % nk for i in idx]
     sigs, st = impl.sign_batch([sks[o] for o in owner], roots)
-    assert set(st) == {0}
+    assert set(st) <= {0}
     pk_list = [pks[o] for o in owner]
-    bad = sorted(rng.sample(range(n), max(1, n // 100)))
-    for j, i in enumerate(bad):
-        kind = j % 3
-        if kind == 0:    # wrong root
-            roots[i] = bytes(32 - len(roots[i][:1])) + roots[i][:1]
-        elif kind == 1:  # swapped share (another validator's pubshare)
-            pk_list[i] = pks[(owner[i] + 1) % nkeys]
-        else:            # flipped bit in the signature
-            s = bytearray(sigs[i])
+    bad = set()
+    for j, i in enumerate(idx):
+        is_bad, kind = c2_is_bad(i)
+        if not is_bad:
+            continue
+        bad.add(j)
+        if kind == 0:
+            roots[j] = _hb("c2", "wrong-root", i)
+        elif kind == 1:
+            pk_list[j] = pks[(owner[j] + 1) % nk]
+        else:
+            s = bytearray(sigs[j])
             s[40] ^= 0x04
-            sigs[i] = bytes(s)
-    return pk_list, roots, sigs, set(bad)
+            sigs[j] = bytes(s)
+    return pk_list, roots, sigs, bad
 
 
-def make_c3(impl, groups, rng, t=7, n=10):
-    """groups DVs, each split t-of-n; a random t-subset of partials per DV; DV pubkeys + one root each."""
-    secrets_ = [rng.randrange(1, R_ORDER) for _ in range(groups)]
-    roots = [rng.randbytes(32) for _ in range(groups)]
-    part_sks, part_msgs, part_ids, offs = [], [], [], [0]
-    for g in range(groups):
-        poly = [secrets_[g]] + [rng.randrange(R_ORDER) for _ in range(t - 1)]
-        ids = sorted(rng.sample(range(1, n + 1), t))
+def make_c3(impl, g_lo, g_hi, t=7, n=10):
+    """Validators [g_lo, g_hi) of the C3 node batch: each split t-of-n, a seeded t-subset of partials, the DV pubkey
+    and one root each."""
+    part_sks, part_msgs, part_ids, offs, secrets_, roots = [], [], [], [0], [], []
+    for v in range(g_lo, g_hi):
+        secret = _scalar("c3", "sk", v)
+        poly = [secret] + [_scalar("c3", "poly", v, k) - 1 for k in range(t - 1)]
+        ids = sorted(random.Random(_hi("c3", "ids", v)).sample(range(1, n + 1), t))
+        root = _hb("c3", "root", v)
+        secrets_.append(secret)
+        roots.append(root)
         for i in ids:
             acc = 0
             for c in reversed(poly):
                 acc = (acc * i + c) % R_ORDER
             part_sks.append(acc.to_bytes(32, "big"))
-            part_msgs.append(roots[g])
+            part_msgs.append(root)
             part_ids.append(i)
         offs.append(len(part_ids))
     psigs, st = impl.sign_batch(part_sks, part_msgs)
-    assert set(st) == {0}
+    assert set(st) <= {0}
     dv_pks, st = impl.secret_to_public_key_batch([s.to_bytes(32, "big") for s in secrets_])
-    assert set(st) == {0}
+    assert set(st) <= {0}
     return psigs, part_ids, offs, dv_pks, roots
 
 
-def make_c4(impl, n_dv, rng, shared_roots=0, shares=4, nkeys=4096):
-    """C4 shard: n_dv validators x `shares` partials, items grouped by validator.  One root per
-    validator (variant i) or `shared_roots` committee roots (variant ii).  1% corrupted."""
-    n = n_dv * shares
-    sks = [rng.randrange(1, R_ORDER).to_bytes(32, "big") for _ in range(nkeys)]
-    keys, st = impl.secret_to_public_key_batch(sks)
-    assert set(st) == {0}
-    if shared_roots:
-        roots = [rng.randbytes(32) for _ in range(shared_roots)]
-        dv_root = [d * shared_roots // n_dv for d in range(n_dv)]  # contiguous committees
+def c4_item(tag, v, j, nk):
+    """(owner key, bad?, kind) of partial j of validator v."""
+    r = _hi(tag, v, j)
+    return r % nk, (r >> 20) % 100 == 0, (r >> 40) & 1
+
+
+def make_c4(impl, keys, tag, v_lo, v_hi, v_node, n_roots_node=0, shares=4):
+    """Validators [v_lo, v_hi) of a C4 node batch of v_node validators x `shares` partials, items grouped by
+    validator.  One root per validator (n_roots_node = 0, variant i) or n_roots_node committee roots over the node
+    batch, contiguous committees (variant ii).  ~1% corrupted (swapped share / flipped signature bit)."""
+    sks, pks = keys
+    nk = len(sks)
+    if n_roots_node:
+        root_of = [v * n_roots_node // v_node for v in range(v_lo, v_hi)]
     else:
-        roots = [rng.randbytes(32) for _ in range(n_dv)]
-        dv_root = list(range(n_dv))
-    owner = [rng.randrange(nkeys) for _ in range(n)]
-    midx = [dv_root[i // shares] for i in range(n)]
+        root_of = list(range(v_lo, v_hi))
+    first = root_of[0] if root_of else 0
+    roots = [_hb(tag, "root", g) for g in range(first, (root_of[-1] + 1) if root_of else 0)]
+    owner, midx, bad, kinds = [], [], set(), {}
+    for dv, v in enumerate(range(v_lo, v_hi)):
+        for j in range(shares):
+            o, is_bad, kind = c4_item(tag, v, j, nk)
+            if is_bad:
+                bad.add(len(owner))
+                kinds[len(owner)] = kind
+            owner.append(o)
+            midx.append(root_of[dv] - first)
     sigs, st = impl.sign_batch([sks[o] for o in owner], [roots[m] for m in midx])
-    assert set(st) == {0}
-    pks = [keys[o] for o in owner]
-    bad = sorted(rng.sample(range(n), max(1, n // 100)))
-    for j, i in enumerate(bad):
-        if j % 2 == 0:  # swapped share
-            pks[i] = keys[(owner[i] + 1) % nkeys]
-        else:           # flipped bit in the signature
+    assert set(st) <= {0}
+    pk_list = [pks[o] for o in owner]
+    for i, kind in kinds.items():
+        if kind == 0:
+            pk_list[i] = pks[(owner[i] + 1) % nk]
+        else:
             s = bytearray(sigs[i])
             s[40] ^= 0x04
             sigs[i] = bytes(s)
-    return pks, sigs, midx, roots, set(bad)
+    return pk_list, sigs, midx, roots, bad
 
 
-def traffic_from_pmc(path=os.path.join(ROOT, "profiles", "r01_pmc_verify.json")):
-    """HBM bytes per k_verify_fused launch from the committed rocprofv3 PMC passes of this build
-    (FETCH_SIZE + WRITE_SIZE, scripts/pmc_summary.py); None when absent.  Almost all of it is
-    scratch (register-spill) traffic, ~8000x the 188 B/verify of algorithmic input."""
+def c4_node_bad(tag, v_node, nk, shares=4):
+    return {v * shares + j for v in range(v_node) for j in range(shares) if c4_item(tag, v, j, nk)[1]}
+
+
+def pmc_summary(path=os.path.join(ROOT, "profiles", "r02_pmc_verify.json")):
+    """k_verify_fused counters from the committed rocprofv3 --pmc passes over this build's bench (scripts/gpu_pmc.sh,
+    scripts/pmc_summary.py): HBM bytes per launch (FETCH_SIZE + WRITE_SIZE), their ratio to the 188 B/verify of
+    algorithmic input, VALU utilisation (SQ_ACTIVE_INST_VALU / SQ_BUSY_CYCLES per SIMD) and the fraction of wave
+    cycles spent waiting.  {} when absent."""
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch_raw")
+            d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return {}
+    return {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch_raw"), "traffic_ratio": d.get("traffic_ratio"),
+            "valu_util": d.get("valu_util"), "wait_any_frac": d.get("wait_any_frac"),
+            "source": os.path.relpath(path, ROOT)}
 
 
 def _cpu_model():
@@ -239,6 +294,38 @@ def cpu_baseline(impl, c2, n_sample, rng):
                             "threshold_aggregates_per_s": round(G / t_agg, 1)}}
 
 
+def timed_loop(step, steps, dev, barrier, world):
+    """barrier + synchronize, `steps` calls, synchronize + barrier; max over ranks (seconds)."""
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    else:
+        t = torch.tensor([el], dtype=torch.float64)
+    return float(t.item())
+
+
+def kernel_ms(lib, names):
+    out = {}
+    for k in names:
+        a = ctypes.c_double()
+        c = ctypes.c_uint64()
+        lib.hipbls_kernel_timing(k.encode(), ctypes.byref(a), ctypes.byref(c))
+        if c.value:  # lane-pair (_lg2) or one-lane kernels, whichever HIPBLS_PAIR_AUTO picked
+            out[k] = round(a.value, 3)
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -247,250 +334,217 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:  # "nccl" is RCCL on ROCm
-        dist.init_process_group(backend="nccl", device_id=dev)
+    # one rank per GPU; more ranks than GPUs only in a rehearsal (HIPBLS_BENCH_BACKEND=gloo on a one-GPU box)
+    local_dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
+    if world > 1:  # "nccl" is RCCL on ROCm: the production path
+        backend = os.environ.get("HIPBLS_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend=backend)
 
-    from charon_amd.shard import gather_bitmaps, pack_bitmap, unpack_bitmap
+    from charon_amd.shard import gather_aggregates, gather_bitmap_rows, gather_node_bitmap, shard_range, unpack_bitmap
     from charon_amd.tbls import HipBLS, load_library
-    impl = HipBLS(device=local)
+    impl = HipBLS(device=local_dev)
     lib = load_library()
     lib.hipbls_set_timing(1)  # per-kernel HIP events for the roofline (off by default in the library)
-
-    rng = random.Random(SEED * 1000003 + rank)  # validator-index shard of this rank
-    t0 = time.time()
-    pks, roots, sigs, bad = make_c2(impl, args.n, rng)
-    log("rank %d: C2 data (%d items) in %.1fs" % (rank, args.n, time.time() - t0))
-
-    n = args.n
-    d_pk = torch.frombuffer(bytearray(b"".join(pks)), dtype=torch.uint8).to(dev)
-    d_sig = torch.frombuffer(bytearray(b"".join(sigs)), dtype=torch.uint8).to(dev)
-    d_msg = torch.frombuffer(bytearray(b"".join(roots)), dtype=torch.uint8).to(dev)
-    d_off = torch.arange(0, 32 * (n + 1), 32, dtype=torch.int64).to(dev)
-    d_st = torch.full((n,), -1, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
-    gathered = [None]
-
-    def step():
-        rc = lib.hipbls_verify_batch_device(d_pk.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(), d_sig.data_ptr(),
-                                            n, d_st.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
-        if rc != 0:
-            raise RuntimeError("hipbls_verify_batch_device rc=%d %s" % (rc, lib.hipbls_last_error()))
-        if world > 1:  # the only collective: all-gather of the per-rank verify bitmaps (RCCL/xGMI)
-            gathered[0] = gather_bitmaps(pack_bitmap(d_st))
+    sp = ctypes.c_void_p(stream.cuda_stream)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
+    def u8(blobs):
+        return torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8).to(dev)
+
+    # ---- C2 (headline): the node batch is n x world items; this rank verifies its shard_range slice, then the
+    # per-rank bitmaps are all-gathered over RCCL inside the timed step (the only collective)
+    t0 = time.time()
+    keys2 = share_keys(impl, 4096, "c2")
+    n_node = args.n * world
+    lo, hi = shard_range(n_node, rank, world)
+    n = hi - lo
+    pks, roots, sigs, bad = make_c2(impl, keys2, lo, hi)
+    log("rank %d: C2 slice [%d, %d) of %d in %.1fs" % (rank, lo, hi, n_node, time.time() - t0))
+    d_pk, d_sig, d_msg = u8(pks), u8(sigs), u8(roots)
+    d_off = torch.arange(0, 32 * (n + 1), 32, dtype=torch.int64).to(dev)
+    d_st = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    node_ok = [None]
+
+    def step():
+        rc = lib.hipbls_verify_batch_device(d_pk.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(), d_sig.data_ptr(),
+                                            n, d_st.data_ptr(), sp)
+        if rc != 0:
+            raise RuntimeError("hipbls_verify_batch_device rc=%d %s" % (rc, lib.hipbls_last_error()))
+        if world > 1:
+            node_ok[0] = gather_node_bitmap(d_st, n_node)
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     lib.hipbls_kernel_timing_reset()
-    barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t_start
-
+    elapsed = timed_loop(step, args.steps, dev, barrier, world)
     st = d_st.cpu().tolist()
-    fails = {i for i, s in enumerate(st) if s != 0}
-    assert fails == bad, "verify bitmap mismatch: %d unexpected, %d missed" % (len(fails - bad), len(bad - fails))
-    if world > 1:  # my row of the gathered node bitmap equals my local result
-        mine = unpack_bitmap(gathered[0][rank], n).cpu()
-        assert {i for i in range(n) if not mine[i]} == bad, "gathered bitmap mismatch"
+    assert {i for i, s in enumerate(st) if s != 0} == bad, "verify bitmap mismatch"
+    if world > 1:  # the gathered node bitmap equals the node batch's construction
+        want = {i for i in range(n_node) if c2_is_bad(i)[0]}
+        got = node_ok[0].cpu()
+        assert {i for i in range(n_node) if not got[i]} == want, "gathered node bitmap mismatch"
     avg_ms = ctypes.c_double()
     launches = ctypes.c_uint64()
     lib.hipbls_kernel_timing(b"verify", ctypes.byref(avg_ms), ctypes.byref(launches))
+    value = n_node * args.steps / elapsed
 
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    elapsed = float(t_max.item())
-    total = n * args.steps * world
-    value = total / elapsed
-
-    # ---- C2 with the resident pubshare table (SURVEY §8f.2; extra field): same items, keys by index
+    # ---- C2 with the resident pubshare table (SURVEY 8f.2; extra field): same items, keys by index
     keys_rate = None
     if args.keys:
         table = list(dict.fromkeys(pks))
         pos = {k: j for j, k in enumerate(table)}
-        assert set(impl.load_pubshares(table)) == {0}
+        assert set(impl.load_pubshares(table)) <= {0}
         d_kidx = torch.tensor([pos[p] for p in pks], dtype=torch.int32).to(dev)
         d_kst = torch.full((n,), -1, dtype=torch.int32, device=dev)
 
         def kstep():
             rc = lib.hipbls_verify_batch_keys_device(d_kidx.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(),
-                                                     d_sig.data_ptr(), n, d_kst.data_ptr(),
-                                                     ctypes.c_void_p(stream.cuda_stream))
+                                                     d_sig.data_ptr(), n, d_kst.data_ptr(), sp)
             assert rc == 0
 
         kstep()
-        torch.cuda.synchronize(dev)
-        barrier()
-        ts = time.perf_counter()
-        for _ in range(args.steps):
-            kstep()
-        torch.cuda.synchronize(dev)
-        barrier()
-        tk = time.perf_counter() - ts
+        tk = timed_loop(kstep, args.steps, dev, barrier, world)
         assert d_kst.cpu().tolist() == st, "key-table bitmap differs from wire-format Verify"
-        tt = torch.tensor([tk], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        keys_rate = n * args.steps * world / float(tt.item())
+        keys_rate = n_node * args.steps / tk
 
-    # ---- C3: threshold aggregation + Verify of the aggregate (extra field)
+    # ---- C3: threshold aggregation + Verify of each aggregate; node batch = groups x world validators, this rank's
+    # slice; the 96-byte aggregates and the verify bitmap are all-gathered inside the timed step
     tagg = None
     if args.tagg_groups > 0:
         t0 = time.time()
-        psigs, pids, poffs, dv_pks, droots = make_c3(impl, args.tagg_groups, rng)
-        log("rank %d: C3 data (%d groups) in %.1fs" % (rank, args.tagg_groups, time.time() - t0))
-        G = args.tagg_groups
-        d_psig = torch.frombuffer(bytearray(b"".join(psigs)), dtype=torch.uint8).to(dev)
+        G_node = args.tagg_groups * world
+        g_lo, g_hi = shard_range(G_node, rank, world)
+        G = g_hi - g_lo
+        psigs, pids, poffs, dv_pks, droots = make_c3(impl, g_lo, g_hi)
+        log("rank %d: C3 slice [%d, %d) of %d validators in %.1fs" % (rank, g_lo, g_hi, G_node, time.time() - t0))
+        d_psig = u8(psigs)
         d_pid = torch.tensor(pids, dtype=torch.int64).to(dev)
         d_poff = torch.tensor(poffs, dtype=torch.int64).to(dev)
         d_agg = torch.zeros(G * 96, dtype=torch.uint8, device=dev)
         d_gst = torch.full((G,), -1, dtype=torch.int32, device=dev)
-        d_dpk = torch.frombuffer(bytearray(b"".join(dv_pks)), dtype=torch.uint8).to(dev)
-        d_dmsg = torch.frombuffer(bytearray(b"".join(droots)), dtype=torch.uint8).to(dev)
+        d_dpk, d_dmsg = u8(dv_pks), u8(droots)
         d_doff = torch.arange(0, 32 * (G + 1), 32, dtype=torch.int64).to(dev)
         d_vst = torch.full((G,), -1, dtype=torch.int32, device=dev)
+        node_aggs = [None, None]
 
         def tstep():
             rc = lib.hipbls_threshold_aggregate_batch_device(d_psig.data_ptr(), d_pid.data_ptr(), d_poff.data_ptr(), G,
-                                                             len(pids), d_agg.data_ptr(), d_gst.data_ptr(),
-                                                             ctypes.c_void_p(stream.cuda_stream))
+                                                             len(pids), d_agg.data_ptr(), d_gst.data_ptr(), sp)
             assert rc == 0
             rc = lib.hipbls_verify_batch_device(d_dpk.data_ptr(), d_dmsg.data_ptr(), d_doff.data_ptr(),
-                                                d_agg.data_ptr(), G, d_vst.data_ptr(),
-                                                ctypes.c_void_p(stream.cuda_stream))
+                                                d_agg.data_ptr(), G, d_vst.data_ptr(), sp)
             assert rc == 0
+            if world > 1:
+                node_aggs[0] = gather_aggregates(d_agg, G_node)
+                node_aggs[1] = gather_node_bitmap(d_vst, G_node)
 
         tstep()
-        torch.cuda.synchronize(dev)
-        barrier()
-        ts = time.perf_counter()
-        for _ in range(args.tagg_steps):
-            tstep()
-        torch.cuda.synchronize(dev)
-        barrier()
-        tel = time.perf_counter() - ts
+        tel = timed_loop(tstep, args.tagg_steps, dev, barrier, world)
         assert set(d_gst.cpu().tolist()) == {0} and set(d_vst.cpu().tolist()) == {0}, "aggregate mismatch"
-        tt = torch.tensor([tel], dtype=torch.float64, device=dev)
         if world > 1:
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        tagg = G * args.tagg_steps * world / float(tt.item())
+            assert torch.equal(node_aggs[0][96 * g_lo:96 * g_hi], d_agg), "gathered aggregates differ from local"
+            assert bool(node_aggs[1].all()), "an aggregate of the node batch failed Verify"
+        tagg = G_node * args.tagg_steps / tel
 
-    # ---- C4: random-linear-combination BatchVerify of this rank's shard (extra fields)
+    # ---- C4: RLC BatchVerify of the 1M-partial node batch, validator-index slices over the ranks (strong scaling:
+    # the node batch is fixed); node bitmap all-gathered inside the timed step
     rlc = {}
-    if args.rlc_validators > 0:
-        variants = [("i_root_per_validator", args.rlc_validators, 0),
-                    ("ii_committee_roots", args.rlc_validators, max(1, args.rlc_validators // 128))]
-        if args.rlc_big_validators > 0:
-            variants.append(("i_node_batch_on_each_gpu", args.rlc_big_validators, 0))
-        for variant, n_dv, shared in variants:
+    c4i = None
+    if args.rlc_node_validators > 0:
+        V = args.rlc_node_validators
+        v_lo, v_hi = shard_range(V, rank, world)
+        keys4 = share_keys(impl, 4096, "c4")
+        for variant, tag, n_roots in (("i_root_per_validator", "c4i", 0),
+                                      ("ii_committee_roots", "c4ii", max(1, V // 128))):
             t0 = time.time()
-            pks4, sigs4, midx4, roots4, bad4 = make_c4(impl, n_dv, rng, shared_roots=shared)
+            pks4, sigs4, midx4, roots4, bad4 = make_c4(impl, keys4, tag, v_lo, v_hi, V, n_roots)
             n4 = len(pks4)
-            log("rank %d: C4(%s) data (%d items, %d roots) in %.1fs" % (rank, variant, n4, len(roots4), time.time() - t0))
-            d_pk4 = torch.frombuffer(bytearray(b"".join(pks4)), dtype=torch.uint8).to(dev)
-            d_sig4 = torch.frombuffer(bytearray(b"".join(sigs4)), dtype=torch.uint8).to(dev)
+            log("rank %d: C4(%s) validators [%d, %d) of %d: %d items, %d roots in %.1fs"
+                % (rank, variant, v_lo, v_hi, V, n4, len(roots4), time.time() - t0))
+            d_pk4, d_sig4, d_msg4 = u8(pks4), u8(sigs4), u8(roots4)
             d_midx4 = torch.tensor(midx4, dtype=torch.int32).to(dev)
-            d_msg4 = torch.frombuffer(bytearray(b"".join(roots4)), dtype=torch.uint8).to(dev)
             d_off4 = torch.arange(0, 32 * (len(roots4) + 1), 32, dtype=torch.int64).to(dev)
             d_st4 = torch.full((n4,), -7, dtype=torch.int32, device=dev)
             seed = os.urandom(32)
+            node4 = [None]
 
             def rstep():
                 rc = lib.hipbls_batch_verify_rlc_device(d_pk4.data_ptr(), d_sig4.data_ptr(), d_midx4.data_ptr(), n4,
                                                         d_msg4.data_ptr(), d_off4.data_ptr(), len(roots4), seed,
-                                                        d_st4.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+                                                        d_st4.data_ptr(), sp)
                 if rc != 0:
                     raise RuntimeError("hipbls_batch_verify_rlc_device rc=%d" % rc)
+                if world > 1:
+                    node4[0] = gather_node_bitmap(d_st4, 4 * V)
 
             rstep()
             torch.cuda.synchronize(dev)
             lib.hipbls_kernel_timing_reset()
-            barrier()
-            torch.cuda.synchronize(dev)
-            ts = time.perf_counter()
-            for _ in range(args.rlc_steps):
-                rstep()
-            torch.cuda.synchronize(dev)
-            barrier()
-            tel = time.perf_counter() - ts
+            tel = timed_loop(rstep, args.rlc_steps, dev, barrier, world)
             st4 = d_st4.cpu().tolist()
             assert {i for i, x in enumerate(st4) if x != 0} == bad4, "RLC bitmap mismatch"
+            if world > 1:
+                got = node4[0].cpu()
+                want = c4_node_bad(tag, V, len(keys4[0]))
+                assert {i for i in range(4 * V) if not got[i]} == want, "gathered RLC node bitmap mismatch"
             w = ctypes.c_uint64()
             wf = ctypes.c_uint64()
             fb = ctypes.c_uint64()
             lib.hipbls_rlc_stats(ctypes.byref(w), ctypes.byref(wf), ctypes.byref(fb))
-            kms = {}
-            for k in ("rlc_items", "rlc_hash", "rlc_window", "rlc_window_lg2", "rlc_fallback", "rlc_fallback_lg2"):
-                a = ctypes.c_double()
-                c = ctypes.c_uint64()
-                lib.hipbls_kernel_timing(k.encode(), ctypes.byref(a), ctypes.byref(c))
-                if c.value:  # lane-pair (_lg2) or one-lane kernels, whichever HIPBLS_PAIR_AUTO picked
-                    kms[k] = round(a.value, 3)
-            tt = torch.tensor([tel], dtype=torch.float64, device=dev)
-            if world > 1:
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            per_win = RLC_FPMUL["window_1msg"] if shared else RLC_FPMUL["window_2msg"]
+            per_win = RLC_FPMUL["window_1msg"] if n_roots else RLC_FPMUL["window_2msg"]
             fpmul = (RLC_FPMUL["item"] * n4 + RLC_FPMUL["hash"] * len(roots4) + per_win * w.value
                      + RLC_FPMUL["fallback"] * fb.value)
-            ach = fpmul * MADS_PER_FPMUL * args.rlc_steps / float(tt.item()) / 1e12
-            rlc[variant] = {"verified_partial_sigs_per_s": round(n4 * args.rlc_steps * world / float(tt.item()), 1),
-                            "fpmul_per_item": round(fpmul / n4, 1),
+            ach = fpmul * MADS_PER_FPMUL * args.rlc_steps / tel / 1e12
+            rlc[variant] = {"verified_partial_sigs_per_s": round(4 * V * args.rlc_steps / tel, 1),
+                            "node_items": 4 * V, "items_this_gpu": n4, "distinct_roots_this_gpu": len(roots4),
+                            "fpmul_per_item": round(fpmul / max(n4, 1), 1),
                             "pipeline_roofline": {"achieved": round(ach, 3), "peak": MAD_PEAK_T, "unit": "Tmad/s",
                                                   "frac": round(ach / MAD_PEAK_T, 4),
-                                                  "note": "whole 4-stage pipeline over wall time (not one kernel)"},
-                            "items_per_gpu": n4, "distinct_roots_per_gpu": len(roots4),
-                            "ms_per_batch": round(1000 * float(tt.item()) / args.rlc_steps, 3),
+                                                  "note": "rank 0's 4-stage pipeline over wall time (not one kernel)"},
+                            "ms_per_batch": round(1000 * tel / args.rlc_steps, 3),
                             "windows": w.value, "windows_failed": wf.value, "items_fallback": fb.value,
-                            "kernel_avg_ms": kms}
+                            "kernel_avg_ms": kernel_ms(lib, ("rlc_items", "rlc_hash", "rlc_window", "rlc_window_lg2",
+                                                             "rlc_fallback", "rlc_fallback_lg2"))}
             if args.keys and variant == "i_root_per_validator":
-                # same batch with pubshares from the resident table
                 table4 = list(dict.fromkeys(pks4))
                 pos4 = {k: j for j, k in enumerate(table4)}
-                assert set(impl.load_pubshares(table4)) == {0}
+                assert set(impl.load_pubshares(table4)) <= {0}
                 d_k4 = torch.tensor([pos4[p] for p in pks4], dtype=torch.int32).to(dev)
 
                 def rkstep():
-                    rc = lib.hipbls_batch_verify_rlc_keys_device(d_k4.data_ptr(), d_sig4.data_ptr(),
-                                                                 d_midx4.data_ptr(), n4, d_msg4.data_ptr(),
-                                                                 d_off4.data_ptr(), len(roots4), seed,
-                                                                 d_st4.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+                    rc = lib.hipbls_batch_verify_rlc_keys_device(d_k4.data_ptr(), d_sig4.data_ptr(), d_midx4.data_ptr(),
+                                                                 n4, d_msg4.data_ptr(), d_off4.data_ptr(), len(roots4),
+                                                                 seed, d_st4.data_ptr(), sp)
                     assert rc == 0
 
                 rkstep()
-                torch.cuda.synchronize(dev)
-                barrier()
-                ts = time.perf_counter()
-                for _ in range(args.rlc_steps):
-                    rkstep()
-                torch.cuda.synchronize(dev)
-                barrier()
-                tk = time.perf_counter() - ts
+                tk = timed_loop(rkstep, args.rlc_steps, dev, barrier, world)
                 assert d_st4.cpu().tolist() == st4, "RLC key-table bitmap differs"
-                tt = torch.tensor([tk], dtype=torch.float64, device=dev)
-                if world > 1:
-                    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                rlc[variant]["verified_partial_sigs_per_s_pubshare_table"] = round(
-                    n4 * args.rlc_steps * world / float(tt.item()), 1)
+                rlc[variant]["verified_partial_sigs_per_s_pubshare_table"] = round(4 * V * args.rlc_steps / tk, 1)
+                del d_k4
+            if variant == "i_root_per_validator":
+                c4i = (pks4, sigs4, midx4, roots4, bad4)
             del d_pk4, d_sig4, d_midx4, d_msg4, d_off4, d_st4
 
-    # ---- C5: full-slot mix on this rank's shard: RLC over the C4 shard + 32 validators x 4 proposer
-    # partials (own roots), concurrently with a 512-key sync-committee FastAggregateVerify
+    # ---- C5: full-slot mix on this rank's slice: RLC over the C4(i) slice + its slice of 32 validators x 4 proposer
+    # partials (own roots), with the 512-key sync-committee FastAggregateVerify (hash-to-G2 of its root) overlapped on
+    # rank 0
     c5 = None
-    if args.c5 and args.rlc_validators > 0:
+    if args.c5 and c4i is not None:
         t0 = time.time()
-        pks5, sigs5, midx5, roots5, bad5 = make_c4(impl, args.rlc_validators, rng)
-        ppks, psigs, pmidx, proots, pbad = make_c4(impl, 32, rng, nkeys=128)
+        pks5, sigs5, midx5, roots5, bad5 = [list(x) if not isinstance(x, set) else set(x) for x in c4i]
+        p_lo, p_hi = shard_range(32, rank, world)
+        ppks, psigs, pmidx, proots, pbad = make_c4(impl, share_keys(impl, 128, "c5p"), "c5p", p_lo, p_hi, 32)
         off = len(roots5)
         base = len(pks5)
         pks5 += ppks
@@ -499,59 +553,59 @@ def main():
         roots5 += proots
         bad5 |= {base + i for i in pbad}
         n5 = len(pks5)
-        sync_sks = [rng.randrange(1, R_ORDER).to_bytes(32, "big") for _ in range(512)]
+        sync_sks = [_scalar("c5sync", k).to_bytes(32, "big") for k in range(512)]
         sync_pks, _ = impl.secret_to_public_key_batch(sync_sks)
-        sync_root = rng.randbytes(32)
+        sync_root = _hb("c5sync", "root")
         ssigs, _ = impl.sign_batch(sync_sks, [sync_root] * 512)
         sync_agg = impl.aggregate(ssigs)
         log("rank %d: C5 data (%d partials + 512-key sync aggregate) in %.1fs" % (rank, n5, time.time() - t0))
-        d_pk5 = torch.frombuffer(bytearray(b"".join(pks5)), dtype=torch.uint8).to(dev)
-        d_sig5 = torch.frombuffer(bytearray(b"".join(sigs5)), dtype=torch.uint8).to(dev)
+        d_pk5, d_sig5, d_msg5 = u8(pks5), u8(sigs5), u8(roots5)
         d_midx5 = torch.tensor(midx5, dtype=torch.int32).to(dev)
-        d_msg5 = torch.frombuffer(bytearray(b"".join(roots5)), dtype=torch.uint8).to(dev)
         d_off5 = torch.arange(0, 32 * (len(roots5) + 1), 32, dtype=torch.int64).to(dev)
         d_st5 = torch.full((n5,), -7, dtype=torch.int32, device=dev)
-        d_spk = torch.frombuffer(bytearray(b"".join(sync_pks)), dtype=torch.uint8).to(dev)
+        d_spk = u8(sync_pks)
         d_skoff = torch.tensor([0, 512], dtype=torch.int64).to(dev)
-        d_ssig = torch.frombuffer(bytearray(sync_agg), dtype=torch.uint8).to(dev)
-        d_smsg = torch.frombuffer(bytearray(sync_root), dtype=torch.uint8).to(dev)
+        d_ssig, d_smsg = u8([sync_agg]), u8([sync_root])
         d_smoff = torch.tensor([0, 32], dtype=torch.int64).to(dev)
         d_sst = torch.full((1,), -7, dtype=torch.int32, device=dev)
         seed5 = os.urandom(32)
+        node5 = [None]
+        n5_node = 4 * args.rlc_node_validators + 128
+        c5_rows = [4 * (shard_range(V, r, world)[1] - shard_range(V, r, world)[0])
+                   + 4 * (shard_range(32, r, world)[1] - shard_range(32, r, world)[0]) for r in range(world)]
+        c5_max = max(c5_rows)
 
         def c5step():
-            # the sync-committee check goes on the library's own stream (NULL) and overlaps the RLC
-            rc = lib.hipbls_verify_aggregate_batch_device(d_spk.data_ptr(), 512, d_skoff.data_ptr(), 1,
-                                                          d_ssig.data_ptr(), d_smsg.data_ptr(), d_smoff.data_ptr(),
-                                                          d_sst.data_ptr(), None)
-            assert rc == 0
+            if rank == 0:  # on the library's own stream (NULL), overlapping the RLC
+                rc = lib.hipbls_verify_aggregate_batch_device(d_spk.data_ptr(), 512, d_skoff.data_ptr(), 1,
+                                                              d_ssig.data_ptr(), d_smsg.data_ptr(), d_smoff.data_ptr(),
+                                                              d_sst.data_ptr(), None)
+                assert rc == 0
             rc = lib.hipbls_batch_verify_rlc_device(d_pk5.data_ptr(), d_sig5.data_ptr(), d_midx5.data_ptr(), n5,
                                                     d_msg5.data_ptr(), d_off5.data_ptr(), len(roots5), seed5,
-                                                    d_st5.data_ptr(), ctypes.c_void_p(stream.cuda_stream))
+                                                    d_st5.data_ptr(), sp)
             assert rc == 0
+            if world > 1:
+                node5[0] = gather_bitmap_rows(d_st5, c5_max)
 
         c5step()
         torch.cuda.synchronize()
-        barrier()
-        ts = time.perf_counter()
-        for _ in range(args.rlc_steps):
-            c5step()
+        t5 = timed_loop(c5step, args.rlc_steps, dev, barrier, world)
         torch.cuda.synchronize()
-        barrier()
-        t5 = time.perf_counter() - ts
         assert {i for i, x in enumerate(d_st5.cpu().tolist()) if x != 0} == bad5, "C5 bitmap mismatch"
-        assert d_sst.cpu().tolist() == [0], "sync-committee FastAggregateVerify failed"
-        tt = torch.tensor([t5], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t5 = float(tt.item())
-        c5 = {"workload": "C5 (BASELINE configs[4]) per GPU: RLC BatchVerify of the C4 shard (%d validators x 4, "
-                          "one root each) + 32 validators x 4 proposer partials (own roots), 1%% corrupted, with a "
-                          "512-key sync-committee FastAggregateVerify (hash-to-G2 of its root) overlapped"
-                          % args.rlc_validators,
-              "partials_per_slot_per_gpu": n5, "ms_per_slot": round(1000 * t5 / args.rlc_steps, 3),
-              "verified_partial_sigs_per_s": round(n5 * args.rlc_steps * world / t5, 1),
-              "sync_aggregate_verifies_per_s": round(args.rlc_steps * world / t5, 3)}
+        if rank == 0:
+            assert d_sst.cpu().tolist() == [0], "sync-committee FastAggregateVerify failed"
+        if world > 1:  # node-wide failure count == construction
+            rows = node5[0]
+            fails = sum(int((~unpack_bitmap(rows[r], c5_rows[r])).sum()) for r in range(world))
+            assert fails == len(c4_node_bad("c4i", V, 4096)) + len(c4_node_bad("c5p", 32, 128)), "C5 node bitmap"
+        c5 = {"workload": "C5 (BASELINE configs[4]): RLC BatchVerify of the C4(i) node batch (%d validators x 4, one "
+                          "root each) + 32 validators x 4 proposer partials (own roots), ~1%% corrupted, sliced over "
+                          "the ranks by validator index, with a 512-key sync-committee FastAggregateVerify (hash-to-G2 "
+                          "of its root) overlapped on rank 0" % args.rlc_node_validators,
+              "node_partials": n5_node, "partials_this_gpu": n5, "ms_per_slot": round(1000 * t5 / args.rlc_steps, 3),
+              "verified_partial_sigs_per_s": round(n5_node * args.rlc_steps / t5, 1),
+              "sync_aggregate_verifies_per_s": round(args.rlc_steps / t5, 3)}
         del d_pk5, d_sig5, d_midx5, d_msg5, d_off5, d_st5
 
     if rank == 0:
@@ -567,29 +621,32 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic: seeded share keys, distinct 32-byte roots, 1% corrupted (wrong root / swapped "
-                    "share / flipped sig bit); signatures made by the engine's own sign kernel",
+            "data": "synthetic: seeded share keys, distinct 32-byte roots, ~1% corrupted (wrong root / swapped "
+                    "share / flipped sig bit); signatures made by the engine's own sign kernel; every item a function "
+                    "of (seed, global index), each rank builds its shard_range slice of the node batch",
             "config": {"workload": "C2 (BASELINE.json configs[1]): individual tbls.Verify of %d partial sigs per GPU, "
-                                   "distinct messages" % n,
-                       "items_per_gpu": n, "parallelism": "shard-by-validator-index x %d" % world},
+                                   "distinct messages" % args.n,
+                       "items_per_gpu": args.n, "node_items": n_node,
+                       "parallelism": "shard-by-validator-index x %d (RCCL all-gather of the verify bitmaps)" % world},
             "pairings_per_s": round(2 * value, 1),
             "verified_partial_sigs_per_s_pubshare_table": round(keys_rate, 1) if keys_rate else None,
             "threshold_aggregates_per_s": round(tagg, 1) if tagg else None,
-            "threshold_aggregate_workload": "C3: %d validators x 7-of-10 Lagrange in G2 + Verify of each aggregate per GPU"
-                                            % args.tagg_groups if tagg else None,
+            "threshold_aggregate_workload": "C3: %d validators per GPU x 7-of-10 Lagrange in G2 + Verify of each "
+                                            "aggregate; aggregates and bitmap all-gathered" % args.tagg_groups
+            if tagg else None,
         }
         if c5:
             out["full_slot_mix"] = c5
         if rlc:
-            out["rlc_batch_verify"] = dict(rlc, workload="C4 (BASELINE configs[3]): validators x 4 partials per GPU, "
-                                                        "items grouped by validator, 1%% corrupted (swapped share / "
-                                                        "flipped sig bit), windows of 8 items, per-item bitmap == "
-                                                        "tbls.Verify; i/ii = the 1M-partial node batch sharded over 8 "
-                                                        "GPUs (%d validators per GPU), node_batch = all 1M on every GPU"
-                                                        % args.rlc_validators)
+            out["rlc_batch_verify"] = dict(rlc, workload="C4 (BASELINE configs[3]): the %d-validator x 4-partial node "
+                                                        "batch sliced over %d GPU(s) by validator index (strong "
+                                                        "scaling), items grouped by validator, ~1%% corrupted, windows "
+                                                        "of 8 items, per-item bitmap == tbls.Verify, node bitmap "
+                                                        "all-gathered" % (args.rlc_node_validators, world))
         k_ms = avg_ms.value
         if k_ms > 0:
             achieved = FPMUL_PER_VERIFY * MADS_PER_FPMUL * n / (k_ms * 1e-3) / 1e12
+            pmc = pmc_summary()
             out["roofline"] = {
                 "bound": "valu-int (32x32->64 v_mad_u64_u32; no HBM or MFMA bound: ~190 B in per verify)",
                 "kernel": "k_verify_fused",
@@ -597,7 +654,11 @@ def main():
                 "peak": MAD_PEAK_T,
                 "unit": "Tmad/s",
                 "frac": round(achieved / MAD_PEAK_T, 4),
-                "traffic": traffic_from_pmc(),
+                "traffic": pmc.get("hbm_bytes_per_launch"),
+                "traffic_ratio": pmc.get("traffic_ratio"),
+                "valu_util": pmc.get("valu_util"),
+                "wait_any_frac": pmc.get("wait_any_frac"),
+                "pmc_source": pmc.get("source"),
                 "algorithmic_unit": "%d Fp-mul-equivalents x %d MADs per verify" % (FPMUL_PER_VERIFY, MADS_PER_FPMUL),
                 "kernel_avg_ms": round(k_ms, 3),
                 "kernel_launches": int(launches.value),

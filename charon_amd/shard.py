@@ -58,11 +58,15 @@ def _gather_padded(local: torch.Tensor, width: int, group=None) -> torch.Tensor:
     world = dist.get_world_size(group)
     if local.numel() > width:
         raise ValueError("local block larger than the padded width")
-    buf = torch.zeros(width, dtype=torch.uint8, device=local.device)
-    buf[:local.numel()] = local.reshape(-1)
-    out = torch.empty(world * width, dtype=torch.uint8, device=local.device)
+    # gloo has no device-tensor all-gather: a gloo group (the CPU tests, or a multi-rank rehearsal on one GPU) stages
+    # through host memory; RCCL ("nccl") gathers device tensors over xGMI directly
+    stage = local.is_cuda and dist.get_backend(group) == "gloo"
+    dev = torch.device("cpu") if stage else local.device
+    buf = torch.zeros(width, dtype=torch.uint8, device=dev)
+    buf[:local.numel()] = local.reshape(-1).to(dev)
+    out = torch.empty(world * width, dtype=torch.uint8, device=dev)
     dist.all_gather_into_tensor(out, buf, group=group)
-    return out.view(world, width)
+    return out.view(world, width).to(local.device)
 
 
 def gather_bitmaps(local_bits: torch.Tensor, n_items: int = None, group=None) -> torch.Tensor:
@@ -71,6 +75,12 @@ def gather_bitmaps(local_bits: torch.Tensor, n_items: int = None, group=None) ->
     world = dist.get_world_size(group)
     width = local_bits.numel() if n_items is None else (_max_shard(n_items, world) + 7) // 8
     return _gather_padded(local_bits, width, group)
+
+
+def gather_bitmap_rows(local_status: torch.Tensor, max_items: int, group=None) -> torch.Tensor:
+    """All-gather per-rank status vectors of different lengths (at most max_items each) as packed ok-bitmaps:
+    [world, ceil(max_items / 8)] on every rank; row r holds rank r's items in its first bits."""
+    return _gather_padded(pack_bitmap(local_status), (max_items + 7) // 8, group)
 
 
 def gather_node_bitmap(local_status: torch.Tensor, n_items: int, group=None) -> torch.Tensor:

@@ -26,7 +26,7 @@ def main():
     impl = HipBLS(device=0)
     lib = load_library()
     nmax = max(sizes)
-    pks, roots, sigs, bad = bench.make_c2(impl, nmax, random.Random(11))
+    pks, roots, sigs, bad = bench.make_c2(impl, bench.share_keys(impl, 4096, "c2"), 0, nmax)
     d_pk = torch.frombuffer(bytearray(b"".join(pks)), dtype=torch.uint8).to(dev)
     d_sig = torch.frombuffer(bytearray(b"".join(sigs)), dtype=torch.uint8).to(dev)
     d_msg = torch.frombuffer(bytearray(b"".join(roots)), dtype=torch.uint8).to(dev)
