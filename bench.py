@@ -31,12 +31,12 @@ METRIC = "verified BLS partial sigs/sec (node) + threshold aggregates/sec, 1/2/4
 # (one 381-bit Montgomery product, fp_mul or fp_sqr, = 12x12 CIOS = 300 32x32->64 multiply-adds).
 # Counted by the instrumented host build of the same kernels (tests/test_work_counts.py keeps
 # this in sync).  See DESIGN.md "Roofline".
-FPMUL_PER_VERIFY = 28880
+FPMUL_PER_VERIFY = 28076
 MADS_PER_FPMUL = 300
 # RLC BatchVerify stages (charon_amd/csrc/rlc.h), same unit and source (tests/test_work_counts.py):
 # stage 1 per item, stage 2 per distinct message, stage 3 per window of 8 with 2 messages (one per
 # 4-partial validator) or 1 message (committee root), stage 4 per item re-checked after a failed window.
-RLC_FPMUL = {"item": 5832, "hash": 6689, "window_2msg": 24842, "window_1msg": 19962, "fallback": 20004}
+RLC_FPMUL = {"item": 5832, "hash": 5740, "window_2msg": 24842, "window_1msg": 19962, "fallback": 20004}
 # gfx950 32x32->64 integer multiply-add peak (v_mad_u64_u32): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 # at half rate (measured: profiles/r01_mad_probe.txt) = 39.3e12 MAD/s.
 MAD_PEAK_T = 39.3

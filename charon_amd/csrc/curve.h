@@ -419,16 +419,15 @@ BLS_HD BLS_CALL void g2_mul_glv4(g2j& r, const g2j& p_in, const uint32_t* k_plai
   r = acc;
 }
 
-BLS_HD BLS_CALL bool fp2_sqrt(fp2& r, const fp2& a_in) {
+// Second half of fp2_sqrt: given s with s^2 = N(a) = a0^2 + a1^2 (either sign), r = a square root of a; returns
+// whether r^2 == a.  Split out so hash_to_g2 can share the norm's root between its two SSWU candidates.
+BLS_HD BLS_CALL bool fp2_sqrt_from_norm_root(fp2& r, const fp2& a_in, const fp& s_in) {
   const fp2 a = a_in;
-  // a = a0 + a1 u: s = sqrt(a0^2 + a1^2), t = (a0 + s)/2, then sqrt(a) = x0 + a1/(2 x0) u with
-  // x0^2 = t, or a1/(2 x0) + x0 u with x0^2 = -t when t is not a square.  One power
-  // z = t^((p-3)/4) gives both x0 = t z and 1/x0 = z (t square) or -z (t^((p-1)/2) = -1).
-  fp n, s, t, z, x0, inv_x0, t2;
-  fp_sqr(n, a.c0);
-  fp_sqr(t, a.c1);
-  fp_add(n, n, t);
-  fp_sqrt(s, n);  // candidate; correctness is checked at the end
+  const fp s = s_in;
+  // a = a0 + a1 u: t = (a0 + s)/2, then sqrt(a) = x0 + a1/(2 x0) u with x0^2 = t, or a1/(2 x0) + x0 u with
+  // x0^2 = -t when t is not a square.  One power z = t^((p-3)/4) gives both x0 = t z and 1/x0 = z (t square)
+  // or -z (t^((p-1)/2) = -1).
+  fp t, z, x0, inv_x0, t2;
   fp_add(t, a.c0, s);
   fp_mul(t, t, FP_HALF);
   if (fp_is_zero(t)) t = a.c0;  // a1 = 0 and s = -a0: use s = a0 instead
@@ -456,6 +455,16 @@ BLS_HD BLS_CALL bool fp2_sqrt(fp2& r, const fp2& a_in) {
   fp2_sqr(chk, cand);
   r = cand;
   return fp2_eq(chk, a);
+}
+
+BLS_HD BLS_CALL bool fp2_sqrt(fp2& r, const fp2& a_in) {
+  const fp2 a = a_in;
+  fp n, s, t;
+  fp_sqr(n, a.c0);
+  fp_sqr(t, a.c1);
+  fp_add(n, n, t);
+  fp_sqrt(s, n);  // candidate; correctness is checked at the end
+  return fp2_sqrt_from_norm_root(r, a, s);
 }
 
 BLS_HD BLS_CALL int g1_decompress(g1a& out, const uint8_t* b, bool subgroup_check) {

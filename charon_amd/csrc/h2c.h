@@ -244,24 +244,51 @@ BLS_HD BLS_CALL void map_to_curve_sswu_tv(g2a& out, const fp2& u_in, const fp2& 
     fp2_add(t, one, tv1);
     fp2_mul(x1, SSWU_NEG_B_OVER_A, t);
   }
-  // gx1 = x1^3 + A x1 + B
+  // gx1 = x1^3 + A x1 + B, and the second candidate x2 = Z u^2 x1, gx2 = x2^3 + A x2 + B
   fp2_sqr(gx1, x1);
   fp2_mul(gx1, gx1, x1);
   fp2_mul(t, SSWU_A, x1);
   fp2_add(gx1, gx1, t);
   fp2_add(gx1, gx1, SSWU_B);
-  if (fp2_sqrt(y, gx1)) {
+  fp2 x2, gx2;
+  fp2_mul(x2, zu2, x1);
+  fp2_sqr(gx2, x2);
+  fp2_mul(gx2, gx2, x2);
+  fp2_mul(t, SSWU_A, x2);
+  fp2_add(gx2, gx2, t);
+  fp2_add(gx2, gx2, SSWU_B);
+  // One exponentiation decides and roots both (RFC 9380 6.6.2 picks x1 iff gx1 is square; any root of the chosen
+  // g(x) serves, the sign is fixed below).  a in Fp2 is a square iff N(a) is a square in Fp (p = 3 mod 4), and
+  // s = N(gx1)^((p+1)/4) has s^2 = N(gx1) or -N(gx1).  When gx1 is not a square, tv1 != 0 (g(B/(ZA)) is square
+  // by the choice of Z), so gx2 = (Z u^2)^3 gx1 and N(gx2) = N(u)^6 (-N(Z)^3) (-N(gx1)) has the root
+  // N(u)^3 sqrt(-N(Z)^3) s.  The Fp2 root then costs one more exponentiation instead of two per candidate, and no
+  // lane of a wave waits on a second candidate's branch.
+  fp n1, s, s2, nu, q;
+  fp_sqr(n1, gx1.c0);
+  fp_sqr(q, gx1.c1);
+  fp_add(n1, n1, q);
+  fp_pow(s, n1, EXP_SQRT, 378);
+  fp_sqr(s2, s);
+  const bool gx1_square = fp_eq(s2, n1);
+  fp_sqr(nu, u.c0);
+  fp_sqr(q, u.c1);
+  fp_add(nu, nu, q);
+  fp_sqr(q, nu);
+  fp_mul(q, q, nu);
+  fp_mul(q, q, SSWU_SQRT_NEG_NZ3);
+  fp_mul(q, q, s);
+  fp2 w;
+  fp sw;
+  if (gx1_square) {
     x = x1;
+    w = gx1;
+    sw = s;
   } else {
-    fp2 gx2;
-    fp2_mul(x, zu2, x1);
-    fp2_sqr(gx2, x);
-    fp2_mul(gx2, gx2, x);
-    fp2_mul(t, SSWU_A, x);
-    fp2_add(gx2, gx2, t);
-    fp2_add(gx2, gx2, SSWU_B);
-    fp2_sqrt(y, gx2);
+    x = x2;
+    w = gx2;
+    sw = q;
   }
+  fp2_sqrt_from_norm_root(y, w, sw);
   if (fp2_sgn0(u) != fp2_sgn0(y)) fp2_neg(y, y);
   out.x = x;
   out.y = y;

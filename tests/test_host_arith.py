@@ -68,12 +68,25 @@ def test_expand_message(L):
 
 
 def test_map_to_curve(L):
+    """Both SSWU candidates (gx1 square / not: the shared-exponentiation path of h2c.h) and the exceptional
+    u = 0 (tv1 = 0, x1 = B/(ZA)), against the oracle's straight RFC 9380 map."""
     rng = random.Random(7)
     out = buf(192)
-    for _ in range(6):
-        u = (rng.randrange(P), rng.randrange(P))
+    branches = set()
+    for u in [(0, 0), (1, 0), (0, 1)] + [(rng.randrange(P), rng.randrange(P)) for _ in range(16)]:
         L.ht_map_to_curve(be48(u[0]) + be48(u[1]), out)
-        assert g2_from(out.raw) == bls.map_to_curve_sswu(u)
+        assert g2_from(out.raw) == bls.map_to_curve_sswu(u), u
+        # which candidate the RFC picks: x1 = -B/A (1 + 1/(Z^2 u^4 + Z u^2)) (or B/(ZA)), gx1 square?
+        zu2 = bls.f2_mul(bls.SSWU_Z, bls.f2_sqr(u))
+        den = bls.f2_add(bls.f2_sqr(zu2), zu2)
+        if bls.f2_is_zero(den):
+            x1 = bls.f2_mul(bls.SSWU_B, bls.f2_inv(bls.f2_mul(bls.SSWU_Z, bls.SSWU_A)))
+        else:
+            x1 = bls.f2_mul(bls.f2_mul(bls.f2_neg(bls.SSWU_B), bls.f2_inv(bls.SSWU_A)),
+                            bls.f2_add((1, 0), bls.f2_inv(den)))
+        gx1 = bls.f2_add(bls.f2_add(bls.f2_mul(bls.f2_sqr(x1), x1), bls.f2_mul(bls.SSWU_A, x1)), bls.SSWU_B)
+        branches.add(bls.f2_is_square(gx1))
+    assert branches == {True, False}
 
 
 def test_hash_to_g2(L):
