@@ -68,10 +68,10 @@ BLS_HD BLS_INLINE void jac_neg(jac<F>& r, const jac<F>& a) {
   r.z = a.z;
 }
 
-// dbl-2009-l (a = 0)
+// dbl-2009-l (a = 0).  The body is force-inlined into the scalar-multiplication loops (the accumulator then stays
+// in registers across doublings); jac_dbl is the called form for everything else.
 template <class F>
-BLS_HD BLS_CALL void jac_dbl(jac<F>& r, const jac<F>& p_in) {
-  const jac<F> p = p_in;
+BLS_HD BLS_INLINE void jac_dbl_body(jac<F>& r, const jac<F>& p) {
   F A, B, C, D, E, Fv, t;
   f_sqr(A, p.x);
   f_sqr(B, p.y);
@@ -97,6 +97,13 @@ BLS_HD BLS_CALL void jac_dbl(jac<F>& r, const jac<F>& p_in) {
   f_add(C, C, C);
   f_sub(r.y, t, C);
   r.x = x3;
+}
+template <class F>
+BLS_HD BLS_CALL void jac_dbl(jac<F>& r, const jac<F>& p_in) {
+  const jac<F> p = p_in;
+  jac<F> t;
+  jac_dbl_body(t, p);
+  r = t;
 }
 
 // add-2007-bl with the exceptional cases handled (P = Q doubles, P = -Q gives infinity)
@@ -208,12 +215,24 @@ BLS_HD BLS_CALL void jac_add_aff(jac<F>& r, const jac<F>& p_in, const aff<F>& q_
 // r = [k] p for a 64-bit scalar k (uniform across lanes when k is a constant)
 template <class F>
 BLS_HD BLS_CALL void jac_mul_u64(jac<F>& r, const jac<F>& p_in, uint64_t k) {
-  const jac<F> p = p_in;
+  // Left-to-right from the top set bit (k is wave-uniform).  The doubling is inlined and the accumulator's address
+  // is never taken, so it stays in registers; the base is read from the caller's frame by the few additions.
   jac<F> acc;
   jac_set_inf(acc);
-  for (int i = 63; i >= 0; --i) {
-    jac_dbl(acc, acc);
-    if ((k >> i) & 1ull) jac_add(acc, acc, p);
+  int i = 63;
+  while (i >= 0 && !((k >> i) & 1ull)) --i;
+  if (i >= 0) {
+    acc = p_in;
+    for (--i; i >= 0; --i) {
+      jac<F> t;
+      jac_dbl_body(t, acc);
+      acc = t;
+      if ((k >> i) & 1ull) {
+        jac<F> x = acc, y;
+        jac_add(y, x, p_in);
+        acc = y;
+      }
+    }
   }
   r = acc;
 }
@@ -221,12 +240,17 @@ BLS_HD BLS_CALL void jac_mul_u64(jac<F>& r, const jac<F>& p_in, uint64_t k) {
 // r = [k] p for a scalar given as nlimbs little-endian 32-bit limbs
 template <class F>
 BLS_HD BLS_CALL void jac_mul_limbs(jac<F>& r, const jac<F>& p_in, const uint32_t* k, int nlimbs) {
-  const jac<F> p = p_in;
-  jac<F> acc;
+  jac<F> acc;  // register-resident accumulator, inlined doubling (see jac_mul_u64)
   jac_set_inf(acc);
   for (int i = nlimbs * 32 - 1; i >= 0; --i) {
-    jac_dbl(acc, acc);
-    if ((k[i >> 5] >> (i & 31)) & 1u) jac_add(acc, acc, p);
+    jac<F> t;
+    jac_dbl_body(t, acc);
+    acc = t;
+    if ((k[i >> 5] >> (i & 31)) & 1u) {
+      jac<F> x = acc, y;
+      jac_add(y, x, p_in);
+      acc = y;
+    }
   }
   r = acc;
 }
@@ -411,10 +435,16 @@ BLS_HD BLS_CALL void g2_mul_glv4(g2j& r, const g2j& p_in, const uint32_t* k_plai
   g2j acc;
   jac_set_inf(acc);
   for (int bit = 63; bit >= 0; --bit) {
-    jac_dbl(acc, acc);
+    g2j t;
+    jac_dbl_body(t, acc);  // inlined; acc's address is never taken (it stays in registers)
+    acc = t;
     const int d = (int)((e[0] >> bit) & 1u) | (int)(((e[1] >> bit) & 1u) << 1) |
                   (int)(((e[2] >> bit) & 1u) << 2) | (int)(((e[3] >> bit) & 1u) << 3);
-    if (d) jac_add(acc, acc, tab[d]);
+    if (d) {
+      g2j x = acc, y;
+      jac_add(y, x, tab[d]);
+      acc = y;
+    }
   }
   r = acc;
 }

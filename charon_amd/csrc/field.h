@@ -363,10 +363,26 @@ BLS_HD BLS_CALL void fp_pow(fp& r, const fp& a, const uint32_t* e, int top_bit) 
       v = (v << 1) | bit(k);
       if (started) fp_sqr(acc, acc);
     }
+    // the table index is wave-uniform: select through a switch of constant indices so the table stays in
+    // registers (a dynamic index would put it in scratch and cost a memory round trip per window)
+    fp w;
+    switch (v >> 1) {
+#define BLS_POW_CASE(k) \
+  case k:               \
+    w = tbl[k];         \
+    break;
+      BLS_POW_CASE(0) BLS_POW_CASE(1) BLS_POW_CASE(2) BLS_POW_CASE(3) BLS_POW_CASE(4) BLS_POW_CASE(5)
+      BLS_POW_CASE(6) BLS_POW_CASE(7) BLS_POW_CASE(8) BLS_POW_CASE(9) BLS_POW_CASE(10) BLS_POW_CASE(11)
+      BLS_POW_CASE(12) BLS_POW_CASE(13) BLS_POW_CASE(14)
+#undef BLS_POW_CASE
+      default:
+        w = tbl[15];
+        break;
+    }
     if (started) {
-      fp_mul(acc, acc, tbl[v >> 1]);
+      fp_mul(acc, acc, w);
     } else {
-      acc = tbl[v >> 1];
+      acc = w;
       started = true;
     }
     i = j - 1;

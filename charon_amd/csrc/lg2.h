@@ -176,13 +176,16 @@ __device__ __forceinline__ void fp12h_gather(fp12& full, const fp6& h, uint32_t 
 
 // r = a^|x| for a in the cyclotomic subgroup (split)
 BLS_CALL __device__ void fp12h_exp_xabs(fp6& r, const fp6& a_in, uint32_t m) {
-  const fp6 a = a_in;
-  fp6 acc = a;
+  fp6 acc = a_in;  // the base stays in the caller's frame (see fp12_cyc_exp_xabs)
   for (int bit = 62; bit >= 0; --bit) {
     fp6 t;
     fp12h_cyc_sqr(t, acc, m);
     acc = t;
-    if ((X_ABS >> bit) & 1ull) fp12h_mul(acc, acc, a, m);
+    if ((X_ABS >> bit) & 1ull) {  // through temporaries: acc's address is never taken
+      fp6 x = acc, y;
+      fp12h_mul(y, x, a_in, m);
+      acc = y;
+    }
   }
   r = acc;
 }

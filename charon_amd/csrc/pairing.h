@@ -148,14 +148,20 @@ BLS_HD BLS_CALL void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bo
 }
 
 // r = a^|x| for a in the cyclotomic subgroup
+// The base is NOT copied in: it is needed only by the 5 multiplications, so it stays in the caller's frame and
+// fp12_mul reads it there, leaving the register file to the squaring chain (a register copy of it spilled
+// inside the loop).  Likewise the accumulator's address is never taken, so it is not pinned to the stack.
 BLS_HD BLS_CALL void fp12_cyc_exp_xabs(fp12& r, const fp12& a_in) {
-  const fp12 a = a_in;
-  fp12 acc = a;
+  fp12 acc = a_in;
   for (int bit = 62; bit >= 0; --bit) {
     fp12 t;
     fp12_cyclotomic_sqr_body(t, acc);  // inlined: acc stays in registers between squarings
     acc = t;
-    if ((X_ABS >> bit) & 1ull) fp12_mul(acc, acc, a);
+    if ((X_ABS >> bit) & 1ull) {  // through temporaries: taking acc's address would pin it to the stack
+      fp12 x = acc, y;
+      fp12_mul(y, x, a_in);
+      acc = y;
+    }
   }
   r = acc;
 }

@@ -64,10 +64,16 @@ BLS_HD BLS_CALL void jac_mul2_u32(jac<F>& r, const jac<F>& P_in, const jac<F>& Q
   jac_add(PQ, P, Q);
   jac_set_inf(acc);
   for (int bit = 31; bit >= 0; --bit) {
-    jac_dbl(acc, acc);
+    jac<F> t;
+    jac_dbl_body(t, acc);  // inlined doubling; acc's address is never taken, so it stays in registers
+    acc = t;
     const uint32_t d = ((a >> bit) & 1u) | (((b >> bit) & 1u) << 1);
     addend = d == 1 ? P : (d == 2 ? Q : PQ);
-    if (d) jac_add(acc, acc, addend);
+    if (d) {
+      jac<F> x = acc, y;
+      jac_add(y, x, addend);
+      acc = y;
+    }
   }
   r = acc;
 }

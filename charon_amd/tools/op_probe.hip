@@ -68,6 +68,49 @@ __global__ void __launch_bounds__(64) k_op(const uint32_t* in, uint32_t* out, ui
       f.c0.c0 = a.x;
       f.c0.c1.c0.v[0] ^= (uint32_t)st;
     }
+    if (K == 21) {
+      uint8_t b[96];
+      b[0] = 0xa0;
+      for (int k = 1; k < 96; ++k) b[k] = (uint8_t)(f.c0.c0.c0.v[k % 12] >> (k & 24));
+      g2a a;
+      const int st = g2_decompress(a, b, false);
+      f.c0.c0 = a.x;
+      f.c0.c1.c0.v[0] ^= (uint32_t)st;
+    }
+    if (K == 22) {
+      g2j pj;
+      pj.x = T.x;
+      pj.y = T.y;
+      fp2_set_one(pj.z);
+      f.c0.c1.c0.v[1] ^= g2_in_subgroup(pj) ? 1u : 0u;
+      T.x = T.y;
+    }
+    if (K == 16) fp_pow(f.c0.c0.c0, f.c0.c0.c0, EXP_SQRT, 378);
+    if (K == 18) {
+      fp2 y;
+      const bool ok = fp2_sqrt(y, f.c0.c0);
+      f.c0.c0 = y;
+      f.c0.c1.c0.v[0] ^= ok ? 1u : 0u;
+    }
+    if (K == 19) f.c0.c1.c0.v[1] ^= g2_in_subgroup(T) ? 1u : 0u;
+    if (K == 20) {
+      g1j q, p1;
+      p1.x = P.x;
+      p1.y = P.y;
+      fp_set_one(p1.z);
+      jac_mul_u64(q, p1, X_ABS);
+      P.x = q.x;
+      P.y = q.y;
+    }
+    if (K == 17) {
+      g1a a;
+      uint8_t b[48];
+      b[0] = 0x80 | (uint8_t)(f.c0.c0.c0.v[0] & 0x1f);
+      for (int k = 1; k < 48; ++k) b[k] = (uint8_t)(f.c0.c0.c1.v[k % 12] >> (k & 24));
+      const int st = g1_decompress(a, b, true);
+      f.c0.c0.c0 = a.x;
+      f.c0.c1.c0.v[0] ^= (uint32_t)st;
+    }
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   uint32_t acc = 0;
@@ -88,13 +131,14 @@ static double median(uint64_t* h, int n) {
 }
 
 int main() {
-  const char* names[16] = {"fp_mul", "fp_add", "fp2_mul", "fp6_mul", "fp12_sqr", "fp12_mul", "fp12_mul_line2",
+  constexpr int NOPS = 23;
+  const char* names[NOPS] = {"fp_mul", "fp_add", "fp2_mul", "fp6_mul", "fp12_sqr", "fp12_mul", "fp12_mul_line2",
                            "fp12_cyclotomic_sqr", "miller_dbl_step", "jac_dbl<fp2>", "fp_sub",
                            "final_exponentiation", "fp12_cyc_exp_xabs", "miller_loop_n(2)", "hash_to_g2",
-                           "g2_decompress+subgroup"};
+                           "g2_decompress+subgroup", "fp_pow(sqrt)", "g1_decompress+subgroup", "fp2_sqrt", "g2_in_subgroup", "jac_mul_u64<fp>(|x|)", "g2_decompress(no sub)", "g2_in_subgroup(z=1)"};
   // Fp products per op (host instrumented build: tests/test_work_counts.py); 0 = not a product count
-  const int products[16] = {1, 0, 3, 18, 36, 54, 69, 18, 25, 16, 0, 8150, 1404, 10700, 5740, 2203};
-  const int iters[16] = {400, 400, 200, 40, 20, 20, 20, 40, 40, 40, 400, 1, 2, 1, 2, 4};
+  const int products[NOPS] = {1, 0, 3, 18, 36, 54, 69, 18, 25, 16, 0, 8150, 1404, 10700, 5740, 2203, 458, 0, 0, 0, 0, 0, 0};
+  const int iters[NOPS] = {400, 400, 200, 40, 20, 20, 20, 40, 40, 40, 400, 1, 2, 1, 2, 4, 4, 4, 4, 4, 4, 4, 4};
   uint32_t *d_in, *d_out;
   uint64_t* d_cyc;
   uint32_t h_in[4096];
@@ -103,11 +147,11 @@ int main() {
   (void)hipMemcpy(d_in, h_in, sizeof(h_in), hipMemcpyHostToDevice);
   uint64_t h_cyc[1024];
   double per_product = 0;
-  for (int k = 0; k < 16; ++k) {
+  for (int k = 0; k < NOPS; ++k) {
     for (int rep = 0; rep < 2; ++rep) {
       switch (k) {
 #define L(K) case K: hipLaunchKernelGGL(k_op<K>, dim3(1024), dim3(64), 0, 0, d_in, d_out, d_cyc, iters[K]); break;
-        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15)
+        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15) L(16) L(17) L(18) L(19) L(20) L(21) L(22)
       }
       if (hipDeviceSynchronize() != hipSuccess) return 2;
     }
