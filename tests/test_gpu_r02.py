@@ -295,7 +295,7 @@ def test_queue_async_in_flight_throughput(impl):
     assert got == want
     rate = n / dt
     print("\nqueue: %d n=1 Verify calls from 64 threads in %.3f s = %.0f Verify/s, %d batches" % (n, dt, rate, b1 - b0))
-    assert rate > 20000
+    assert rate > 40000  # measured 50.7k/s on MI355X
 
 
 # ---------------------------------------------------------------- cross-stream workspace ordering
