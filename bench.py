@@ -37,6 +37,10 @@ MADS_PER_FPMUL = 300
 # stage 1 per item, stage 2 per distinct message, stage 3 per window of 8 with 2 messages (one per
 # 4-partial validator) or 1 message (committee root), stage 4 per item re-checked after a failed window.
 RLC_FPMUL = {"item": 5832, "hash": 5740, "window_2msg": 24842, "window_1msg": 19962, "fallback": 20004}
+# Batch-wide check (charon_amd/csrc/rlcb.h), same unit and source: stage 1 per item, the Pippenger MSM per item
+# (2 points x 2 windows of mixed additions; the bucket/segment folds add ~15 per item at 1M items and are left
+# out), and one multi-Miller loop per 16-item chunk with 4 message runs (one root per 4-partial validator).
+RLCB_FPMUL = {"item": 4306, "msm_per_item": 116, "chunk_4runs": 20784}
 # gfx950 32x32->64 integer multiply-add peak (v_mad_u64_u32): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 # at half rate (measured: profiles/r01_mad_probe.txt) = 39.3e12 MAD/s.
 MAD_PEAK_T = 39.3
@@ -149,13 +153,13 @@ def make_c3(impl, g_lo, g_hi, t=7, n=10):
     return psigs, part_ids, offs, dv_pks, roots
 
 
-def c4_item(tag, v, j, nk):
-    """(owner key, bad?, kind) of partial j of validator v."""
+def c4_item(tag, v, j, nk, corrupt=True):
+    """(owner key, bad?, kind) of partial j of validator v; corrupt=False: an all-valid node batch."""
     r = _hi(tag, v, j)
-    return r % nk, (r >> 20) % 100 == 0, (r >> 40) & 1
+    return r % nk, corrupt and (r >> 20) % 100 == 0, (r >> 40) & 1
 
 
-def make_c4(impl, keys, tag, v_lo, v_hi, v_node, n_roots_node=0, shares=4):
+def make_c4(impl, keys, tag, v_lo, v_hi, v_node, n_roots_node=0, shares=4, corrupt=True):
     """Validators [v_lo, v_hi) of a C4 node batch of v_node validators x `shares` partials, items grouped by
     validator.  One root per validator (n_roots_node = 0, variant i) or n_roots_node committee roots over the node
     batch, contiguous committees (variant ii).  ~1% corrupted (swapped share / flipped signature bit)."""
@@ -170,7 +174,7 @@ def make_c4(impl, keys, tag, v_lo, v_hi, v_node, n_roots_node=0, shares=4):
     owner, midx, bad, kinds = [], [], set(), {}
     for dv, v in enumerate(range(v_lo, v_hi)):
         for j in range(shares):
-            o, is_bad, kind = c4_item(tag, v, j, nk)
+            o, is_bad, kind = c4_item(tag, v, j, nk, corrupt)
             if is_bad:
                 bad.add(len(owner))
                 kinds[len(owner)] = kind
@@ -189,8 +193,8 @@ def make_c4(impl, keys, tag, v_lo, v_hi, v_node, n_roots_node=0, shares=4):
     return pk_list, sigs, midx, roots, bad
 
 
-def c4_node_bad(tag, v_node, nk, shares=4):
-    return {v * shares + j for v in range(v_node) for j in range(shares) if c4_item(tag, v, j, nk)[1]}
+def c4_node_bad(tag, v_node, nk, shares=4, corrupt=True):
+    return {v * shares + j for v in range(v_node) for j in range(shares) if c4_item(tag, v, j, nk, corrupt)[1]}
 
 
 def pmc_summary(path=os.path.join(ROOT, "profiles", "r02_pmc_verify.json")):
@@ -346,7 +350,7 @@ def main():
             dist.init_process_group(backend=backend)
 
     from charon_amd.shard import gather_aggregates, gather_bitmap_rows, gather_node_bitmap, shard_range, unpack_bitmap
-    from charon_amd.tbls import HipBLS, load_library
+    from charon_amd.tbls import RLC_AUTO, RLC_BATCH, RLC_WINDOWS, HipBLS, load_library
     impl = HipBLS(device=local_dev)
     lib = load_library()
     lib.hipbls_set_timing(1)  # per-kernel HIP events for the roofline (off by default in the library)
@@ -464,10 +468,14 @@ def main():
         V = args.rlc_node_validators
         v_lo, v_hi = shard_range(V, rank, world)
         keys4 = share_keys(impl, 4096, "c4")
-        for variant, tag, n_roots in (("i_root_per_validator", "c4i", 0),
-                                      ("ii_committee_roots", "c4ii", max(1, V // 128))):
+        for variant, tag, n_roots, corrupt in (("i_root_per_validator", "c4i", 0, True),
+                                               ("ii_committee_roots", "c4ii", max(1, V // 128), True),
+                                               ("i_all_valid", "c4h", 0, False)):
+            # the mode HIPBLS_RLC_AUTO settles on for each stream: windows while invalid partials keep arriving
+            # (its batch-wide check keeps failing), the batch-wide check for an all-valid stream
+            impl.set_rlc_mode(RLC_BATCH if not corrupt else RLC_WINDOWS)
             t0 = time.time()
-            pks4, sigs4, midx4, roots4, bad4 = make_c4(impl, keys4, tag, v_lo, v_hi, V, n_roots)
+            pks4, sigs4, midx4, roots4, bad4 = make_c4(impl, keys4, tag, v_lo, v_hi, V, n_roots, corrupt=corrupt)
             n4 = len(pks4)
             log("rank %d: C4(%s) validators [%d, %d) of %d: %d items, %d roots in %.1fs"
                 % (rank, variant, v_lo, v_hi, V, n4, len(roots4), time.time() - t0))
@@ -490,12 +498,14 @@ def main():
             rstep()
             torch.cuda.synchronize(dev)
             lib.hipbls_kernel_timing_reset()
+            b_att0, b_pass0, _ = impl.rlc_batch_stats()
             tel = timed_loop(rstep, args.rlc_steps, dev, barrier, world)
+            b_att1, b_pass1, _ = impl.rlc_batch_stats()
             st4 = d_st4.cpu().tolist()
             assert {i for i, x in enumerate(st4) if x != 0} == bad4, "RLC bitmap mismatch"
             if world > 1:
                 got = node4[0].cpu()
-                want = c4_node_bad(tag, V, len(keys4[0]))
+                want = c4_node_bad(tag, V, len(keys4[0]), corrupt=corrupt)
                 assert {i for i in range(4 * V) if not got[i]} == want, "gathered RLC node bitmap mismatch"
             w = ctypes.c_uint64()
             wf = ctypes.c_uint64()
@@ -504,6 +514,9 @@ def main():
             per_win = RLC_FPMUL["window_1msg"] if n_roots else RLC_FPMUL["window_2msg"]
             fpmul = (RLC_FPMUL["item"] * n4 + RLC_FPMUL["hash"] * len(roots4) + per_win * w.value
                      + RLC_FPMUL["fallback"] * fb.value)
+            if b_pass1 > b_pass0:  # the batch-wide check decided alone: no window pairing work
+                fpmul = ((RLCB_FPMUL["item"] + RLCB_FPMUL["msm_per_item"]) * n4 + RLC_FPMUL["hash"] * len(roots4)
+                         + RLCB_FPMUL["chunk_4runs"] * ((n4 + 15) // 16))
             ach = fpmul * MADS_PER_FPMUL * args.rlc_steps / tel / 1e12
             rlc[variant] = {"verified_partial_sigs_per_s": round(4 * V * args.rlc_steps / tel, 1),
                             "node_items": 4 * V, "items_this_gpu": n4, "distinct_roots_this_gpu": len(roots4),
@@ -513,9 +526,12 @@ def main():
                                                   "note": "rank 0's 4-stage pipeline over wall time (not one kernel)"},
                             "ms_per_batch": round(1000 * tel / args.rlc_steps, 3),
                             "windows": w.value, "windows_failed": wf.value, "items_fallback": fb.value,
+                            "batch_checks": {"attempted": b_att1 - b_att0, "passed": b_pass1 - b_pass0},
                             "kernel_avg_ms": kernel_ms(lib, ("rlc_items", "rlc_hash", "rlc_window", "rlc_window_lg2",
-                                                             "rlc_fallback", "rlc_fallback_lg2"))}
-            if args.keys and variant == "i_root_per_validator":
+                                                             "rlc_fallback", "rlc_fallback_lg2", "rlcb_items",
+                                                             "rlcb_msm", "rlcb_chunks", "rlcb_product", "rlcb_final",
+                                                             "rlcb_mark"))}
+            if args.keys and variant in ("i_root_per_validator", "i_all_valid"):
                 table4 = list(dict.fromkeys(pks4))
                 pos4 = {k: j for j, k in enumerate(table4)}
                 assert set(impl.load_pubshares(table4)) <= {0}
@@ -535,6 +551,7 @@ def main():
             if variant == "i_root_per_validator":
                 c4i = (pks4, sigs4, midx4, roots4, bad4)
             del d_pk4, d_sig4, d_midx4, d_msg4, d_off4, d_st4
+        impl.set_rlc_mode(RLC_AUTO)
 
     # ---- C5: full-slot mix on this rank's slice: RLC over the C4(i) slice + its slice of 32 validators x 4 proposer
     # partials (own roots), with the 512-key sync-committee FastAggregateVerify (hash-to-G2 of its root) overlapped on
@@ -640,8 +657,10 @@ def main():
         if rlc:
             out["rlc_batch_verify"] = dict(rlc, workload="C4 (BASELINE configs[3]): the %d-validator x 4-partial node "
                                                         "batch sliced over %d GPU(s) by validator index (strong "
-                                                        "scaling), items grouped by validator, ~1%% corrupted, windows "
-                                                        "of 8 items, per-item bitmap == tbls.Verify, node bitmap "
+                                                        "scaling), items grouped by validator, ~1%% corrupted (i, ii) "
+                                                        "or all valid (i_all_valid: decided by the batch-wide "
+                                                        "Pippenger check of rlcb.h alone), windows of 8 items for the "
+                                                        "rest, per-item bitmap == tbls.Verify, node bitmap "
                                                         "all-gathered" % (args.rlc_node_validators, world))
         k_ms = avg_ms.value
         if k_ms > 0:

@@ -92,6 +92,14 @@ struct Context {
   hipEvent_t ev_fork = nullptr, ev_hash = nullptr, ev_join[kSub] = {};
   hipEvent_t ws_done = nullptr;  // last workspace user's completion (cross-stream ordering)
   uint64_t r_windows = 0;        // window count of the last RLC call (hipbls_rlc_stats)
+  // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
+  DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_FS, m_flag;
+  int32_t* rlcb_host_flag = nullptr;  // pinned copy of the last verdict
+  hipEvent_t rlcb_ev = nullptr, rlcb_ev_items = nullptr, rlcb_ev_msm = nullptr;
+  bool rlcb_pending = false;          // a verdict copy is in flight
+  int rlcb_last = -1;                 // last verdict read back: -1 none, 0 failed, 1 passed
+  int rlcb_skipped = 0;               // AUTO: calls run windows-only since the last failed batch check
+  uint64_t rlcb_attempted = 0, rlcb_passed = 0;
   HCache hcache;
   std::mutex tmu;                            // timing table (also used by the queue worker)
   std::map<std::string, TimingSlot> timing;  // per kernel name: HIP events on the launch stream
@@ -251,6 +259,12 @@ int launch_verify(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d
   });
 }
 
+bool use_rlc_batch(uint64_t n);
+int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n,
+                     const uint8_t* d_msgs, const uint64_t* d_offs, uint64_t n_msgs, const rlc_seed& seed,
+                     int32_t* d_status, hipStream_t s, const uint32_t* d_kidx, uint32_t* d_H, uint64_t hstride,
+                     const uint32_t* d_hslot, const uint32_t* d_mlist, uint64_t n_hash);
+
 int ensure_rlc_streams() {
   Context& c = g_ctx;
   if (c.ev_fork) return HIPBLS_OK;
@@ -300,6 +314,9 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
   HIP_TRY(c.r_win.ensure(n_win * 4));
   HIP_TRY(c.r_list.ensure(n * 4));
   HIP_TRY(c.r_cnt.ensure(Context::kSub * 4));
+  if (use_rlc_batch(n))
+    return launch_rlc_batch(d_pks, d_sigs, d_midx, n, d_msgs, d_offs, n_msgs, seed, d_status, s, d_kidx, d_H, hstride,
+                            d_hslot, d_mlist, n_hash);
   uint32_t* rpk = (uint32_t*)c.r_pk.p;
   uint32_t* rsig = (uint32_t*)c.r_sig.p;
   int32_t* win = (int32_t*)c.r_win.p;
@@ -367,6 +384,202 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
     HIP_TRY(hipEventRecord(c.ev_join[k], ss));
     HIP_TRY(hipStreamWaitEvent(s, c.ev_join[k], 0));
   }
+  c.r_windows = n_win;
+  return ws_end(s);
+}
+
+// ============================================================================ batch-wide RLC check (rlcb.h)
+// Policy (hipbls_rlc_set_mode): WINDOWS = rlc.h only; BATCH = the batch-wide check first, windows for whatever it
+// leaves pending; AUTO (default) = BATCH for batches of >= 1,024 items unless the last batch check failed, in
+// which case the next 8 calls run windows only (a cluster that sends invalid partials keeps sending them; one
+// whose batches pass keeps the cheap path).  The verdict comes back asynchronously (pinned copy + event), so the
+// policy never blocks a launch.
+std::atomic<int> g_rlc_mode{HIPBLS_RLC_AUTO};
+constexpr uint64_t kRlcbMinItems = 1024;
+constexpr int kRlcbBackoff = 8;
+
+void rlcb_poll(bool wait) {
+  Context& c = g_ctx;
+  if (!c.rlcb_pending) return;
+  if (wait) {
+    if (hipEventSynchronize(c.rlcb_ev) != hipSuccess) return;
+  } else if (hipEventQuery(c.rlcb_ev) != hipSuccess) {
+    return;
+  }
+  c.rlcb_pending = false;
+  c.rlcb_last = *c.rlcb_host_flag ? 1 : 0;
+  c.rlcb_passed += (uint64_t)c.rlcb_last;
+  if (!c.rlcb_last) c.rlcb_skipped = 0;
+}
+
+bool use_rlc_batch(uint64_t n) {
+  Context& c = g_ctx;
+  const int mode = g_rlc_mode.load();
+  if (mode == HIPBLS_RLC_WINDOWS) return false;
+  if (mode == HIPBLS_RLC_BATCH) return true;
+  rlcb_poll(false);
+  if (n < kRlcbMinItems) return false;
+  if (c.rlcb_last == 0 && c.rlcb_skipped < kRlcbBackoff) {
+    ++c.rlcb_skipped;
+    return false;
+  }
+  return true;
+}
+
+// Stages 1-6 of rlcb.h on stream s, then the window/fallback stages of rlc.h for the items still pending (none
+// when the batch check passed: those kernels then find nothing to do).  Shares launch_rlc's H(m) table setup.
+int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n,
+                     const uint8_t* d_msgs, const uint64_t* d_offs, uint64_t n_msgs, const rlc_seed& seed,
+                     int32_t* d_status, hipStream_t s, const uint32_t* d_kidx, uint32_t* d_H, uint64_t hstride,
+                     const uint32_t* d_hslot, const uint32_t* d_mlist, uint64_t n_hash) {
+  Context& c = g_ctx;
+  const uint64_t T = c.t_size;
+  const int32_t* tcode = (const int32_t*)c.t_code.p;
+  const uint32_t* tab = (const uint32_t*)c.t_tab.p;
+  const uint64_t npts = 2 * n;
+  const uint64_t nch = (n + RLCB_C - 1) / RLCB_C;
+  const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
+  if (!c.rlcb_host_flag) {
+    HIP_TRY(hipHostMalloc((void**)&c.rlcb_host_flag, sizeof(int32_t), hipHostMallocDefault));
+    HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_items, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_msm, hipEventDisableTiming));
+  }
+  int rc = ensure_rlc_streams();
+  if (rc) return rc;
+  rlcb_poll(true);  // the pinned flag is about to be overwritten
+  HIP_TRY(c.m_pts.ensure(npts * 48 * 4));
+  HIP_TRY(c.m_sc.ensure(npts * 4));
+  HIP_TRY(c.m_cnt.ensure((uint64_t)MSM_WINDOWS * MSM_NB * 4));
+  HIP_TRY(c.m_off.ensure((uint64_t)MSM_WINDOWS * (MSM_NB + 1) * 4));
+  HIP_TRY(c.m_cur.ensure((uint64_t)MSM_WINDOWS * MSM_NB * 4));
+  HIP_TRY(c.m_list.ensure((uint64_t)MSM_WINDOWS * npts * 4));
+  HIP_TRY(c.m_B.ensure((uint64_t)MSM_WINDOWS * MSM_NB * 72 * 4));
+  HIP_TRY(c.m_Sg.ensure((uint64_t)MSM_WINDOWS * MSM_NSEG * 72 * 4));
+  HIP_TRY(c.m_W.ensure((uint64_t)MSM_WINDOWS * 72 * 4));
+  HIP_TRY(c.m_F.ensure(nch * 144 * 4));
+  HIP_TRY(c.m_F2.ensure(((nch + 15) / 16) * 144 * 4));
+  HIP_TRY(c.m_FS.ensure(144 * 4));
+  HIP_TRY(c.m_flag.ensure(4));
+  uint32_t* rpk = (uint32_t*)c.r_pk.p;
+  uint32_t* rsig = (uint32_t*)c.r_sig.p;
+  uint32_t* pts = (uint32_t*)c.m_pts.p;
+  uint32_t* sc = (uint32_t*)c.m_sc.p;
+  int32_t* flag = (int32_t*)c.m_flag.p;
+  // Streams: the caller's stream s hashes the messages; sub[0] runs items -> MSM -> the (-g1, S) Miller value;
+  // sub[1] runs the chunk Miller loops and their product once the items and the hash are done; s joins both for
+  // the verdict and the window stages.
+  hipStream_t s0 = c.sub[0], s1 = c.sub[1];
+  rc = ws_begin(s);
+  if (rc) return rc;
+  HIP_TRY(hipMemsetAsync(c.m_cnt.p, 0, (size_t)MSM_WINDOWS * MSM_NB * 4, s));
+  HIP_TRY(hipMemsetAsync(c.r_cnt.p, 0, 4, s));
+  HIP_TRY(hipEventRecord(c.ev_fork, s));
+  if (n_hash) {
+    rc = timed("rlc_hash", s, [&] {
+      hipLaunchKernelGGL(k_rlc_hash, dim3((unsigned)grid_for(n_hash)), dim3(kBlock), 0, s, d_msgs, d_offs, n_hash,
+                         d_mlist, d_H, hstride, d_hslot);
+    });
+    if (rc) return rc;
+  }
+  HIP_TRY(hipEventRecord(c.ev_hash, s));
+  HIP_TRY(hipStreamWaitEvent(s0, c.ev_fork, 0));
+  rc = timed("rlcb_items", s0, [&] {
+    hipLaunchKernelGGL(k_rlcb_items, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s0, n, d_pks, d_sigs, d_midx, n_msgs,
+                       seed, rpk, pts, sc, d_status, d_kidx, T, tcode, tab);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c.rlcb_ev_items, s0));
+  rc = timed("rlcb_msm", s0, [&] {
+    hipStream_t s = s0;
+    const unsigned g256 = (unsigned)((npts + 255) / 256);
+    hipLaunchKernelGGL(k_msm_hist, dim3(g256), dim3(256), 0, s, npts, (const uint32_t*)sc, (uint32_t*)c.m_cnt.p);
+    hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(kScanThreads), 0, s, (const uint32_t*)c.m_cnt.p, (uint32_t*)c.m_off.p,
+                       (uint32_t*)c.m_cur.p);
+    hipLaunchKernelGGL(k_msm_scatter, dim3(g256), dim3(256), 0, s, npts, (const uint32_t*)sc, (uint32_t*)c.m_cur.p,
+                       (uint32_t*)c.m_list.p);
+    hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)grid_for((uint64_t)MSM_WINDOWS * MSM_NB)), dim3(kBlock), 0, s,
+                       (const uint32_t*)c.m_off.p, (const uint32_t*)c.m_list.p, npts, (const uint32_t*)pts,
+                       (uint32_t*)c.m_B.p);
+    hipLaunchKernelGGL(k_msm_segment, dim3((unsigned)grid_for((uint64_t)MSM_WINDOWS * MSM_NSEG)), dim3(kBlock), 0, s,
+                       (const uint32_t*)c.m_B.p, (uint32_t*)c.m_Sg.p);
+    hipLaunchKernelGGL(k_msm_window, dim3(MSM_WINDOWS), dim3(kSumBlock), 0, s, (const uint32_t*)c.m_Sg.p,
+                       (uint32_t*)c.m_W.p);
+  });
+  if (rc) return rc;
+  rc = timed("rlcb_sfactor", s0, [&] {
+    hipLaunchKernelGGL(k_rlcb_sfactor, dim3(1), dim3(kBlock), 0, s0, (const uint32_t*)c.m_W.p, (uint32_t*)c.m_FS.p);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c.rlcb_ev_msm, s0));
+  HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_items, 0));
+  HIP_TRY(hipStreamWaitEvent(s1, c.ev_hash, 0));
+  rc = timed("rlcb_chunks", s1, [&] {
+    hipLaunchKernelGGL(k_rlcb_chunks, dim3((unsigned)grid_for(nch)), dim3(kBlock), 0, s1, n, (const int32_t*)d_status,
+                       d_midx, (const uint32_t*)rpk, (const uint32_t*)d_H, hstride, d_hslot, (uint32_t*)c.m_F.p, nch);
+  });
+  if (rc) return rc;
+  uint32_t* src = (uint32_t*)c.m_F.p;
+  uint32_t* dst = (uint32_t*)c.m_F2.p;
+  uint64_t cur = nch;
+  rc = timed("rlcb_product", s1, [&] {
+    while (cur > 1) {
+      const uint64_t nxt = (cur + 15) / 16;
+      hipLaunchKernelGGL(k_fp12_prod, dim3((unsigned)grid_for(nxt)), dim3(kBlock), 0, s1, (const uint32_t*)src, cur,
+                         dst, nxt, 16);
+      uint32_t* t = src;
+      src = dst;
+      dst = t;
+      cur = nxt;
+    }
+  });
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c.ev_join[1], s1));
+  HIP_TRY(hipStreamWaitEvent(s, c.rlcb_ev_msm, 0));
+  HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
+  rc = timed("rlcb_final", s, [&] {
+    hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, (const uint32_t*)c.m_FS.p, flag);
+  });
+  if (rc) return rc;
+  rc = timed("rlcb_mark", s, [&] {
+    hipLaunchKernelGGL(k_rlcb_mark, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, n, (const int32_t*)flag, d_status,
+                       (const uint32_t*)pts, (const uint32_t*)sc, rsig);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c.rlcb_host_flag, flag, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(c.rlcb_ev, s));
+  c.rlcb_pending = true;
+  c.rlcb_attempted += 1;
+  // window + fallback stages over whatever is still pending (nothing when the batch check passed)
+  int32_t* win = (int32_t*)c.r_win.p;
+  uint32_t* list = (uint32_t*)c.r_list.p;
+  uint32_t* cnt = (uint32_t*)c.r_cnt.p;
+  if (use_pairs(n_win, kLg2MaxWindows))
+    rc = timed("rlc_window_lg2", s, [&] {
+      hipLaunchKernelGGL(k_rlc_window_lg2, dim3((unsigned)grid_for(2 * n_win)), dim3(kBlock), 0, s, (uint64_t)0, n_win,
+                         n, d_midx, (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
+                         d_status, win, list, cnt);
+    });
+  else
+    rc = timed("rlc_window", s, [&] {
+      hipLaunchKernelGGL(k_rlc_window, dim3((unsigned)grid_for(n_win)), dim3(kBlock), 0, s, (uint64_t)0, n_win, n,
+                         d_midx, (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
+                         d_status, win, list, cnt);
+    });
+  if (rc) return rc;
+  if (g_pair_mode.load() != HIPBLS_PAIR_SINGLE)
+    rc = timed("rlc_fallback_lg2", s, [&] {
+      hipLaunchKernelGGL(k_rlc_fallback_lg2, dim3((unsigned)grid_for(2 * n)), dim3(kBlock), 0, s,
+                         (const uint32_t*)list, (const uint32_t*)cnt, n, d_pks, d_sigs, d_midx, (const uint32_t*)d_H,
+                         hstride, d_hslot, d_status, d_kidx, T, tab);
+    });
+  else
+    rc = timed("rlc_fallback", s, [&] {
+      hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, (const uint32_t*)list,
+                         (const uint32_t*)cnt, n, d_pks, d_sigs, d_midx, (const uint32_t*)d_H, hstride, d_hslot,
+                         d_status, d_kidx, T, tab);
+    });
+  if (rc) return rc;
   c.r_windows = n_win;
   return ws_end(s);
 }
@@ -708,6 +921,22 @@ const char* hipbls_last_error(void) { return g_last_error.c_str(); }
 
 int hipbls_set_timing(int enabled) {
   g_ctx.timing_enabled = enabled != 0;
+  return HIPBLS_OK;
+}
+
+int hipbls_rlc_set_mode(int mode) {
+  if (mode != HIPBLS_RLC_AUTO && mode != HIPBLS_RLC_WINDOWS && mode != HIPBLS_RLC_BATCH)
+    return arg_err("unknown RLC mode");
+  return g_rlc_mode.exchange(mode);
+}
+
+int hipbls_rlc_batch_stats(uint64_t* attempted, uint64_t* passed, int32_t* last) {
+  if (!attempted || !passed || !last) return arg_err("null output");
+  ENTER();
+  rlcb_poll(true);
+  *attempted = g_ctx.rlcb_attempted;
+  *passed = g_ctx.rlcb_passed;
+  *last = g_ctx.rlcb_last;
   return HIPBLS_OK;
 }
 

@@ -6,6 +6,7 @@
 #include "lg2.h"
 #include "ops.h"
 #include "rlc.h"
+#include "rlcb.h"
 
 using namespace bls;
 
@@ -592,6 +593,157 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback_lg2(const uint32_t* __r
     }
   });
   if (!m) status[i] = ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+}
+
+// ---------------------------------------------------------------- batch-wide RLC check (rlcb.h)
+__global__ void __launch_bounds__(kBlock) k_rlcb_items(uint64_t n, const uint8_t* __restrict__ pks,
+                                                       const uint8_t* __restrict__ sigs,
+                                                       const uint32_t* __restrict__ msg_idx, uint64_t n_msgs,
+                                                       rlc_seed seed, uint32_t* __restrict__ rpk,
+                                                       uint32_t* __restrict__ pts, uint32_t* __restrict__ sc,
+                                                       int32_t* __restrict__ status,
+                                                       const uint32_t* __restrict__ key_idx, uint64_t T,
+                                                       const int32_t* __restrict__ tcode,
+                                                       const uint32_t* __restrict__ tab) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < n) rlcb_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk, pts, sc, status, key_idx, T, tcode, tab);
+}
+
+__global__ void __launch_bounds__(256) k_msm_hist(uint64_t npts, const uint32_t* __restrict__ sc,
+                                                  uint32_t* __restrict__ cnt) {
+  const uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (p < npts) msm_hist_lane(p, sc, cnt);
+}
+
+// Exclusive scan of the MSM_WINDOWS x MSM_NB digit counts: one workgroup of 1024 threads, 512 per window, each
+// owning 128 consecutive buckets.  off gets MSM_NB + 1 entries per window (the last is the window's total), cursor
+// the same offsets as the scatter's write positions.
+constexpr int kScanThreads = 1024;
+__global__ void __launch_bounds__(kScanThreads) k_msm_scan(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off,
+                                                           uint32_t* __restrict__ cursor) {
+  constexpr int per_w = kScanThreads / MSM_WINDOWS;            // threads per window
+  constexpr uint32_t span = MSM_NB / per_w;                    // buckets per thread
+  __shared__ uint32_t part[kScanThreads];
+  const int t = threadIdx.x;
+  const int w = t / per_w;
+  const uint32_t j0 = (uint32_t)(t % per_w) * span;
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < span; ++k) sum += cnt[w * MSM_NB + j0 + k];
+  part[t] = sum;
+  __syncthreads();
+  if (t % per_w == 0) {  // serial scan of this window's 512 partial sums
+    uint32_t acc = 0;
+    for (int k = 0; k < per_w; ++k) {
+      const uint32_t v = part[t + k];
+      part[t + k] = acc;
+      acc += v;
+    }
+    off[w * (MSM_NB + 1) + MSM_NB] = acc;
+  }
+  __syncthreads();
+  uint32_t acc = part[t];
+  for (uint32_t k = 0; k < span; ++k) {
+    off[w * (MSM_NB + 1) + j0 + k] = acc;
+    cursor[w * MSM_NB + j0 + k] = acc;
+    acc += cnt[w * MSM_NB + j0 + k];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_msm_scatter(uint64_t npts, const uint32_t* __restrict__ sc,
+                                                     uint32_t* __restrict__ cursor, uint32_t* __restrict__ list) {
+  const uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (p < npts) msm_scatter_lane(p, sc, cursor, list, npts);
+}
+
+__global__ void __launch_bounds__(kBlock) k_msm_bucket(const uint32_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ list, uint64_t npts,
+                                                       const uint32_t* __restrict__ pts, uint32_t* __restrict__ B) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t < (uint64_t)MSM_WINDOWS * MSM_NB) msm_bucket_lane((uint32_t)(t / MSM_NB), (uint32_t)(t % MSM_NB), off, list,
+                                                          npts, pts, B);
+}
+
+__global__ void __launch_bounds__(kBlock) k_msm_segment(const uint32_t* __restrict__ B, uint32_t* __restrict__ Sg) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t < (uint64_t)MSM_WINDOWS * MSM_NSEG) msm_segment_lane((uint32_t)(t / MSM_NSEG), (uint32_t)(t % MSM_NSEG), B, Sg);
+}
+
+// Window sums: workgroup w folds its window's MSM_NSEG segment results (strided, then the LDS tree of
+// g2_block_tree_sum) into W[w] (72 contiguous words).
+__global__ void __launch_bounds__(kSumBlock) k_msm_window(const uint32_t* __restrict__ Sg, uint32_t* __restrict__ W) {
+  __shared__ uint32_t red[72 * kSumBlock];
+  const uint32_t w = blockIdx.x;
+  g2j acc;
+  jac_set_inf(acc);
+  for (uint32_t s = threadIdx.x; s < MSM_NSEG; s += kSumBlock) {
+    g2j p;
+    soa_load<72>(&p.x.c0.v[0], Sg, (uint64_t)MSM_WINDOWS * MSM_NSEG, (uint64_t)w * MSM_NSEG + s);
+    g2j x = acc, y;
+    jac_add(y, x, p);
+    acc = y;
+  }
+  g2_block_tree_sum(acc, red);
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 72; ++k) W[72 * w + k] = (&acc.x.c0.v[0])[k];
+}
+
+__global__ void __launch_bounds__(kBlock) k_rlcb_chunks(uint64_t n, const int32_t* __restrict__ status,
+                                                        const uint32_t* __restrict__ msg_idx,
+                                                        const uint32_t* __restrict__ rpk,
+                                                        const uint32_t* __restrict__ H, uint64_t hstride,
+                                                        const uint32_t* __restrict__ hslot, uint32_t* __restrict__ F,
+                                                        uint64_t n_chunks) {
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c < n_chunks) rlcb_chunk_lane(c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks);
+}
+
+__global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict__ Fin, uint64_t nin,
+                                                      uint32_t* __restrict__ Fout, uint64_t nout, int fan) {
+  const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (g < nout) fp12_prod_lane(g, Fin, nin, Fout, nout, fan);
+}
+
+// The Miller value of (-g1, S), S = W0 + [2^16] W1 (one lane; runs beside the chunk stage on its own stream).
+__global__ void __launch_bounds__(kBlock) k_rlcb_sfactor(const uint32_t* __restrict__ W, uint32_t* __restrict__ FS) {
+  if (threadIdx.x != 0) return;
+  g2j W0, W1, S;
+  for (int k = 0; k < 72; ++k) {
+    (&W0.x.c0.v[0])[k] = W[k];
+    (&W1.x.c0.v[0])[k] = W[72 + k];
+  }
+  msm_combine(S, W0, W1);
+  fp12 f;
+  if (jac_is_inf(S)) {
+    fp12_set_one(f);
+  } else {
+    g1a P[1];
+    g2a Q[1];
+    P[0].x = G1_GEN_X;
+    P[0].y = G1_NEG_GEN_Y;
+    jac_to_aff(Q[0], S);
+    miller_loop_multi<1>(f, P, Q, 1);
+  }
+  soa_store<144>(FS, 1, 0, &f.c0.c0.c0.v[0]);
+}
+
+// The verdict, on lanes 0 and 1 as a pair (lg2.h): lane 0 holds the Miller value of (-g1, S), lane 1 the product of
+// the chunks' Miller values; split final exponentiation; flag[0] = 1 when the product is 1.
+__global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restrict__ Ftot,
+                                                       const uint32_t* __restrict__ FS, int32_t* __restrict__ flag) {
+  const int t = threadIdx.x;
+  if (t >= 2) return;
+  const uint32_t m = t ? ~0u : 0u;
+  fp12 f;
+  soa_load<144>(&f.c0.c0.c0.v[0], t ? Ftot : FS, 1, 0);
+  const bool ok = lg2_finish(f, m);
+  if (t == 0) flag[0] = ok ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(kBlock) k_rlcb_mark(uint64_t n, const int32_t* __restrict__ flag,
+                                                      int32_t* __restrict__ status, const uint32_t* __restrict__ pts,
+                                                      const uint32_t* __restrict__ sc, uint32_t* __restrict__ rsig) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < n) rlcb_mark_lane(i, n, flag[0] != 0, status, pts, sc, rsig);
 }
 
 // ---------------------------------------------------------------- resident pubshare table

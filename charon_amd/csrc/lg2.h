@@ -243,13 +243,8 @@ __device__ __forceinline__ bool fp12h_is_one(const fp6& h, uint32_t m) {
 // Pairing-product check over n pairs split across a lane pair: this lane takes pairs i with i % 2 == parity
 // (at most MAXN of them).  Both lanes must call it together with the same n.  Returns prod e(P_i, Q_i) == 1 on
 // both lanes.  P_i / Q_i are read through callables so the caller decides where the pairs come from.
-template <int MAXN>
-__device__ bool lg2_check_pairs(const g1a* P, const g2a* Q, int k, uint32_t m) {
-  fp12 f;
-  if (k > 0)
-    miller_loop_multi<MAXN>(f, P, Q, k);
-  else
-    fp12_set_one(f);
+// Both lanes hold a full Fp12 (their own Miller value): the check prod == 1 after the split final exponentiation.
+static __device__ bool lg2_finish(const fp12& f, uint32_t m) {
   fp12 g;
   fp12 mine = f;
   // combine the two lanes' Miller values: own half of f_even * f_odd
@@ -264,6 +259,16 @@ __device__ bool lg2_check_pairs(const g1a* P, const g2a* Q, int k, uint32_t m) {
   fp12h_mul_full(h, fe, fo, m);
   final_exponentiation_split(e, h, m);
   return fp12h_is_one(e, m);
+}
+
+template <int MAXN>
+__device__ bool lg2_check_pairs(const g1a* P, const g2a* Q, int k, uint32_t m) {
+  fp12 f;
+  if (k > 0)
+    miller_loop_multi<MAXN>(f, P, Q, k);
+  else
+    fp12_set_one(f);
+  return lg2_finish(f, m);
 }
 
 template <int MAXN, class GetPair>

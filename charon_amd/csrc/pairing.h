@@ -23,7 +23,7 @@ struct g1_pair_in {  // P in affine coordinates, or is_inf
 
 // r = f^((p^12-1)/r * 3)
 
-BLS_HD BLS_CALL void miller_dbl_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const fp& xp_in, const fp& yp_in) {
+BLS_HD BLS_INLINE void miller_dbl_step_inl(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const fp& xp_in, const fp& yp_in) {
   const fp xp = xp_in;
   const fp yp = yp_in;
   g2j T = T_in;
@@ -65,8 +65,9 @@ BLS_HD BLS_CALL void miller_dbl_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const
   T.z = Z3;
   T_in = T;
 }
+BLS_HD BLS_MILLER_CALL void miller_dbl_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const fp& xp_in, const fp& yp_in) { miller_dbl_step_inl(T_in, g0, g1, h1, xp_in, yp_in); }
 
-BLS_HD BLS_CALL void miller_add_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const g2a& Q_in, const fp& xp_in,
+BLS_HD BLS_INLINE void miller_add_step_inl(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const g2a& Q_in, const fp& xp_in,
                                          const fp& yp_in) {
   const g2a Q = Q_in;
   const fp xp = xp_in;
@@ -106,6 +107,34 @@ BLS_HD BLS_CALL void miller_add_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const
   T.z = Z3;
   T_in = T;
 }
+BLS_HD BLS_MILLER_CALL void miller_add_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const g2a& Q_in, const fp& xp_in,
+                                         const fp& yp_in) { miller_add_step_inl(T_in, g0, g1, h1, Q_in, xp_in, yp_in); }
+
+// Fused 2-pair Miller iterations: one call per step instead of four, so f, T0, T1 cross the stack once per step
+// and one prologue saves the callee-saved registers instead of four (each Fp12-level function saves ~180 of
+// them).  BLS_MILLER_FUSE = 1: squaring + both doubling steps + line-pair product in one call; 2: the squaring
+// stays a separate call.
+#ifndef BLS_MILLER_FUSE
+#define BLS_MILLER_FUSE 0
+#endif
+BLS_HD BLS_CALL void miller_dbl2_line2(fp12& f_io, g2j& T0_io, g2j& T1_io, const g1a& P0_in, const g1a& P1_in,
+                                       bool square) {
+  fp12 f = f_io;
+  g2j T0 = T0_io, T1 = T1_io;
+  const g1a P0 = P0_in, P1 = P1_in;
+  if (square) {
+    fp12 s;
+    fp12_sqr_inl(s, f);
+    f = s;
+  }
+  fp2 a0, a1, ah, g0, g1, h1;
+  miller_dbl_step_inl(T0, a0, a1, ah, P0.x, P0.y);
+  miller_dbl_step_inl(T1, g0, g1, h1, P1.x, P1.y);
+  fp12_mul_line2_inl(f, a0, a1, ah, g0, g1, h1);
+  f_io = f;
+  T0_io = T0;
+  T1_io = T1;
+}
 
 BLS_HD BLS_CALL void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bool* skip, int n) {
   constexpr int MAXN = 2;
@@ -119,13 +148,20 @@ BLS_HD BLS_CALL void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bo
   fp2 g0, g1, h1;
   bool first = true;
   for (int bit = 62; bit >= 0; --bit) {
-    if (!first) fp12_sqr(f, f);
-    first = false;
     if (n == 2 && !skip[0] && !skip[1]) {  // both lines live: one line-pair product (fp12_mul_line2)
       fp2 a0, a1, ah;
+#if BLS_MILLER_FUSE == 1
+      miller_dbl2_line2(f, T[0], T[1], P[0], P[1], !first);
+#elif BLS_MILLER_FUSE == 2
+      if (!first) fp12_sqr(f, f);
+      miller_dbl2_line2(f, T[0], T[1], P[0], P[1], false);
+#else
+      if (!first) fp12_sqr(f, f);
       miller_dbl_step(T[0], a0, a1, ah, P[0].x, P[0].y);
       miller_dbl_step(T[1], g0, g1, h1, P[1].x, P[1].y);
       fp12_mul_line2(f, a0, a1, ah, g0, g1, h1);
+#endif
+      first = false;
       if ((X_ABS >> bit) & 1ull) {
         miller_add_step(T[0], a0, a1, ah, Q[0], P[0].x, P[0].y);
         miller_add_step(T[1], g0, g1, h1, Q[1], P[1].x, P[1].y);
@@ -133,6 +169,8 @@ BLS_HD BLS_CALL void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bo
       }
       continue;
     }
+    if (!first) fp12_sqr(f, f);
+    first = false;
     for (int i = 0; i < n; ++i) {
       miller_dbl_step(T[i], g0, g1, h1, P[i].x, P[i].y);
       if (!skip[i]) fp12_mul_line(f, g0, g1, h1);

@@ -1,0 +1,262 @@
+// Batch-wide RLC check with a Pippenger MSM (BASELINE.json north star: "Random-linear-combination batch
+// verification uses a Pippenger MSM over G1/G2 with LDS-staged bucket accumulation").
+//
+// The windowed RLC of rlc.h gives every window of 8 items its own final exponentiation, because at the bench's
+// 1 % invalid partials a single batch-wide check fails on every batch.  When invalid partials are rare (the
+// normal case for a healthy cluster), one check over the whole batch is much cheaper:
+//
+//     prod_runs e( sum_{i in run} r_i pk_i , H(m_run) ) * e( -g1 , sum_i r_i sig_i ) == 1
+//
+// with the same per-item scalars r_i = a_i + b_i x as the windows (rlc_scalars), so the windows can take over
+// without recomputing anything when the batch check fails.  Stages (one lane per unit; kernels.h, hipbls.hip):
+//   1. items    : decode + subgroup tests (herumi's order, final statuses), [r_i] pk_i in G1 (Shamir, as rlc.h),
+//                 and the MSM inputs sig_i, psi(sig_i) (affine, psi = [x] on G2) with 32-bit scalars a_i, b_i;
+//   2. MSM      : S = sum_i [a_i] sig_i + [b_i] psi(sig_i), Pippenger with 16-bit windows: counting sort of the
+//                 2n points by digit (histogram, scan, scatter), one lane per bucket sums its points, one lane
+//                 per 16-bucket segment folds sum_j j B_j by running sums, two workgroups tree-sum the
+//                 segments in LDS, and S = W0 + [2^16] W1;
+//   3. chunks   : one lane per 16 consecutive items: runs of equal message among pending items are summed in G1
+//                 and paired with H(m) in one multi-Miller loop (no final exponentiation) -> f_chunk;
+//   4. product  : the chunks' Miller values multiplied together (fan-in 16 per level);
+//   5. final    : a lane pair multiplies in the Miller value of (-g1, S) and runs the split final
+//                 exponentiation (lg2.h); the verdict goes to a device flag;
+//   6. mark     : pass -> every pending item is valid; fail -> each pending item gets [r_i] sig_i for the window
+//                 stages of rlc.h, which then decide item by item.
+// Soundness is the windows' argument over the whole batch: a batch with an invalid item passes with
+// probability <= 2^-64 over the scalars.  Bucket 0 is skipped (digit 0 adds nothing).
+#pragma once
+#include "rlc.h"
+
+namespace bls {
+
+constexpr int RLCB_C = 16;                     // items per Miller chunk
+constexpr int MSM_BITS = 16;                   // Pippenger window width
+constexpr int MSM_WINDOWS = 2;                 // 32-bit scalars
+constexpr uint32_t MSM_NB = 1u << MSM_BITS;    // buckets per window (bucket 0 unused)
+constexpr int MSM_SEG = 16;                    // buckets folded per segment lane
+constexpr uint32_t MSM_NSEG = MSM_NB / MSM_SEG;
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define BLS_ATOMIC_ADD_U32(p, v) atomicAdd((p), (v))
+#else
+BLS_HD BLS_INLINE uint32_t bls_serial_add_u32(uint32_t* p, uint32_t v) {  // host build: lanes run one by one
+  const uint32_t o = *p;
+  *p = o + v;
+  return o;
+}
+#define BLS_ATOMIC_ADD_U32(p, v) bls_serial_add_u32((p), (v))
+#endif
+
+// ---- stage 1 ------------------------------------------------------------------------------------
+// pts: affine G2 SoA with 2n columns (sig_i at i, psi(sig_i) at n + i); sc: 2n scalars (a_i, then b_i).
+BLS_HD BLS_INLINE void rlcb_items_lane(uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
+                                       uint64_t n, uint64_t n_msgs, const rlc_seed& seed, uint32_t* rpk,
+                                       uint32_t* pts, uint32_t* sc, int32_t* status,
+                                       const uint32_t* key_idx = nullptr, uint64_t T = 0,
+                                       const int32_t* tcode = nullptr, const uint32_t* tab = nullptr) {
+  g1j rp;
+  jac_set_inf(rp);
+  g2a sig, psig;
+  fp2_set_zero(sig.x);
+  fp2_set_zero(sig.y);
+  psig = sig;
+  uint32_t a = 0, b = 0;
+  int st;
+  if (msg_idx[i] >= n_msgs || (!pks && key_idx[i] >= T)) {
+    st = HIPBLS_ERR_ARG;
+  } else {
+    g1a pk;
+    g1j xpk;
+    const int dp = pks ? g1_decompress_keep_x(pk, xpk, pks + 48 * i) : pubtab_get(pk, xpk, key_idx[i], T, tcode, tab);
+    st = RLC_PENDING;
+    if (dp == DEC_BAD) st = HIPBLS_ERR_PUBKEY;
+    if (st == RLC_PENDING) {
+      const int ds = g2_decompress(sig, sigs + 96 * i, true);
+      if (ds == DEC_BAD)
+        st = HIPBLS_ERR_SIGNATURE;
+      else if (dp == DEC_INF || ds == DEC_INF)
+        st = HIPBLS_ERR_VERIFY;
+    }
+    if (st == RLC_PENDING) {
+      rlc_scalars(a, b, seed, i);
+      g1j pj;
+      jac_from_aff(pj, pk);
+      jac_mul2_u32(rp, pj, xpk, a, b);
+      g2j sj, psj;
+      jac_from_aff(sj, sig);
+      g2_psi(psj, sj);  // Z stays 1: psi of an affine point is affine
+      psig.x = psj.x;
+      psig.y = psj.y;
+    } else {
+      fp2_set_zero(sig.x);
+      fp2_set_zero(sig.y);
+    }
+  }
+  soa_store<36>(rpk, n, i, &rp.x.v[0]);
+  soa_store<48>(pts, 2 * n, i, &sig.x.c0.v[0]);
+  soa_store<48>(pts, 2 * n, n + i, &psig.x.c0.v[0]);
+  sc[i] = a;
+  sc[n + i] = b;
+  status[i] = st;
+}
+
+// ---- stage 2: Pippenger ----------------------------------------------------------------------------
+BLS_HD BLS_INLINE uint32_t msm_digit(uint32_t s, int w) { return (s >> (MSM_BITS * w)) & (MSM_NB - 1); }
+
+// cnt: MSM_WINDOWS x MSM_NB counters (zeroed)
+BLS_HD BLS_INLINE void msm_hist_lane(uint64_t p, const uint32_t* sc, uint32_t* cnt) {
+  const uint32_t s = sc[p];
+  for (int w = 0; w < MSM_WINDOWS; ++w) {
+    const uint32_t d = msm_digit(s, w);
+    if (d) BLS_ATOMIC_ADD_U32(&cnt[w * MSM_NB + d], 1u);
+  }
+}
+
+// cursor: the exclusive scan of cnt (per window); list: MSM_WINDOWS x npts point indices grouped by bucket
+BLS_HD BLS_INLINE void msm_scatter_lane(uint64_t p, const uint32_t* sc, uint32_t* cursor, uint32_t* list,
+                                        uint64_t npts) {
+  const uint32_t s = sc[p];
+  for (int w = 0; w < MSM_WINDOWS; ++w) {
+    const uint32_t d = msm_digit(s, w);
+    if (d) {
+      const uint32_t at = BLS_ATOMIC_ADD_U32(&cursor[w * MSM_NB + d], 1u);
+      list[(uint64_t)w * npts + at] = (uint32_t)p;
+    }
+  }
+}
+
+// bucket (w, j): the sum of its points.  off: MSM_WINDOWS x (MSM_NB + 1) exclusive offsets.  B: Jacobian SoA,
+// 72 words x (MSM_WINDOWS * MSM_NB).
+BLS_HD BLS_INLINE void msm_bucket_lane(uint32_t w, uint32_t j, const uint32_t* off, const uint32_t* list,
+                                       uint64_t npts, const uint32_t* pts, uint32_t* B) {
+  g2j acc;
+  jac_set_inf(acc);
+  const uint32_t k0 = off[w * (MSM_NB + 1) + j], k1 = off[w * (MSM_NB + 1) + j + 1];
+  for (uint32_t k = k0; k < k1; ++k) {
+    g2a q;
+    soa_load<48>(&q.x.c0.v[0], pts, npts, list[(uint64_t)w * npts + k]);
+    g2j x = acc, y;
+    jac_add_aff(y, x, q);
+    acc = y;
+  }
+  soa_store<72>(B, (uint64_t)MSM_WINDOWS * MSM_NB, (uint64_t)w * MSM_NB + j, &acc.x.c0.v[0]);
+}
+
+// segment (w, s): sum_{j in [16 s, 16 s + 16)} j B_j = T + (16 s - 1) R with R = sum B_j and T = sum (j - 16 s + 1) B_j
+// from running sums (top bucket first).  Sg: Jacobian SoA, 72 words x (MSM_WINDOWS * MSM_NSEG).
+BLS_HD BLS_INLINE void msm_segment_lane(uint32_t w, uint32_t s, const uint32_t* B, uint32_t* Sg) {
+  g2j R, T;
+  jac_set_inf(R);
+  jac_set_inf(T);
+  for (int k = MSM_SEG - 1; k >= 0; --k) {
+    g2j b;
+    soa_load<72>(&b.x.c0.v[0], B, (uint64_t)MSM_WINDOWS * MSM_NB, (uint64_t)w * MSM_NB + s * MSM_SEG + k);
+    g2j x = R, y;
+    jac_add(y, x, b);
+    R = y;
+    g2j u = T, v;
+    jac_add(v, u, R);
+    T = v;
+  }
+  g2j m, out;
+  if (s == 0) {
+    jac_neg(m, R);
+  } else {
+    jac_mul_u64(m, R, (uint64_t)s * MSM_SEG - 1);
+  }
+  jac_add(out, T, m);
+  soa_store<72>(Sg, (uint64_t)MSM_WINDOWS * MSM_NSEG, (uint64_t)w * MSM_NSEG + s, &out.x.c0.v[0]);
+}
+
+// S = W0 + [2^16] W1
+BLS_HD BLS_INLINE void msm_combine(g2j& S, const g2j& W0, const g2j& W1) {
+  g2j t = W1;
+  for (int k = 0; k < MSM_BITS; ++k) {
+    g2j u;
+    jac_dbl(u, t);
+    t = u;
+  }
+  jac_add(S, W0, t);
+}
+
+// ---- stage 3: per-chunk multi-Miller loop ----------------------------------------------------------
+// F: Fp12 SoA, 144 words x n_chunks.  Chunks without pending items store 1.
+BLS_HD BLS_INLINE void rlcb_chunk_lane(uint64_t c, uint64_t n, const int32_t* status, const uint32_t* msg_idx,
+                                       const uint32_t* rpk, const uint32_t* H, uint64_t hstride,
+                                       const uint32_t* hslot, uint32_t* F, uint64_t n_chunks) {
+  g1a P[RLCB_C];
+  g2a Q[RLCB_C];
+  int np = 0;
+  g1j run;
+  jac_set_inf(run);
+  uint32_t run_msg = 0xffffffffu;
+  const uint64_t i0 = c * RLCB_C, i1 = i0 + RLCB_C < n ? i0 + RLCB_C : n;
+  for (uint64_t i = i0; i < i1; ++i) {
+    if (status[i] != RLC_PENDING) continue;
+    g1j qp;
+    soa_load<36>(&qp.x.v[0], rpk, n, i);
+    const uint32_t m = msg_idx[i];
+    if (m != run_msg) {
+      if (run_msg != 0xffffffffu && !jac_is_inf(run)) {
+        jac_to_aff(P[np], run);
+        soa_load<48>(&Q[np].x.c0.v[0], H, hstride, h_col(hslot, run_msg));
+        ++np;
+      }
+      run = qp;
+      run_msg = m;
+    } else {
+      g1j x = run, y;
+      jac_add(y, x, qp);
+      run = y;
+    }
+  }
+  if (run_msg != 0xffffffffu && !jac_is_inf(run)) {
+    jac_to_aff(P[np], run);
+    soa_load<48>(&Q[np].x.c0.v[0], H, hstride, h_col(hslot, run_msg));
+    ++np;
+  }
+  fp12 f;
+  if (np)
+    miller_loop_multi<RLCB_C>(f, P, Q, np);
+  else
+    fp12_set_one(f);
+  soa_store<144>(F, n_chunks, c, &f.c0.c0.c0.v[0]);
+}
+
+// ---- stage 4: product of Miller values, fan-in `fan` ----------------------------------------------------
+BLS_HD BLS_INLINE void fp12_prod_lane(uint64_t g, const uint32_t* Fin, uint64_t nin, uint32_t* Fout, uint64_t nout,
+                                      int fan) {
+  fp12 acc;
+  fp12_set_one(acc);
+  const uint64_t k0 = g * (uint64_t)fan, k1 = k0 + fan < nin ? k0 + fan : nin;
+  for (uint64_t k = k0; k < k1; ++k) {
+    fp12 f;
+    soa_load<144>(&f.c0.c0.c0.v[0], Fin, nin, k);
+    fp12 x = acc, y;
+    fp12_mul(y, x, f);
+    acc = y;
+  }
+  soa_store<144>(Fout, nout, g, &acc.c0.c0.c0.v[0]);
+}
+
+// ---- stage 6 -------------------------------------------------------------------------------------
+// pass: every pending item is valid.  Otherwise [r_i] sig_i = [a_i] sig_i + [b_i] psi(sig_i) goes to rsig (Jacobian
+// SoA, 72 x n) for the window stages, which decide the pending items.
+BLS_HD BLS_INLINE void rlcb_mark_lane(uint64_t i, uint64_t n, bool pass, int32_t* status, const uint32_t* pts,
+                                      const uint32_t* sc, uint32_t* rsig) {
+  if (status[i] != RLC_PENDING) return;
+  if (pass) {
+    status[i] = HIPBLS_OK;
+    return;
+  }
+  g2a s, ps;
+  soa_load<48>(&s.x.c0.v[0], pts, 2 * n, i);
+  soa_load<48>(&ps.x.c0.v[0], pts, 2 * n, n + i);
+  g2j sj, psj, rs;
+  jac_from_aff(sj, s);
+  jac_from_aff(psj, ps);
+  jac_mul2_u32(rs, sj, psj, sc[i], sc[n + i]);
+  soa_store<72>(rsig, n, i, &rs.x.c0.v[0]);
+}
+
+}  // namespace bls

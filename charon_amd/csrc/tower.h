@@ -9,6 +9,10 @@
 #ifndef BLS_FP6_CALL
 #define BLS_FP6_CALL BLS_INLINE
 #endif
+// Miller-loop building blocks (Fp12 squaring, line products, doubling/addition steps).
+#ifndef BLS_MILLER_CALL
+#define BLS_MILLER_CALL BLS_CALL
+#endif
 
 namespace bls {
 
@@ -312,7 +316,7 @@ BLS_HD BLS_CALL void fp12_mul(fp12& r, const fp12& a_in, const fp12& b_in) {
   fp6_add(r.c0, t0, t1);
   r.c1 = c1;
 }
-BLS_HD BLS_CALL void fp12_sqr(fp12& r, const fp12& a_in) {
+BLS_HD BLS_INLINE void fp12_sqr_inl(fp12& r, const fp12& a_in) {
   // complex squaring: c0 = (a0+a1)(a0+v a1) - t - v t, c1 = 2t, t = a0 a1
   const fp12 a = a_in;
   fp6 t, s0, s1, vt;
@@ -326,6 +330,7 @@ BLS_HD BLS_CALL void fp12_sqr(fp12& r, const fp12& a_in) {
   fp6_sub(r.c0, s0, vt);
   fp6_add(r.c1, t, t);
 }
+BLS_HD BLS_MILLER_CALL void fp12_sqr(fp12& r, const fp12& a_in) { fp12_sqr_inl(r, a_in); }
 BLS_HD BLS_CALL void fp12_inv(fp12& r, const fp12& a_in) {
   const fp12 a = a_in;
   fp6 t0, t1;
@@ -338,7 +343,7 @@ BLS_HD BLS_CALL void fp12_inv(fp12& r, const fp12& a_in) {
   fp6_mul(t1, a.c1, t0);
   fp6_neg(r.c1, t1);
 }
-BLS_HD BLS_CALL void fp12_mul_line(fp12& f_in, const fp2& g0_in, const fp2& g1_in, const fp2& h1_in) {
+BLS_HD BLS_MILLER_CALL void fp12_mul_line(fp12& f_in, const fp2& g0_in, const fp2& g1_in, const fp2& h1_in) {
   const fp2 g0 = g0_in;
   const fp2 g1 = g1_in;
   const fp2 h1 = h1_in;
@@ -361,7 +366,7 @@ BLS_HD BLS_CALL void fp12_mul_line(fp12& f_in, const fp2& g0_in, const fp2& g1_i
 // f *= la * lb for two M-twist lines l = (g0 + g1 v) + (h1 v) w.  The line product is
 // (c0 dense) + (x v + y v^2) w with w^2 = v, v^3 = xi (6 Fp2 products); multiplying it into f
 // costs 17 more, 23 in all instead of 26 for two fp12_mul_line calls.
-BLS_HD BLS_CALL void fp12_mul_line2(fp12& f_in, const fp2& ga0_in, const fp2& ga1_in, const fp2& ha1_in, const fp2& gb0_in,
+BLS_HD BLS_INLINE void fp12_mul_line2_inl(fp12& f_in, const fp2& ga0_in, const fp2& ga1_in, const fp2& ha1_in, const fp2& gb0_in,
                                     const fp2& gb1_in, const fp2& hb1_in) {
   const fp2 ga0 = ga0_in;
   const fp2 ga1 = ga1_in;
@@ -425,6 +430,8 @@ BLS_HD BLS_CALL void fp12_mul_line2(fp12& f_in, const fp2& ga0_in, const fp2& ga
   fp6_add(f.c0, t0, t1);
   f_in = f;
 }
+BLS_HD BLS_MILLER_CALL void fp12_mul_line2(fp12& f_in, const fp2& ga0_in, const fp2& ga1_in, const fp2& ha1_in, const fp2& gb0_in,
+                                    const fp2& gb1_in, const fp2& hb1_in) { fp12_mul_line2_inl(f_in, ga0_in, ga1_in, ha1_in, gb0_in, gb1_in, hb1_in); }
 BLS_HD BLS_CALL void fp12_frobenius(fp12& r, const fp12& a_in, int j) {
   const fp12 a = a_in;
   // coefficient of w^k (k = 2i + h for a.c_h.c_i) is conj^j(c) * gamma_{j,k}

@@ -24,6 +24,7 @@ OK, ERR_PUBKEY, ERR_SIGNATURE, ERR_VERIFY, ERR_SECRET, ERR_COMBINE, ERR_ZERO_SIG
 INFINITY_G2 = b"\xc0" + bytes(95)  # compressed point at infinity (the empty Aggregate, herumi.go:220-242)
 ERR_ARG, ERR_DEVICE = 16, 17
 PAIR_AUTO, PAIR_SINGLE, PAIR_LANES = 0, 1, 2  # hipbls_set_pair_mode: pairing-check layout (include/hipbls.h)
+RLC_AUTO, RLC_WINDOWS, RLC_BATCH = 0, 1, 2     # hipbls_rlc_set_mode: batch-wide check policy (include/hipbls.h)
 
 # tbls/herumi.go error strings by status code
 VERIFY_ERRORS = {
@@ -64,6 +65,8 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_current_device": ([], ctypes.c_int),
         "hipbls_set_timing": ([ctypes.c_int], ctypes.c_int),
         "hipbls_set_pair_mode": ([ctypes.c_int], ctypes.c_int),
+        "hipbls_rlc_set_mode": ([ctypes.c_int], ctypes.c_int),
+        "hipbls_rlc_batch_stats": ([u64p, u64p, i32p], ctypes.c_int),
         "hipbls_verify": ([u8p, u8p, u64, u8p, i32p], ctypes.c_int),
         "hipbls_verify_submit": ([u8p, u8p, u64, u8p, u64p], ctypes.c_int),
         "hipbls_verify_wait": ([u64, i32p], ctypes.c_int),
@@ -126,6 +129,7 @@ def exported_symbols() -> List[str]:
         "hipbls_current_device", "hipbls_set_timing", "hipbls_verify", "hipbls_verify_submit", "hipbls_verify_wait",
         "hipbls_queue_config", "hipbls_queue_stats", "hipbls_verify_signed_data_batch", "hipbls_aggregate_device",
         "hipbls_hcache_config", "hipbls_hcache_stats", "hipbls_set_pair_mode",
+        "hipbls_rlc_set_mode", "hipbls_rlc_batch_stats",
     ]
 
 
@@ -518,3 +522,17 @@ class HipBLS:
         if rc not in (PAIR_AUTO, PAIR_SINGLE, PAIR_LANES):
             _check(rc, self.lib)
         return rc
+
+    # ---------------------------------------------------------------- batch-wide RLC check (rlcb.h)
+    def set_rlc_mode(self, mode: int) -> int:
+        """RLC_AUTO / RLC_WINDOWS / RLC_BATCH; returns the previous mode.  Statuses never depend on it."""
+        rc = self.lib.hipbls_rlc_set_mode(mode)
+        if rc not in (RLC_AUTO, RLC_WINDOWS, RLC_BATCH):
+            _check(rc, self.lib)
+        return rc
+
+    def rlc_batch_stats(self) -> Tuple[int, int, int]:
+        """(batch-wide checks launched, passed, last verdict: -1 none / 0 failed / 1 passed)."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int32()
+        _check(self.lib.hipbls_rlc_batch_stats(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), self.lib)
+        return a.value, b.value, c.value

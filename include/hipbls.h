@@ -58,7 +58,7 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 6
+#define HIPBLS_ABI_VERSION 7
 int hipbls_abi_version(void);
 
 /* Select the HIP device used by the calling process (one process per GPU); idempotent.
@@ -180,6 +180,16 @@ int hipbls_batch_verify_rlc_keys(const uint32_t* key_idx, const uint8_t* sigs, c
 /* Windows checked, windows that failed, and items re-verified one by one in the last RLC call
  * (synchronizes the device). */
 int hipbls_rlc_stats(uint64_t* windows, uint64_t* windows_failed, uint64_t* items_fallback);
+/* Batch-wide check (charon_amd/csrc/rlcb.h): one multi-pairing over the whole batch with a Pippenger MSM for
+ * sum r_i sig_i, ahead of the windows.  It decides an all-valid batch alone; when it fails, the windows decide
+ * item by item, so statuses never depend on the mode.  HIPBLS_RLC_AUTO (default): batch-wide first for batches of
+ * >= 1,024 items unless the last batch-wide check failed (then 8 calls windows-only); HIPBLS_RLC_WINDOWS: windows
+ * only; HIPBLS_RLC_BATCH: batch-wide first always.  Returns the previous mode or HIPBLS_ERR_ARG. */
+enum { HIPBLS_RLC_AUTO = 0, HIPBLS_RLC_WINDOWS = 1, HIPBLS_RLC_BATCH = 2 };
+int hipbls_rlc_set_mode(int mode);
+/* Batch-wide checks launched and passed since load, and the last verdict (-1 none, 0 failed, 1 passed); waits for
+ * the last one in flight. */
+int hipbls_rlc_batch_stats(uint64_t* attempted, uint64_t* passed, int32_t* last);
 
 /* Resident H(m) cache used by the host-buffer RLC calls: each distinct message is hashed to G2
  * once and kept in HBM across calls (FIFO over `capacity` slots, 192 B each); 0 disables it (the default).

@@ -338,3 +338,133 @@ extern "C" int ht_verify_key(const uint8_t* pk48, const uint8_t* msg, uint32_t l
   const int dp = pubtab_get(pk, xpk, 0, 1, &code, tab);
   return op_verify_decoded_pk(dp, pk, msg, len, sig);
 }
+
+// ---- batch-wide RLC check with the Pippenger MSM (charon_amd/csrc/rlcb.h), lane by lane ------------------
+#include "../../charon_amd/csrc/rlcb.h"
+
+namespace {
+// Pippenger over npts affine SoA points with 32-bit scalars: the device stages run serially.
+void host_msm(g2j& S, const uint32_t* pts, const uint32_t* sc, uint64_t npts) {
+  std::vector<uint32_t> cnt(MSM_WINDOWS * MSM_NB, 0), off(MSM_WINDOWS * (MSM_NB + 1)), cur(MSM_WINDOWS * MSM_NB);
+  std::vector<uint32_t> list(MSM_WINDOWS * (npts ? npts : 1));
+  for (uint64_t p = 0; p < npts; ++p) msm_hist_lane(p, sc, cnt.data());
+  for (int w = 0; w < MSM_WINDOWS; ++w) {
+    uint32_t acc = 0;
+    for (uint32_t j = 0; j < MSM_NB; ++j) {
+      off[w * (MSM_NB + 1) + j] = acc;
+      cur[w * MSM_NB + j] = acc;
+      acc += cnt[w * MSM_NB + j];
+    }
+    off[w * (MSM_NB + 1) + MSM_NB] = acc;
+  }
+  for (uint64_t p = 0; p < npts; ++p) msm_scatter_lane(p, sc, cur.data(), list.data(), npts);
+  std::vector<uint32_t> B((uint64_t)MSM_WINDOWS * MSM_NB * 72), Sg((uint64_t)MSM_WINDOWS * MSM_NSEG * 72);
+  for (int w = 0; w < MSM_WINDOWS; ++w)
+    for (uint32_t j = 0; j < MSM_NB; ++j) msm_bucket_lane(w, j, off.data(), list.data(), npts, pts, B.data());
+  for (int w = 0; w < MSM_WINDOWS; ++w)
+    for (uint32_t s = 0; s < MSM_NSEG; ++s) msm_segment_lane(w, s, B.data(), Sg.data());
+  g2j W[MSM_WINDOWS];
+  for (int w = 0; w < MSM_WINDOWS; ++w) {
+    jac_set_inf(W[w]);
+    for (uint32_t s = 0; s < MSM_NSEG; ++s) {
+      g2j t;
+      soa_load<72>(&t.x.c0.v[0], Sg.data(), (uint64_t)MSM_WINDOWS * MSM_NSEG, (uint64_t)w * MSM_NSEG + s);
+      jac_add(W[w], W[w], t);
+    }
+  }
+  msm_combine(S, W[0], W[1]);
+}
+}  // namespace
+
+// sum_i [sc_i] P_i for affine plain points (x0, x1, y0, y1 big-endian, 192 B each); out = compressed 96 B
+extern "C" void ht_msm_g2(const uint8_t* pts192, const uint32_t* sc, uint64_t n, uint8_t* out96) {
+  std::vector<uint32_t> pts(48 * (n ? n : 1));
+  for (uint64_t i = 0; i < n; ++i) {
+    g2a a;
+    fp_in(a.x.c0, pts192 + 192 * i);
+    fp_in(a.x.c1, pts192 + 192 * i + 48);
+    fp_in(a.y.c0, pts192 + 192 * i + 96);
+    fp_in(a.y.c1, pts192 + 192 * i + 144);
+    soa_store<48>(pts.data(), n, i, &a.x.c0.v[0]);
+  }
+  g2j S;
+  host_msm(S, pts.data(), sc, n);
+  g2_compress(out96, S);
+}
+
+// The batch-check pipeline (stages 1-6 of rlcb.h) followed by the window/fallback stages of rlc.h for whatever
+// the batch check left pending.  *passed = the batch-wide verdict.
+// counts6 (optional): Fp products of items, hash, MSM, chunk Miller loops, product + verdict, windows + fallback.
+extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
+                              const uint8_t* msgs, const uint64_t* offs, uint64_t n_msgs, const uint8_t* seed32,
+                              int32_t* status, int32_t* passed, uint64_t* counts6) {
+  uint64_t c0 = g_fp_mul_count + g_fp_sqr_count;
+  auto mark = [&](int k) {
+    const uint64_t c = g_fp_mul_count + g_fp_sqr_count;
+    if (counts6) counts6[k] = c - c0;
+    c0 = c;
+  };
+  rlc_seed seed;
+  for (int k = 0; k < 8; ++k)
+    seed.w[k] = (uint32_t)seed32[4 * k] << 24 | (uint32_t)seed32[4 * k + 1] << 16 | (uint32_t)seed32[4 * k + 2] << 8 |
+                (uint32_t)seed32[4 * k + 3];
+  std::vector<uint32_t> rpk(n * 36), rsig(n * 72), pts(2 * n * 48), sc(2 * n), H((n_msgs ? n_msgs : 1) * 48);
+  for (uint64_t i = 0; i < n; ++i)
+    rlcb_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk.data(), pts.data(), sc.data(), status);
+  mark(0);
+  for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, H.data(), n_msgs, nullptr);
+  mark(1);
+  g2j S;
+  host_msm(S, pts.data(), sc.data(), 2 * n);
+  mark(2);
+  const uint64_t nch = (n + RLCB_C - 1) / RLCB_C;
+  std::vector<uint32_t> F(144 * (nch ? nch : 1));
+  for (uint64_t c = 0; c < nch; ++c)
+    rlcb_chunk_lane(c, n, status, msg_idx, rpk.data(), H.data(), n_msgs, nullptr, F.data(), nch);
+  mark(3);
+  uint64_t cur = nch;
+  while (cur > 1) {
+    const uint64_t nxt = (cur + 15) / 16;
+    std::vector<uint32_t> G(144 * nxt);
+    for (uint64_t g = 0; g < nxt; ++g) fp12_prod_lane(g, F.data(), cur, G.data(), nxt, 16);
+    F.swap(G);
+    cur = nxt;
+  }
+  bool any = false;
+  for (uint64_t i = 0; i < n; ++i) any = any || status[i] == RLC_PENDING;
+  bool pass = true;
+  if (any) {
+    fp12 f;
+    if (nch)
+      soa_load<144>(&f.c0.c0.c0.v[0], F.data(), 1, 0);
+    else
+      fp12_set_one(f);
+    if (!jac_is_inf(S)) {
+      g1a P[1];
+      g2a Q[1];
+      P[0].x = G1_GEN_X;
+      P[0].y = G1_NEG_GEN_Y;
+      jac_to_aff(Q[0], S);
+      fp12 g;
+      miller_loop_multi<1>(g, P, Q, 1);
+      fp12 x = f;
+      fp12_mul(f, x, g);
+    }
+    fp12 e;
+    final_exponentiation(e, f);
+    pass = fp12_is_one(e);
+  }
+  for (uint64_t i = 0; i < n; ++i) rlcb_mark_lane(i, n, pass, status, pts.data(), sc.data(), rsig.data());
+  *passed = pass ? 1 : 0;
+  mark(4);
+  const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
+  std::vector<int32_t> win(n_win ? n_win : 1);
+  std::vector<uint32_t> list;
+  for (uint64_t w = 0; w < n_win; ++w)
+    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
+      for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
+        if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
+  for (uint32_t i : list) rlc_fallback_lane(i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status);
+  mark(5);
+  return 0;
+}

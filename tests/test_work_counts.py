@@ -59,3 +59,25 @@ def test_bench_rlc_stage_counts_match():
     pks, msgs, sigs, _ = validator_batch(host_sign(L), host_pk(L), 4, 4, seed=3, bad=(1, 9))
     stats, cnt = run(pks, msgs, sigs)
     assert abs(cnt[3] / stats[2] - want["fallback"]) / want["fallback"] < 0.03
+
+
+def test_bench_rlcb_stage_counts_match():
+    """bench.RLCB_FPMUL (the batch-wide check's unit) against the host build of its stages."""
+    import bench
+    from tests.rlc_cases import message_table, validator_batch
+    from tests.test_rlc_host import host_pk, host_sign
+    L = lib()
+    pks, msgs, sigs, _ = validator_batch(host_sign(L), host_pk(L), 16, 4, seed=5)  # 64 items, 4 chunks of 4 runs
+    table, idx = message_table(msgs)
+    n = len(pks)
+    offs = (ctypes.c_uint64 * (len(table) + 1))(*[32 * i for i in range(len(table) + 1)])
+    st = (ctypes.c_int32 * n)()
+    passed = ctypes.c_int32()
+    cnt = (ctypes.c_uint64 * 6)()
+    arr = (ctypes.c_uint32 * n)(*idx)
+    L.ht_rlcb_verify(b"".join(pks), b"".join(sigs), arr, ctypes.c_uint64(n), b"".join(table), offs,
+                     ctypes.c_uint64(len(table)), bytes(32), st, ctypes.byref(passed), cnt)
+    assert passed.value == 1 and cnt[5] == 0  # decided by the batch-wide check alone
+    want = bench.RLCB_FPMUL
+    assert abs(cnt[0] / n - want["item"]) / want["item"] < 0.02
+    assert abs(cnt[3] / 4 - want["chunk_4runs"]) / want["chunk_4runs"] < 0.02
