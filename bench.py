@@ -441,12 +441,10 @@ def main():
         d_vst = torch.full((G,), -1, dtype=torch.int32, device=dev)
         node_aggs = [None, None]
 
-        def tstep():
-            rc = lib.hipbls_threshold_aggregate_batch_device(d_psig.data_ptr(), d_pid.data_ptr(), d_poff.data_ptr(), G,
-                                                             len(pids), d_agg.data_ptr(), d_gst.data_ptr(), sp)
-            assert rc == 0
-            rc = lib.hipbls_verify_batch_device(d_dpk.data_ptr(), d_dmsg.data_ptr(), d_doff.data_ptr(),
-                                                d_agg.data_ptr(), G, d_vst.data_ptr(), sp)
+        def tstep():  # sigagg in one call: aggregate + Verify of each aggregate against the DV root key
+            rc = lib.hipbls_threshold_aggregate_verify_batch_device(
+                d_psig.data_ptr(), d_pid.data_ptr(), d_poff.data_ptr(), G, len(pids), d_dpk.data_ptr(),
+                d_dmsg.data_ptr(), d_doff.data_ptr(), d_agg.data_ptr(), d_gst.data_ptr(), d_vst.data_ptr(), sp)
             assert rc == 0
             if world > 1:
                 node_aggs[0] = gather_aggregates(d_agg, G_node)
@@ -649,7 +647,8 @@ def main():
             "verified_partial_sigs_per_s_pubshare_table": round(keys_rate, 1) if keys_rate else None,
             "threshold_aggregates_per_s": round(tagg, 1) if tagg else None,
             "threshold_aggregate_workload": "C3: %d validators per GPU x 7-of-10 Lagrange in G2 + Verify of each "
-                                            "aggregate; aggregates and bitmap all-gathered" % args.tagg_groups
+                                            "aggregate (hipbls_threshold_aggregate_verify_batch_device, sigagg in one "
+                                            "call); aggregates and bitmap all-gathered" % args.tagg_groups
             if tagg else None,
         }
         if c5:

@@ -607,6 +607,66 @@ int launch_tagg(const uint8_t* d_sigs, const int64_t* d_ids, const uint64_t* d_g
   return ws_end(s);
 }
 
+// sigagg in one call: ThresholdAggregate on sub[0] while sub[1] decodes the validators' root keys and hashes their
+// messages; the caller's stream joins both and runs the pairing checks on the aggregates (kernels.h, k_tagg_sum_v).
+int launch_tagg_verify(const uint8_t* d_sigs, const int64_t* d_ids, const uint64_t* d_goffs, uint64_t n_groups,
+                       uint64_t n_parts, const uint8_t* d_dvpks, const uint8_t* d_msgs, const uint64_t* d_moffs,
+                       uint8_t* d_out, int32_t* d_astatus, int32_t* d_vstatus, hipStream_t s) {
+  Context& c = g_ctx;
+  if (n_groups == 0) return HIPBLS_OK;
+  int rc = ensure_rlc_streams();
+  if (rc) return rc;
+  HIP_TRY(c.b_pts.ensure((n_parts ? n_parts : 1) * 72 * 4));
+  HIP_TRY(c.b_pst.ensure((n_parts ? n_parts : 1) * 4));
+  HIP_TRY(c.v_ws.ensure(n_groups * 120 * 4));
+  HIP_TRY(c.b_aux.ensure(n_groups * 4));
+  uint32_t* ws = (uint32_t*)c.v_ws.p;
+  int32_t* agg_inf = (int32_t*)c.b_aux.p;
+  hipStream_t s0 = c.sub[0], s1 = c.sub[1];
+  rc = ws_begin(s);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c.ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(s0, c.ev_fork, 0));
+  HIP_TRY(hipStreamWaitEvent(s1, c.ev_fork, 0));
+  if (n_parts) {
+    rc = timed("tagg_scale", s0, [&] {
+      hipLaunchKernelGGL(k_tagg_scale, dim3((unsigned)grid_for(n_parts)), dim3(kBlock), 0, s0, d_sigs, d_ids, d_goffs,
+                         n_groups, n_parts, (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);
+    });
+    if (rc) return rc;
+  }
+  rc = timed("tagg_sum", s0, [&] {
+    hipLaunchKernelGGL(k_tagg_sum_v, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s0,
+                       (const uint32_t*)c.b_pts.p, (const int32_t*)c.b_pst.p, d_goffs, n_groups, n_parts, d_out,
+                       d_astatus, ws, agg_inf);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c.ev_join[0], s0));
+  rc = timed("tv_prep_pk", s1, [&] {
+    hipLaunchKernelGGL(k_tv_prep_pk, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s1, d_dvpks, d_msgs, d_moffs,
+                       n_groups, ws, d_vstatus);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c.ev_join[1], s1));
+  HIP_TRY(hipStreamWaitEvent(s, c.ev_join[0], 0));
+  HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
+  hipLaunchKernelGGL(k_tv_join, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s, n_groups,
+                     (const int32_t*)d_astatus, (const int32_t*)agg_inf, d_vstatus);
+  HIP_TRY(hipGetLastError());
+  if (use_pairs(n_groups, kLg2MaxVerify))
+    rc = timed("verify_pair_lg2", s, [&] {
+      hipLaunchKernelGGL(k_verify_pair_lg2, dim3((unsigned)grid_for(2 * n_groups)), dim3(kBlock), 0, s,
+                         (const uint32_t*)ws, n_groups, d_vstatus);
+    });
+  else
+    rc = timed("verify_pair_single", s, [&] {
+      hipLaunchKernelGGL(k_verify_pair_single, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s,
+                         (const uint32_t*)ws, n_groups, d_vstatus);
+    });
+  if (rc) return rc;
+  return ws_end(s);
+}
+
 int launch_fav(const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_goff, uint64_t n_groups, const uint8_t* d_sigs,
                const uint8_t* d_msgs, const uint64_t* d_moffs, int32_t* d_status, hipStream_t s) {
   Context& c = g_ctx;
@@ -1080,6 +1140,66 @@ int hipbls_threshold_aggregate_batch(const uint8_t* sigs, const int64_t* share_i
   HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
   HIP_TRY(hipStreamSynchronize(c.stream));
   return HIPBLS_OK;
+}
+
+int hipbls_threshold_aggregate_verify_batch(const uint8_t* sigs, const int64_t* share_idx,
+                                            const uint64_t* group_offsets, uint64_t n_groups, const uint8_t* dv_pks,
+                                            const uint8_t* msgs, const uint64_t* msg_offsets, uint8_t* out_sigs,
+                                            int32_t* agg_status, int32_t* verify_status) {
+  if (n_groups == 0) return HIPBLS_OK;
+  if (!group_offsets || !dv_pks || !msg_offsets || !out_sigs || !agg_status || !verify_status ||
+      mul_overflows(n_groups, 120 * 4))
+    return arg_err("bad arguments");
+  if (group_offsets[0] != 0) return arg_err("group_offsets[0] != 0");
+  for (uint64_t g = 0; g < n_groups; ++g)
+    if (group_offsets[g + 1] < group_offsets[g]) return arg_err("decreasing group offsets");
+  if (!offsets_ok(msg_offsets, n_groups)) return arg_err("bad message offsets");
+  const uint64_t n_parts = group_offsets[n_groups];
+  const uint64_t msg_total = msg_offsets[n_groups];
+  if (n_parts && (!sigs || !share_idx)) return arg_err("null partials");
+  if (msg_total && !msgs) return arg_err("null messages");
+  if (mul_overflows(n_parts, 288)) return arg_err("too many partials");
+  ENTER();
+  Context& c = g_ctx;
+  HIP_TRY(c.b_sig.ensure((n_parts ? n_parts : 1) * 96));
+  HIP_TRY(c.b_ids.ensure((n_parts ? n_parts : 1) * 8));
+  HIP_TRY(c.b_off.ensure((n_groups + 1) * 8));
+  HIP_TRY(c.b_pk.ensure(n_groups * 48));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_kidx.ensure((n_groups + 1) * 8));  // message offsets
+  HIP_TRY(c.b_out.ensure(n_groups * 96));
+  HIP_TRY(c.b_st.ensure(n_groups * 8));          // aggregate statuses, then verify statuses
+  if (n_parts) {
+    HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_parts * 96, hipMemcpyHostToDevice, c.stream));
+    HIP_TRY(hipMemcpyAsync(c.b_ids.p, share_idx, n_parts * 8, hipMemcpyHostToDevice, c.stream));
+  }
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, group_offsets, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_pk.p, dv_pks, n_groups * 48, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_kidx.p, msg_offsets, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  int32_t* ast = (int32_t*)c.b_st.p;
+  int32_t* vst = ast + n_groups;
+  int rc = launch_tagg_verify((const uint8_t*)c.b_sig.p, (const int64_t*)c.b_ids.p, (const uint64_t*)c.b_off.p,
+                              n_groups, n_parts, (const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p,
+                              (const uint64_t*)c.b_kidx.p, (uint8_t*)c.b_out.p, ast, vst, c.stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out_sigs, c.b_out.p, n_groups * 96, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipMemcpyAsync(agg_status, ast, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipMemcpyAsync(verify_status, vst, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int hipbls_threshold_aggregate_verify_batch_device(const uint8_t* d_sigs, const int64_t* d_share_idx,
+                                                   const uint64_t* d_group_offsets, uint64_t n_groups,
+                                                   uint64_t n_parts, const uint8_t* d_dv_pks, const uint8_t* d_msgs,
+                                                   const uint64_t* d_msg_offsets, uint8_t* d_out_sigs,
+                                                   int32_t* d_agg_status, int32_t* d_verify_status, void* stream) {
+  if (n_groups == 0) return HIPBLS_OK;
+  if (mul_overflows(n_parts, 288) || mul_overflows(n_groups, 120 * 4)) return arg_err("too many items");
+  ENTER();
+  return launch_tagg_verify(d_sigs, d_share_idx, d_group_offsets, n_groups, n_parts, d_dv_pks, d_msgs, d_msg_offsets,
+                            d_out_sigs, d_agg_status, d_verify_status, pick(stream));
 }
 
 int hipbls_threshold_aggregate_batch_device(const uint8_t* d_sigs, const int64_t* d_share_idx,

@@ -184,6 +184,109 @@ __global__ void __launch_bounds__(kBlock) k_tagg_sum(const uint32_t* __restrict_
   status[g] = st;
 }
 
+// ---------------------------------------------------------------- sigagg: aggregate + Verify in one call
+// core/sigagg/sigagg.go:138-159 threshold-aggregates each validator's partials and verifies the aggregate
+// against the validator's root pubkey.  hipbls_threshold_aggregate_verify_batch fuses the two: the key decode and
+// H(m) (k_tv_prep_pk) run beside the aggregation, the group sum hands its point straight to the pairing check
+// (k_tagg_sum_v: the 96-byte encoding is still written, and decompressing it would return the same point, which
+// is in G2 by construction), so the aggregate is never decompressed or subgroup-checked again.
+// ws: the lane-pair Verify layout (pk 24 words, H(m) 48, sig 48; SoA over the groups).
+
+// Stage 2 of ThresholdAggregate (k_tagg_sum) that also leaves the affine aggregate in ws (sig slot) and
+// agg_inf[g] = 1 when it is the point at infinity.
+__global__ void __launch_bounds__(kBlock) k_tagg_sum_v(const uint32_t* __restrict__ pts,
+                                                       const int32_t* __restrict__ pstat,
+                                                       const uint64_t* __restrict__ goffs, uint64_t n_groups,
+                                                       uint64_t n_parts, uint8_t* __restrict__ out,
+                                                       int32_t* __restrict__ status, uint32_t* __restrict__ ws,
+                                                       int32_t* __restrict__ agg_inf) {
+  const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  const uint64_t g0 = goffs[g], g1 = goffs[g + 1];
+  int st = g1 > g0 ? HIPBLS_OK : HIPBLS_ERR_COMBINE;
+  for (uint64_t k = g0; k < g1; ++k)
+    if (pstat[k] == HIPBLS_ERR_SIGNATURE) st = HIPBLS_ERR_SIGNATURE;
+  if (st == HIPBLS_OK)
+    for (uint64_t k = g0; k < g1; ++k)
+      if (pstat[k] != HIPBLS_OK) st = pstat[k];
+  g2j acc;
+  jac_set_inf(acc);
+  if (st == HIPBLS_OK) {
+    for (uint64_t k = g0; k < g1; ++k) {
+      g2j p;
+      soa_load<72>(&p.x.c0.v[0], pts, n_parts, k);
+      g2j x = acc, y;
+      jac_add(y, x, p);
+      acc = y;
+    }
+  }
+  uint8_t sig[96];
+  g2_compress(sig, acc);
+  for (int b = 0; b < 96; ++b) out[96 * g + b] = st == HIPBLS_OK ? sig[b] : (uint8_t)0;
+  status[g] = st;
+  const bool inf = jac_is_inf(acc);
+  g2a a;
+  if (inf) {
+    fp2_set_zero(a.x);
+    fp2_set_zero(a.y);
+  } else {
+    jac_to_aff(a, acc);
+  }
+  soa_store<48>(ws + 72 * n_groups, n_groups, g, &a.x.c0.v[0]);
+  agg_inf[g] = inf ? 1 : 0;
+}
+
+// Verify prep of the key side (one lane per group, beside the aggregation): decode + subgroup-check the
+// validator's root pubkey, hash its message; vstatus = ERR_PUBKEY / ERR_VERIFY (identity key) or pending.
+__global__ void __launch_bounds__(kBlock) k_tv_prep_pk(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ msgs,
+                                                       const uint64_t* __restrict__ offs, uint64_t n,
+                                                       uint32_t* __restrict__ ws, int32_t* __restrict__ vstatus) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a pk;
+  const int dp = g1_decompress(pk, pks + 48 * i, true);
+  int st = RLC_PENDING;
+  if (dp == DEC_BAD)
+    st = HIPBLS_ERR_PUBKEY;
+  else if (dp == DEC_INF)
+    st = HIPBLS_ERR_VERIFY;
+  if (st == RLC_PENDING) {
+    const uint64_t o0 = offs[i], o1 = offs[i + 1];
+    g2j hj;
+    hash_to_g2(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43);
+    g2a hm;
+    jac_to_aff(hm, hj);
+    soa_store<24>(ws, n, i, &pk.x.v[0]);
+    soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);
+  }
+  vstatus[i] = st;
+}
+
+// Join: a group whose aggregation failed reports that status for its Verify too; otherwise the key's status
+// stands (Verify checks the key first), and an aggregate at infinity is "signature not verified".
+__global__ void __launch_bounds__(kBlock) k_tv_join(uint64_t n, const int32_t* __restrict__ astatus,
+                                                    const int32_t* __restrict__ agg_inf, int32_t* __restrict__ vstatus) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (astatus[i] != HIPBLS_OK)
+    vstatus[i] = astatus[i];
+  else if (vstatus[i] == RLC_PENDING && agg_inf[i])
+    vstatus[i] = HIPBLS_ERR_VERIFY;
+}
+
+// One lane per item on the lane-pair Verify layout (for batches too large for lane pairs).
+__global__ void __launch_bounds__(kBlock) k_verify_pair_single(const uint32_t* __restrict__ ws, uint64_t n,
+                                                               int32_t* __restrict__ status) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != RLC_PENDING) return;
+  g1a pk;
+  g2a hm, sig;
+  soa_load<24>(&pk.x.v[0], ws, n, i);
+  soa_load<48>(&hm.x.c0.v[0], ws + 24 * n, n, i);
+  soa_load<48>(&sig.x.c0.v[0], ws + 72 * n, n, i);
+  status[i] = pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+}
+
 // G1 decode of many public keys (FastAggregateVerify): affine SoA (24 words) + code per key
 __global__ void __launch_bounds__(kBlock) k_g1_decode(const uint8_t* __restrict__ pks, uint64_t n,
                                                       uint32_t* __restrict__ pts, int32_t* __restrict__ code) {

@@ -66,6 +66,10 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_set_timing": ([ctypes.c_int], ctypes.c_int),
         "hipbls_set_pair_mode": ([ctypes.c_int], ctypes.c_int),
         "hipbls_rlc_set_mode": ([ctypes.c_int], ctypes.c_int),
+        "hipbls_threshold_aggregate_verify_batch": ([u8p, i64p, u64p, u64, u8p, u8p, u64p, u8p, i32p, i32p],
+                                                    ctypes.c_int),
+        "hipbls_threshold_aggregate_verify_batch_device": ([vp, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, vp],
+                                                           ctypes.c_int),
         "hipbls_rlc_batch_stats": ([u64p, u64p, i32p], ctypes.c_int),
         "hipbls_verify": ([u8p, u8p, u64, u8p, i32p], ctypes.c_int),
         "hipbls_verify_submit": ([u8p, u8p, u64, u8p, u64p], ctypes.c_int),
@@ -129,7 +133,8 @@ def exported_symbols() -> List[str]:
         "hipbls_current_device", "hipbls_set_timing", "hipbls_verify", "hipbls_verify_submit", "hipbls_verify_wait",
         "hipbls_queue_config", "hipbls_queue_stats", "hipbls_verify_signed_data_batch", "hipbls_aggregate_device",
         "hipbls_hcache_config", "hipbls_hcache_stats", "hipbls_set_pair_mode",
-        "hipbls_rlc_set_mode", "hipbls_rlc_batch_stats",
+        "hipbls_rlc_set_mode", "hipbls_rlc_batch_stats", "hipbls_threshold_aggregate_verify_batch",
+        "hipbls_threshold_aggregate_verify_batch_device",
     ]
 
 
@@ -410,6 +415,43 @@ class HipBLS:
             else:
                 res.append(TBLSError("cannot combine signatures"))
         return res
+
+    def batch_threshold_aggregate_verify(self, groups: Sequence[Mapping[int, bytes]], dv_pks: Sequence[bytes],
+                                         msgs: Sequence[bytes]):
+        """core/sigagg in one call (sigagg.go:138-159): ThresholdAggregate of each group and Verify of the aggregate
+        against the validator's root key over its message.  Returns (aggregates: bytes or TBLSError per group,
+        verify statuses: OK / ERR_PUBKEY / ERR_VERIFY, or the aggregation's status when it failed)."""
+        n_groups = len(groups)
+        if not (len(dv_pks) == len(msgs) == n_groups):
+            raise ValueError("mismatching lengths")
+        _check_lengths("public keys", dv_pks, 48)
+        offs = (ctypes.c_uint64 * (n_groups + 1))()
+        ids, sigs = [], []
+        for g, grp in enumerate(groups):
+            offs[g] = len(ids)
+            for idx, sg in grp.items():
+                if len(sg) != 96:
+                    raise ValueError("bad signature length")
+                ids.append(_go_int(idx))
+                sigs.append(bytes(sg))
+        offs[n_groups] = len(ids)
+        arr = (ctypes.c_int64 * max(len(ids), 1))(*ids)
+        blob, moffs = _offsets([bytes(m) for m in msgs])
+        out = ctypes.create_string_buffer(96 * max(n_groups, 1))
+        ast = _status_array(n_groups)
+        vst = _status_array(n_groups)
+        _check(self.lib.hipbls_threshold_aggregate_verify_batch(b"".join(sigs), arr, offs, n_groups, b"".join(dv_pks),
+                                                                blob, moffs, out, ast, vst), self.lib)
+        res = []
+        raw = out.raw
+        for g in range(n_groups):
+            if ast[g] == OK:
+                res.append(raw[96 * g:96 * g + 96])
+            elif ast[g] == ERR_SIGNATURE:
+                res.append(TBLSError("cannot unmarshal signature into Herumi signature"))
+            else:
+                res.append(TBLSError("cannot combine signatures"))
+        return res, list(vst)[:n_groups]
 
     def verify_aggregate(self, shares: Sequence[bytes], signature: bytes, data: bytes) -> None:
         """herumi.go:315-339 (FastAggregateVerify)."""

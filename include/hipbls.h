@@ -58,7 +58,7 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 7
+#define HIPBLS_ABI_VERSION 8
 int hipbls_abi_version(void);
 
 /* Select the HIP device used by the calling process (one process per GPU); idempotent.
@@ -203,6 +203,20 @@ int hipbls_hcache_stats(uint64_t* hits, uint64_t* misses, uint64_t* entries);
 int hipbls_verify_batch_device(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
                                const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream);
 /* n_parts = group_offsets[n_groups], passed explicitly so the call never reads device memory. */
+/* core/sigagg (sigagg.go:138-159) in one call: ThresholdAggregate of every group (as
+ * hipbls_threshold_aggregate_batch: out_sigs, agg_status) and Verify(dv_pks[g], msg g, out_sigs[g]) of each
+ * aggregate (verify_status, as hipbls_verify_batch).  A group whose aggregation failed reports its aggregation
+ * status in verify_status too.  The key decode and hash run beside the aggregation, and the aggregate goes to the
+ * pairing check without being decompressed again: the same verdicts as the two calls, in less time. */
+int hipbls_threshold_aggregate_verify_batch(const uint8_t* sigs, const int64_t* share_idx,
+                                            const uint64_t* group_offsets, uint64_t n_groups, const uint8_t* dv_pks,
+                                            const uint8_t* msgs, const uint64_t* msg_offsets, uint8_t* out_sigs,
+                                            int32_t* agg_status, int32_t* verify_status);
+int hipbls_threshold_aggregate_verify_batch_device(const uint8_t* d_sigs, const int64_t* d_share_idx,
+                                                   const uint64_t* d_group_offsets, uint64_t n_groups,
+                                                   uint64_t n_parts, const uint8_t* d_dv_pks, const uint8_t* d_msgs,
+                                                   const uint64_t* d_msg_offsets, uint8_t* d_out_sigs,
+                                                   int32_t* d_agg_status, int32_t* d_verify_status, void* stream);
 int hipbls_threshold_aggregate_batch_device(const uint8_t* d_sigs, const int64_t* d_share_idx,
                                             const uint64_t* d_group_offsets, uint64_t n_groups, uint64_t n_parts,
                                             uint8_t* d_out_sigs, int32_t* d_status, void* stream);

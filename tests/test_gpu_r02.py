@@ -413,3 +413,49 @@ def test_cluster_locks_bulk_verify(impl, kat):
         pks.append(h(v["distributed_public_key"]))
         sigs.append(h(br["signature"]))
     assert impl.verify_signed_data_status(pks, objs, [domain] * len(pks), sigs) == [0] * len(pks)
+
+
+# ---------------------------------------------------------------- sigagg in one call (sigagg.go:138-159)
+def test_threshold_aggregate_verify_fused_equals_two_calls(impl):
+    """hipbls_threshold_aggregate_verify_batch == batch_threshold_aggregate + batch_verify_status of the
+    aggregates, on honest groups, a failing aggregation (id 0, bad partial), a wrong root key, a wrong message,
+    an identity root key and an all-infinity group (aggregate at infinity)."""
+    from charon_amd.tbls import TBLSError
+    rng = random.Random(404)
+    groups, dvpks, msgs = [], [], []
+    secrets_ = []
+    for g in range(40):
+        secret = rng.randrange(1, R_ORDER)
+        tail = [rng.randrange(R_ORDER) for _ in range(2)]
+        ids = rng.sample(range(1, 9), 3)
+        sh = _shares_at(secret, tail, ids)
+        root = rng.randbytes(32)
+        sigs, _ = impl.sign_batch([sh[i] for i in ids], [root] * 3)
+        groups.append(dict(zip(ids, sigs)))
+        secrets_.append(secret)
+        msgs.append(root)
+    dvpks, _ = impl.secret_to_public_key_batch([s.to_bytes(32, "big") for s in secrets_])
+    dvpks = list(dvpks)
+    groups[3] = {0: list(groups[3].values())[0], 5: list(groups[3].values())[1]}       # id 0: cannot combine
+    k4 = list(groups[4])[0]
+    bad = bytearray(groups[4][k4])
+    bad[0] &= 0x7F
+    groups[4] = dict(groups[4])
+    groups[4][k4] = bytes(bad)                                                          # undecodable partial
+    dvpks[5] = dvpks[6]                                                                 # wrong root key
+    msgs[7] = rng.randbytes(32)                                                         # wrong message
+    dvpks[8] = b"\xc0" + bytes(47)                                                      # identity key
+    groups[9] = {1: b"\xc0" + bytes(95), 2: b"\xc0" + bytes(95)}                       # aggregate = infinity
+    bad_pk = bytearray(dvpks[10])
+    bad_pk[0] &= 0x7F
+    dvpks[10] = bytes(bad_pk)                                                           # undecodable root key
+    res, vst = impl.batch_threshold_aggregate_verify(groups, dvpks, msgs)
+    want_res = impl.batch_threshold_aggregate(groups)
+    assert [r if isinstance(r, bytes) else str(r) for r in res] == \
+        [r if isinstance(r, bytes) else str(r) for r in want_res]
+    ok = [g for g, r in enumerate(want_res) if isinstance(r, bytes)]
+    want_v = impl.batch_verify_status([dvpks[g] for g in ok], [msgs[g] for g in ok], [want_res[g] for g in ok])
+    assert [vst[g] for g in ok] == want_v
+    assert vst[3] == 5 and vst[4] == 2  # aggregation statuses carried over
+    assert vst[5] == 3 and vst[7] == 3 and vst[8] == 3 and vst[9] == 3 and vst[10] == 1
+    assert sum(1 for v in vst if v == 0) == 40 - 7
