@@ -25,6 +25,14 @@ __global__ void __launch_bounds__(64) k_op(const uint32_t* in, uint32_t* out, ui
   g1a P;
   P.x = f.c0.c0.c0;
   P.y = f.c0.c0.c1;
+  uint8_t valid96[96];
+  if (K == 25) {  // a valid compressed G2 point per lane (outside the timed loop)
+    uint8_t m[32];
+    for (int b = 0; b < 32; ++b) m[b] = (uint8_t)(lane + 7 * b);
+    g2j hj;
+    hash_to_g2(hj, m, 32, DST_POP, 43);
+    g2_compress(valid96, hj);
+  }
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
     if (K == 0) fp_mul(f.c0.c0.c0, f.c0.c0.c0, f.c0.c0.c1);
@@ -85,6 +93,39 @@ __global__ void __launch_bounds__(64) k_op(const uint32_t* in, uint32_t* out, ui
       f.c0.c1.c0.v[1] ^= g2_in_subgroup(pj) ? 1u : 0u;
       T.x = T.y;
     }
+    if (K == 23 || K == 24) {  // g2_decompress without the square root (23) / with it (24), inlined here
+      uint8_t b[96];
+      b[0] = 0xa0;
+      for (int k = 1; k < 96; ++k) b[k] = (uint8_t)(f.c0.c0.c0.v[k % 12] >> (k & 24));
+      uint8_t buf[96];
+      for (int i = 0; i < 96; ++i) buf[i] = b[i];
+      buf[0] &= 0x1f;
+      fp2 x;
+      fp_plain_from_be48(x.c1, buf);
+      fp_plain_from_be48(x.c0, buf + 48);
+      int st = (!fp_plain_lt_p(x.c0) || !fp_plain_lt_p(x.c1)) ? 1 : 0;
+      fp_to_mont(x.c0, x.c0);
+      fp_to_mont(x.c1, x.c1);
+      fp2 y2, y;
+      fp2_sqr(y2, x);
+      fp2_mul(y2, y2, x);
+      fp2_add(y2, y2, FP2_B2);
+      if (K == 24) {
+        if (!fp2_sqrt(y, y2)) st |= 2;
+      } else {
+        y = y2;
+      }
+      if (fp2_is_lex_largest(y)) fp2_neg(y, y);
+      f.c0.c0 = y;
+      f.c0.c1.c0.v[0] ^= (uint32_t)st;
+    }
+    if (K == 25) {
+      g2a a;
+      const int st = g2_decompress(a, valid96, false);
+      f.c0.c0 = a.x;
+      f.c0.c1.c0.v[0] ^= (uint32_t)st;
+      valid96[95] ^= (uint8_t)(a.y.c0.v[0] & 0);  // keep the input live per iteration
+    }
     if (K == 16) fp_pow(f.c0.c0.c0, f.c0.c0.c0, EXP_SQRT, 378);
     if (K == 18) {
       fp2 y;
@@ -131,14 +172,14 @@ static double median(uint64_t* h, int n) {
 }
 
 int main() {
-  constexpr int NOPS = 23;
+  constexpr int NOPS = 26;
   const char* names[NOPS] = {"fp_mul", "fp_add", "fp2_mul", "fp6_mul", "fp12_sqr", "fp12_mul", "fp12_mul_line2",
                            "fp12_cyclotomic_sqr", "miller_dbl_step", "jac_dbl<fp2>", "fp_sub",
                            "final_exponentiation", "fp12_cyc_exp_xabs", "miller_loop_n(2)", "hash_to_g2",
-                           "g2_decompress+subgroup", "fp_pow(sqrt)", "g1_decompress+subgroup", "fp2_sqrt", "g2_in_subgroup", "jac_mul_u64<fp>(|x|)", "g2_decompress(no sub)", "g2_in_subgroup(z=1)"};
+                           "g2_decompress+subgroup", "fp_pow(sqrt)", "g1_decompress+subgroup", "fp2_sqrt", "g2_in_subgroup", "jac_mul_u64<fp>(|x|)", "g2_decompress(no sub)", "g2_in_subgroup(z=1)", "g2dec parts w/o sqrt", "g2dec parts + sqrt", "g2_decompress(valid, no sub)"};
   // Fp products per op (host instrumented build: tests/test_work_counts.py); 0 = not a product count
-  const int products[NOPS] = {1, 0, 3, 18, 36, 54, 69, 18, 25, 16, 0, 8150, 1404, 10700, 5740, 2203, 458, 0, 0, 0, 0, 0, 0};
-  const int iters[NOPS] = {400, 400, 200, 40, 20, 20, 20, 40, 40, 40, 400, 1, 2, 1, 2, 4, 4, 4, 4, 4, 4, 4, 4};
+  const int products[NOPS] = {1, 0, 3, 18, 36, 54, 69, 18, 25, 16, 0, 8150, 1404, 10700, 5740, 2203, 458, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const int iters[NOPS] = {400, 400, 200, 40, 20, 20, 20, 40, 40, 40, 400, 1, 2, 1, 2, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4};
   uint32_t *d_in, *d_out;
   uint64_t* d_cyc;
   uint32_t h_in[4096];
@@ -151,7 +192,7 @@ int main() {
     for (int rep = 0; rep < 2; ++rep) {
       switch (k) {
 #define L(K) case K: hipLaunchKernelGGL(k_op<K>, dim3(1024), dim3(64), 0, 0, d_in, d_out, d_cyc, iters[K]); break;
-        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15) L(16) L(17) L(18) L(19) L(20) L(21) L(22)
+        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15) L(16) L(17) L(18) L(19) L(20) L(21) L(22) L(23) L(24) L(25)
       }
       if (hipDeviceSynchronize() != hipSuccess) return 2;
     }
