@@ -94,10 +94,16 @@ struct Context {
   uint64_t r_windows = 0;        // window count of the last RLC call (hipbls_rlc_stats)
   // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
   DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_FS, m_flag;
-  int32_t* rlcb_host_flag = nullptr;  // pinned copy of the last verdict
-  hipEvent_t rlcb_ev = nullptr, rlcb_ev_items = nullptr, rlcb_ev_msm = nullptr;
-  bool rlcb_pending = false;          // a verdict copy is in flight
-  int rlcb_last = -1;                 // last verdict read back: -1 none, 0 failed, 1 passed
+  // Verdicts come back through a ring of pinned slots, one per batch check in flight, so a launch only waits
+  // on the host when kRlcbSlots checks are still unread (never in the enqueue-only *_device paths otherwise).
+  static constexpr int kRlcbSlots = 8;
+  int32_t* rlcb_host_flag = nullptr;  // pinned, kRlcbSlots verdicts
+  hipEvent_t rlcb_ev[kRlcbSlots] = {};
+  hipEvent_t rlcb_ev_items = nullptr, rlcb_ev_msm = nullptr;
+  bool rlcb_pending[kRlcbSlots] = {};
+  uint64_t rlcb_seq[kRlcbSlots] = {};  // launch order of the check in each slot
+  uint64_t rlcb_next_seq = 0, rlcb_last_seq = 0;
+  int rlcb_last = -1;                 // newest verdict read back: -1 none, 0 failed, 1 passed
   int rlcb_skipped = 0;               // AUTO: calls run windows-only since the last failed batch check
   uint64_t rlcb_attempted = 0, rlcb_passed = 0;
   HCache hcache;
@@ -398,18 +404,25 @@ std::atomic<int> g_rlc_mode{HIPBLS_RLC_AUTO};
 constexpr uint64_t kRlcbMinItems = 1024;
 constexpr int kRlcbBackoff = 8;
 
-void rlcb_poll(bool wait) {
+// Reads back every verdict whose copy has landed; with wait_slot >= 0 (or wait_all) blocks on that slot first.
+void rlcb_poll(int wait_slot, bool wait_all = false) {
   Context& c = g_ctx;
-  if (!c.rlcb_pending) return;
-  if (wait) {
-    if (hipEventSynchronize(c.rlcb_ev) != hipSuccess) return;
-  } else if (hipEventQuery(c.rlcb_ev) != hipSuccess) {
-    return;
+  for (int k = 0; k < Context::kRlcbSlots; ++k) {
+    if (!c.rlcb_pending[k]) continue;
+    if (wait_all || k == wait_slot) {
+      if (hipEventSynchronize(c.rlcb_ev[k]) != hipSuccess) continue;
+    } else if (hipEventQuery(c.rlcb_ev[k]) != hipSuccess) {
+      continue;
+    }
+    c.rlcb_pending[k] = false;
+    const int v = c.rlcb_host_flag[k] ? 1 : 0;
+    c.rlcb_passed += (uint64_t)v;
+    if (c.rlcb_seq[k] >= c.rlcb_last_seq) {
+      c.rlcb_last_seq = c.rlcb_seq[k];
+      c.rlcb_last = v;
+      if (!v) c.rlcb_skipped = 0;
+    }
   }
-  c.rlcb_pending = false;
-  c.rlcb_last = *c.rlcb_host_flag ? 1 : 0;
-  c.rlcb_passed += (uint64_t)c.rlcb_last;
-  if (!c.rlcb_last) c.rlcb_skipped = 0;
 }
 
 bool use_rlc_batch(uint64_t n) {
@@ -417,7 +430,7 @@ bool use_rlc_batch(uint64_t n) {
   const int mode = g_rlc_mode.load();
   if (mode == HIPBLS_RLC_WINDOWS) return false;
   if (mode == HIPBLS_RLC_BATCH) return true;
-  rlcb_poll(false);
+  rlcb_poll(-1);
   if (n < kRlcbMinItems) return false;
   if (c.rlcb_last == 0 && c.rlcb_skipped < kRlcbBackoff) {
     ++c.rlcb_skipped;
@@ -440,14 +453,15 @@ int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t
   const uint64_t nch = (n + RLCB_C - 1) / RLCB_C;
   const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
   if (!c.rlcb_host_flag) {
-    HIP_TRY(hipHostMalloc((void**)&c.rlcb_host_flag, sizeof(int32_t), hipHostMallocDefault));
-    HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev, hipEventDisableTiming));
+    HIP_TRY(hipHostMalloc((void**)&c.rlcb_host_flag, Context::kRlcbSlots * sizeof(int32_t), hipHostMallocDefault));
+    for (int k = 0; k < Context::kRlcbSlots; ++k) HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_items, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_msm, hipEventDisableTiming));
   }
   int rc = ensure_rlc_streams();
   if (rc) return rc;
-  rlcb_poll(true);  // the pinned flag is about to be overwritten
+  const int slot = (int)(c.rlcb_next_seq % Context::kRlcbSlots);
+  rlcb_poll(slot);  // only blocks when kRlcbSlots verdicts are still in flight
   HIP_TRY(c.m_pts.ensure(npts * 48 * 4));
   HIP_TRY(c.m_sc.ensure(npts * 4));
   HIP_TRY(c.m_cnt.ensure((uint64_t)MSM_WINDOWS * MSM_NB * 4));
@@ -546,9 +560,10 @@ int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t
                        (const uint32_t*)pts, (const uint32_t*)sc, rsig);
   });
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(c.rlcb_host_flag, flag, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipEventRecord(c.rlcb_ev, s));
-  c.rlcb_pending = true;
+  HIP_TRY(hipMemcpyAsync(c.rlcb_host_flag + slot, flag, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(c.rlcb_ev[slot], s));
+  c.rlcb_pending[slot] = true;
+  c.rlcb_seq[slot] = ++c.rlcb_next_seq;
   c.rlcb_attempted += 1;
   // window + fallback stages over whatever is still pending (nothing when the batch check passed)
   int32_t* win = (int32_t*)c.r_win.p;
@@ -993,7 +1008,7 @@ int hipbls_rlc_set_mode(int mode) {
 int hipbls_rlc_batch_stats(uint64_t* attempted, uint64_t* passed, int32_t* last) {
   if (!attempted || !passed || !last) return arg_err("null output");
   ENTER();
-  rlcb_poll(true);
+  rlcb_poll(-1, true);
   *attempted = g_ctx.rlcb_attempted;
   *passed = g_ctx.rlcb_passed;
   *last = g_ctx.rlcb_last;

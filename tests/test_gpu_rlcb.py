@@ -135,3 +135,20 @@ def test_auto_policy_backs_off_after_a_failure(impl, keys):
         assert att == 0 and got == [0] * len(P)
     got, att, passed, last = _run(impl, RLC_AUTO, P, M, good)
     assert (att, passed, last) == (1, 1, 1) and got == [0] * len(P)
+
+
+def test_verdict_ring_wraps(impl, keys):
+    """More batch checks than verdict slots (8): every verdict is read back once, the newest one is `last`."""
+    from charon_amd.tbls import RLC_BATCH
+    sks, _ = keys
+    idx, P, M, S = _batch(impl, keys, 64, 4, 10)
+    impl.set_rlc_mode(RLC_BATCH)
+    a0, p0, _ = impl.rlc_batch_stats()
+    for _ in range(11):
+        assert impl.batch_verify_rlc_status(P, M, S, seed=bytes(32)) == [0] * len(P)
+    wrong, _ = impl.sign_batch([sks[(idx[0] + 1) % len(sks)]], [M[0]])
+    bad = [wrong[0]] + S[1:]
+    got = impl.batch_verify_rlc_status(P, M, bad, seed=bytes(32))
+    a1, p1, last = impl.rlc_batch_stats()
+    assert got[0] == 3 and got[1:] == [0] * (len(P) - 1)
+    assert (a1 - a0, p1 - p0, last) == (12, 11, 0)
