@@ -249,6 +249,8 @@ typedef uint32_t u32x12 __attribute__((ext_vector_type(12)));
 // Never called: hosts the routine's code (entered only at the local label).
 __device__ __attribute__((used, noinline)) static void bls_fp_asm_routines() {
   asm volatile("s_endpgm\n.p2align 6\n.type bls_fp_mul_rt,@function\nbls_fp_mul_rt:\n\t" BLS_FP_MUL_ASM_BODY
+               "\n\ts_setpc_b64 s[30:31]\n"
+               ".p2align 6\n.type bls_fp2_mul_rt,@function\nbls_fp2_mul_rt:\n\t" BLS_FP2_MUL_ASM_BODY
                "\n\ts_setpc_b64 s[30:31]\n");
 }
 #define BLS_ASM_CALL(fn)                                                                           \

@@ -140,6 +140,21 @@ BLS_HD BLS_INLINE void fp12_conj(fp12& r, const fp12& a) {
 // Frobenius x -> x^(p^j), j in {1,2,3}
 // Granger-Scott squaring for elements of the cyclotomic subgroup
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// Device: one asm routine (tools/gen_fp_asm.py gen_fp2_mul): each coefficient is a single Montgomery reduction of
+// a sum of two products, c1 = (a0 b1 + a1 b0)/R and c0 = (a0 b0 + a1 (p - b1))/R -- no Fp additions and two final
+// subtractions instead of Karatsuba's three reduced products, three subtractions and two sums.
+BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
+  u32x12 a0 = fp_to_vec(a.c0), a1 = fp_to_vec(a.c1), b0 = fp_to_vec(b.c0), b1 = fp_to_vec(b.c1), c0, c1;
+  asm volatile(BLS_ASM_CALL("bls_fp2_mul_rt")
+               : "+{v[0:11]}"(a0), "+{v[12:23]}"(a1), "+{v[24:35]}"(b0), "+{v[36:47]}"(b1), "={v[52:63]}"(c1),
+                 "={v[64:75]}"(c0)
+               :
+               : BLS_FP2_MUL_ASM_CLOBBERS, "s30", "s31", "scc");
+  fp_from_vec(r.c0, c0);
+  fp_from_vec(r.c1, c1);
+}
+#else
 BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
   // Karatsuba: 3 Fp products; the two sums only feed the third product, so they stay unreduced (fp_add_lazy)
   fp t0, t1, t2, s0, s1;
@@ -152,6 +167,7 @@ BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
   fp_sub(t2, t2, t0);
   fp_sub(r.c1, t2, t1);
 }
+#endif
 BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
   // (a0+a1)(a0-a1) + 2 a0 a1 u; the sum and difference only feed the product: unreduced
   fp s, d, m;

@@ -293,6 +293,95 @@ def gen_mul(e64_select=True):
 gen_mul32 = gen_mul  # name used by tools/gen_probe_bodies.py
 
 
+# ---------------------------------------------------------------- Fp2 product as two sums of products
+# (a0 + a1 u)(b0 + b1 u) = (a0 b0 - a1 b1) + (a0 b1 + a1 b0) u.  Each coefficient is ONE Montgomery reduction
+# of a sum of two 768-bit products (product scanning, reduction interleaved per column, as gen_mul):
+#   c1 = (a0 b1 + a1 b0) / R,   c0 = (a0 b0 + a1 (p - b1)) / R   (mod p)
+# 2 x 432 mads instead of the 3 x 288 of Karatsuba with three reduced products, and no Fp additions: the
+# Karatsuba sums, the three subtractions and one of the three final subtractions disappear.  For canonical
+# inputs each sum is < 2p^2 < pR, so one conditional subtraction makes each output canonical.
+# Registers: a0 = v[0:11], a1 = v[12:23], b0 = v[24:35], b1 = v[36:47] (all clobbered); c1 -> v[52:63],
+# c0 -> v[64:75]; v48-v51, s16-s28 and vcc clobbered.
+FP2_A0, FP2_A1, FP2_B0, FP2_B1, FP2_C1, FP2_C0 = 0, 12, 24, 36, 52, 64
+
+
+def _gen_sop(w, X, Y, Z, Wd, M):
+    """Appends r = (X*Y + Z*Wd)/2^384 mod p, in [0, 2p), to the stream w; the quotient digits m_i live in
+    M(i) and the result limb j overwrites M(j) (m_j is dead from column j + 12 on)."""
+    first = [True]
+    src2 = ["v[48:49]"]
+
+    def mac(x, y):
+        w("v_mad_u64_u32 v[48:49], vcc, %s, %s, %s" % (x, y, src2[0]))
+        src2[0] = "v[48:49]"
+        if first[0]:
+            w("v_addc_co_u32_e64 v51, vcc, 0, 0, vcc")
+            first[0] = False
+        else:
+            w("v_addc_co_u32_e32 v51, vcc, 0, v51, vcc")
+
+    def shift():
+        w("v_mov_b32 v50, v49")
+        src2[0] = "v[50:51]"
+        first[0] = True
+
+    Sp = lambda j: "s%d" % (16 + j)
+    w("v_mad_u64_u32 v[48:49], vcc, %s, %s, 0" % (X(0), Y(0)))
+    w("v_mov_b32 v51, 0")
+    first[0] = False
+    mac(Z(0), Wd(0))
+    w("v_mul_lo_u32 %s, v48, s28" % M(0))
+    mac(M(0), "s16")
+    shift()
+    for i in range(1, N32):
+        for j in range(i):
+            mac(X(j), Y(i - j))
+            mac(Z(j), Wd(i - j))
+            mac(M(j), Sp(i - j))
+        mac(X(i), Y(0))
+        mac(Z(i), Wd(0))
+        w("v_mul_lo_u32 %s, v48, s28" % M(i))
+        mac(M(i), "s16")
+        shift()
+    for i in range(N32, 2 * N32 - 1):
+        for j in range(i - N32 + 1, N32):
+            mac(X(j), Y(i - j))
+            mac(Z(j), Wd(i - j))
+            mac(M(j), Sp(i - j))
+        w("v_mov_b32 %s, v48" % M(i - N32))
+        shift()
+    w("v_mov_b32 %s, v50" % M(N32 - 1))
+
+
+def gen_fp2_mul():
+    PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
+    PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    V = lambda base: (lambda j: "v%d" % (base + j))
+    A0, A1, B0, B1, C1, C0 = (V(FP2_A0), V(FP2_A1), V(FP2_B0), V(FP2_B1), V(FP2_C1), V(FP2_C0))
+    out = []
+    w = out.append
+    for j in range(N32):
+        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
+    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    _gen_sop(w, A0, B1, A1, B0, C1)                    # c1 (raw, < 2p) in v[52:63]
+    for j in range(N32):                               # p into VGPRs (the carry chain reads vcc: one
+        w("v_mov_b32 %s, s%d" % (C0(j), 16 + j))       # constant-bus operand only)
+    w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (B1(0), C0(0), B1(0)))
+    for j in range(1, N32):                            # b1 <- p - b1 in (0, p]
+        w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (B1(j), C0(j), B1(j)))
+    _gen_sop(w, A0, B0, A1, B1, C0)                    # c0 (raw) in v[64:75]
+    for j in range(N32):
+        w("v_mov_b32 %s, s%d" % (A0(j), 16 + j))
+    for C in (C1, C0):                                 # canonical: keep c when c - p borrows
+        w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (A1(0), C(0), A0(0)))
+        for j in range(1, N32):
+            w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (A1(j), C(j), A0(j)))
+        w("v_subb_co_u32_e64 %s, vcc, 0, 0, vcc" % B0(0))
+        for j in range(N32):
+            w("v_bfi_b32 %s, %s, %s, %s" % (C(j), B0(0), C(j), A1(j)))
+    return out
+
+
 # ---------------------------------------------------------------- modular add / sub / neg
 # One asm block each, operands allocated by the compiler (positional: outputs r = %0-%11, t = %12-%23,
 # m = %24; inputs a = %25-%36, then b = %37-%48 and p = %49-%60, or p = %37-%48 for neg).  One VCC carry chain
@@ -402,13 +491,15 @@ def emulate_positional(body, outs, ins):
 
 
 # ---------------------------------------------------------------- CPU interpreter
-def emulate(body, a, b):
+def emulate(body, a, b, regs=None):
     """Interprets the instruction subset used above (one lane); a, b: 12 x 32-bit limbs.
-    Returns the 12 output limbs (v0..v11)."""
-    v, s = {}, {}
+    Returns the 12 output limbs (v0..v11).  With regs (a dict VGPR number -> value, updated in place)
+    the register file starts from regs instead of a in v0.. and b in v12.."""
+    v, s = ({}, {}) if regs is None else (regs, {})
     M32, M64 = 0xFFFFFFFF, (1 << 64) - 1
-    for j in range(N32):
-        v[j], v[12 + j] = a[j], b[j]
+    if regs is None:
+        for j in range(N32):
+            v[j], v[12 + j] = a[j], b[j]
 
     def rd(x):
         x = x.strip()
@@ -456,10 +547,13 @@ def emulate(body, a, b):
             r = rd(o[2]) - rd(o[3])
             wr(o[0], r)
             s["vcc"] = 1 if r < 0 else 0
-        elif op == "v_subb_co_u32_e32":
+        elif op in ("v_subb_co_u32_e32", "v_subb_co_u32_e64"):
             r = rd(o[2]) - rd(o[3]) - rd(o[4])
             wr(o[0], r)
             s["vcc"] = 1 if r < 0 else 0
+        elif op == "v_bfi_b32":
+            m = rd(o[1])
+            wr(o[0], (m & rd(o[2])) | (~m & M32 & rd(o[3])))
         elif op in ("v_cndmask_b32_e32", "v_cndmask_b32_e64"):
             wr(o[0], rd(o[2]) if rd(o[3]) else rd(o[1]))
         elif op == "v_lshrrev_b32":
@@ -535,6 +629,8 @@ def emit_header(path, bodies, extra=()):
         lines.append("")
     clob = ", ".join('"v%d"' % r for r in range(24, 40)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
     lines.append("#define BLS_FP_MUL_ASM_CLOBBERS %s" % clob)
+    clob2 = ", ".join('"v%d"' % r for r in range(48, 52)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
+    lines.append("#define BLS_FP2_MUL_ASM_CLOBBERS %s" % clob2)
     for name, body in extra:
         lines.append("")
         lines.append("// %s: %d instructions, positional operands (see tools/gen_fp_asm.py)" % (name, len(body)))
@@ -551,7 +647,8 @@ def main():
     mul = gen_mul()
     check(mul, mont=1 << 384, canonical=True)
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "fp_asm_gfx950.h")
-    emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul)],
+    fp2 = gen_fp2_mul()
+    emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul), ("BLS_FP2_MUL_ASM_BODY", fp2)],
                 extra=[("BLS_FP_ADD_ASM", gen_add()), ("BLS_FP_SUB_ASM", gen_sub()), ("BLS_FP_NEG_ASM", gen_sub(neg=True)),
                        ("BLS_FP_ADD_LAZY_ASM", gen_add_lazy()), ("BLS_FP_SUB_LAZY_ASM", gen_sub_lazy())])
     print("wrote %s: %d instructions" % (path, len(mul)))

@@ -114,3 +114,23 @@ def test_lazy_add_sub_blocks(kind):
         c = rnd.choice(cases)
         for x, y in ((got, got), (got, c), (c, got)):
             assert _val(g.emulate(mul, _limbs(x), _limbs(y))) == x * y * R_INV % g.P
+
+
+def test_fp2_product_routine():
+    """The device fp2_mul routine (BLS_FP2_MUL_ASM_BODY, gen_fp2_mul): emitted text == generator, and the interpreted
+    stream gives c0 = (a0 b0 - a1 b1)/R, c1 = (a0 b1 + a1 b0)/R mod p, canonical, on canonical operands with edges
+    (0, 1, p - 1: the p - b1 = p operand and the final-subtraction boundaries)."""
+    body = _macro_body("BLS_FP2_MUL_ASM_BODY")
+    assert body == g.gen_fp2_mul(), "fp_asm_gfx950.h is stale: rerun charon_amd/tools/gen_fp_asm.py"
+    cases = _cases(60, 41)
+    rnd = random.Random(42)
+    for t in range(250):
+        a0, a1, b0, b1 = (rnd.choice(cases) for _ in range(4))
+        regs = {}
+        for base, x in ((g.FP2_A0, a0), (g.FP2_A1, a1), (g.FP2_B0, b0), (g.FP2_B1, b1)):
+            regs.update({base + j: v for j, v in enumerate(_limbs(x))})
+        g.emulate(body, None, None, regs)
+        c0 = _val([regs[g.FP2_C0 + j] for j in range(12)])
+        c1 = _val([regs[g.FP2_C1 + j] for j in range(12)])
+        assert c0 == (a0 * b0 - a1 * b1) * R_INV % g.P, (t, hex(a0), hex(a1), hex(b0), hex(b1))
+        assert c1 == (a0 * b1 + a1 * b0) * R_INV % g.P, (t, hex(a0), hex(a1), hex(b0), hex(b1))
