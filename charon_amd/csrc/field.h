@@ -251,6 +251,8 @@ __device__ __attribute__((used, noinline)) static void bls_fp_asm_routines() {
   asm volatile("s_endpgm\n.p2align 6\n.type bls_fp_mul_rt,@function\nbls_fp_mul_rt:\n\t" BLS_FP_MUL_ASM_BODY
                "\n\ts_setpc_b64 s[30:31]\n"
                ".p2align 6\n.type bls_fp2_mul_rt,@function\nbls_fp2_mul_rt:\n\t" BLS_FP2_MUL_ASM_BODY
+               "\n\ts_setpc_b64 s[30:31]\n"
+               ".p2align 6\n.type bls_fp2_sqr_rt,@function\nbls_fp2_sqr_rt:\n\t" BLS_FP2_SQR_ASM_BODY
                "\n\ts_setpc_b64 s[30:31]\n");
 }
 #define BLS_ASM_CALL(fn)                                                                           \
@@ -405,7 +407,262 @@ BLS_HD BLS_INLINE void fp_mul_small(fp& r, const fp& a, uint32_t k) {
   r = acc;
 }
 
-BLS_HD BLS_INLINE void fp_inv(fp& r, const fp& a) { fp_pow(r, a, EXP_P_MINUS_2, 380); }
+// ---------------------------------------------------------------------------------- binary-GCD inversion
+// Pornin's optimized binary GCD ("Optimized Binary GCD for Modular Inversion", 2020, Algorithm 2) with k = 31:
+// 30 divsteps per outer iteration on 62-bit approximations (the low 30 bits and the top 32 bits of a and b at
+// the longer one's length), then one signed 2x2 update of the full a, b (30-bit limbs) and of u, v mod p with an
+// exact division by 2^30 (one Montgomery-style digit).  Invariant a = x u, b = x v (mod p); a reaches 0 and b = 1
+// within 2*381 - 1 = 761 divsteps, so 26 iterations of 30; an extra iteration is a no-op (a = 0 stays 0).
+// Every decision is a select on lane data: all lanes run the same instruction stream.  ~33k VALU per inversion
+// against ~300k for the Fermat power x^(p-2) (455 products); inverse of 0 is 0, like the power.
+// Result: x^-1 for the plain integer x = a_mont = aR, then one product by R^3 gives (aR)^-1 R^2 = a^-1 R.
+namespace gcd30 {
+static constexpr uint32_t M30 = 0x3fffffffu;
+static constexpr uint32_t P30[13] = {0x3fffaaabu, 0x27fbffffu, 0x153ffffbu, 0x2affffacu, 0x30f6241eu,
+                                     0x034a83dau, 0x112bf673u, 0x12e13ce1u, 0x2cd76477u, 0x1ed90d2eu,
+                                     0x29a4b1bau, 0x3a8e5ff9u, 0x001a0111u};
+static constexpr uint32_t PINV30 = 0x3ffcfffdu;  // -p^-1 mod 2^30
+static constexpr int ITERS = 27;
+
+// Lane masks as VGPR values and selects by v_bfi_b32.  Written as (non-volatile) asm on the device so the compiler
+// cannot turn "x & mask" back into a v_cndmask_b32_e32 on VCC, which issues at ~19 cycles on gfx950 against ~4.4
+// for v_bfi_b32 (profiles/r02_sel_probe.txt).
+#if defined(__HIP_DEVICE_COMPILE__)
+BLS_HD BLS_INLINE uint32_t mask_bit0(uint32_t x) {  // all ones if x is odd
+  uint32_t m;
+  asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(m) : "v"(x));
+  return m;
+}
+BLS_HD BLS_INLINE uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {  // m ? a : b, bitwise
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+#else
+BLS_HD BLS_INLINE uint32_t mask_bit0(uint32_t x) { return 0u - (x & 1u); }
+BLS_HD BLS_INLINE uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+#endif
+BLS_HD BLS_INLINE uint32_t mask_eq(uint32_t a, uint32_t b) {  // all ones if a == b (a ^ b < 2^31)
+  return (uint32_t)((int32_t)((a ^ b) - 1u) >> 31);
+}
+
+// One divstep on the 62-bit approximations a = (ah:al), b = (bh:bl) and the transition factors:
+//   a odd:  d = a - b;  b <- min(a, b);  a <- |d| / 2;  (f0, f1) <- (+-(f0 - f1), 2 (a < b ? f0 : f1))
+//   a even: a <- a / 2;  f1 <- 2 f1          (likewise g)
+// i.e. Pornin's "if a odd: if a < b: swap; a -= b" followed by the halving, without a branch or a VCC select.
+#if defined(__HIP_DEVICE_COMPILE__)
+BLS_HD BLS_INLINE void divstep(uint32_t& al, uint32_t& ah, uint32_t& bl, uint32_t& bh, uint32_t& f0, uint32_t& g0,
+                               uint32_t& f1, uint32_t& g1) {
+  uint32_t om, s, sw, dl, dh, t;
+  asm("v_bfe_i32 %[om], %[al], 0, 1\n\t"
+      "v_sub_co_u32_e32 %[dl], vcc, %[al], %[bl]\n\t"
+      "v_subb_co_u32_e32 %[dh], vcc, %[ah], %[bh], vcc\n\t"
+      "v_ashrrev_i32_e32 %[s], 31, %[dh]\n\t"
+      "v_and_b32_e32 %[sw], %[om], %[s]\n\t"
+      "v_xor_b32_e32 %[dl], %[dl], %[s]\n\t"
+      "v_xor_b32_e32 %[dh], %[dh], %[s]\n\t"
+      "v_sub_co_u32_e32 %[dl], vcc, %[dl], %[s]\n\t"
+      "v_subb_co_u32_e32 %[dh], vcc, %[dh], %[s], vcc\n\t"
+      "v_bfi_b32 %[bl], %[sw], %[al], %[bl]\n\t"
+      "v_bfi_b32 %[bh], %[sw], %[ah], %[bh]\n\t"
+      "v_bfi_b32 %[al], %[om], %[dl], %[al]\n\t"
+      "v_bfi_b32 %[ah], %[om], %[dh], %[ah]\n\t"
+      "v_alignbit_b32 %[al], %[ah], %[al], 1\n\t"
+      "v_lshrrev_b32_e32 %[ah], 1, %[ah]\n\t"
+      "v_sub_u32_e32 %[t], %[f0], %[f1]\n\t"
+      "v_xor_b32_e32 %[t], %[t], %[sw]\n\t"
+      "v_sub_u32_e32 %[t], %[t], %[sw]\n\t"
+      "v_bfi_b32 %[f1], %[sw], %[f0], %[f1]\n\t"
+      "v_lshlrev_b32_e32 %[f1], 1, %[f1]\n\t"
+      "v_bfi_b32 %[f0], %[om], %[t], %[f0]\n\t"
+      "v_sub_u32_e32 %[t], %[g0], %[g1]\n\t"
+      "v_xor_b32_e32 %[t], %[t], %[sw]\n\t"
+      "v_sub_u32_e32 %[t], %[t], %[sw]\n\t"
+      "v_bfi_b32 %[g1], %[sw], %[g0], %[g1]\n\t"
+      "v_lshlrev_b32_e32 %[g1], 1, %[g1]\n\t"
+      "v_bfi_b32 %[g0], %[om], %[t], %[g0]"
+      : [al] "+v"(al), [ah] "+v"(ah), [bl] "+v"(bl), [bh] "+v"(bh), [f0] "+v"(f0), [g0] "+v"(g0), [f1] "+v"(f1),
+        [g1] "+v"(g1), [om] "=&v"(om), [s] "=&v"(s), [sw] "=&v"(sw), [dl] "=&v"(dl), [dh] "=&v"(dh), [t] "=&v"(t)
+      :
+      : "vcc");
+}
+#else
+BLS_HD BLS_INLINE void divstep(uint32_t& al, uint32_t& ah, uint32_t& bl, uint32_t& bh, uint32_t& f0, uint32_t& g0,
+                               uint32_t& f1, uint32_t& g1) {
+  const uint64_t a = (uint64_t)ah << 32 | al, b = (uint64_t)bh << 32 | bl;
+  const uint32_t om = mask_bit0(al);
+  const int64_t d = (int64_t)(a - b);
+  const uint32_t s = (uint32_t)(d >> 63), sw = om & s;
+  const uint64_t ad = d < 0 ? (uint64_t)-d : (uint64_t)d;
+  const uint64_t nb = sw ? a : b, na = (om ? ad : a) >> 1;
+  const uint32_t tf = ((f0 - f1) ^ sw) - sw, tg = ((g0 - g1) ^ sw) - sw;
+  f1 = bfi(sw, f0, f1) << 1;
+  g1 = bfi(sw, g0, g1) << 1;
+  f0 = bfi(om, tf, f0);
+  g0 = bfi(om, tg, g0);
+  al = (uint32_t)na;
+  ah = (uint32_t)(na >> 32);
+  bl = (uint32_t)nb;
+  bh = (uint32_t)(nb >> 32);
+}
+#endif
+
+// limbs: 12 x 32 -> 13 x 30
+BLS_HD BLS_INLINE void to30(int32_t* o, const uint32_t* x) {
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    const int b = 30 * i, w = b >> 5, s = b & 31;
+    uint64_t v = x[w];
+    if (w + 1 < 12) v |= (uint64_t)x[w + 1] << 32;
+    o[i] = (int32_t)((uint32_t)(v >> s) & M30);
+  }
+}
+// 13 x 30 (non-negative, each < 2^30, value < 2^384) -> 12 x 32
+BLS_HD BLS_INLINE void from30(uint32_t* o, const int32_t* x) {
+#pragma unroll
+  for (int w = 0; w < 12; ++w) {
+    const int b = 32 * w, i = b / 30, s = b % 30;
+    uint64_t v = (uint64_t)(uint32_t)x[i] >> s;
+    v |= (uint64_t)(uint32_t)x[i + 1] << (30 - s);
+    if (i + 2 < 13 && 60 - s < 32) v |= (uint64_t)(uint32_t)x[i + 2] << (60 - s);
+    o[w] = (uint32_t)v;
+  }
+}
+// r = (x f + y g) / 2^30 for 30-bit limb vectors (top limb signed); the low 30 bits of x f + y g are zero.
+BLS_HD BLS_INLINE void lin_shift(int32_t* r, const int32_t* x, const int32_t* y, int32_t f, int32_t g) {
+  int64_t c = (int64_t)x[0] * f + (int64_t)y[0] * g;
+  c >>= 30;
+#pragma unroll
+  for (int i = 1; i < 13; ++i) {
+    c += (int64_t)x[i] * f + (int64_t)y[i] * g;
+    r[i - 1] = (int32_t)((uint32_t)c & M30);
+    c >>= 30;
+  }
+  r[12] = (int32_t)c;
+}
+// r = |r| (top limb signed), returns the mask -1 if r was negative
+BLS_HD BLS_INLINE int32_t cond_neg(int32_t* r) {
+  const int32_t s = r[12] >> 31;
+  int32_t c = s & 1;  // -r = (r ^ -1) + 1 limb-wise
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const int32_t t = (r[i] ^ (s & (int32_t)M30)) + c;
+    r[i] = t & (int32_t)M30;
+    c = t >> 30;
+  }
+  r[12] = (r[12] ^ s) + c;
+  return s;
+}
+// r = (u f + v g) / 2^30 mod p, for u, v in [0, p); result in [0, p)
+BLS_HD BLS_INLINE void lin_mod(int32_t* r, const int32_t* u, const int32_t* v, int32_t f, int32_t g) {
+  int64_t c = (int64_t)u[0] * f + (int64_t)v[0] * g;
+  const int32_t k = (int32_t)(((uint32_t)c * PINV30) & M30);
+  c += (int64_t)k * (int32_t)P30[0];
+  c >>= 30;
+#pragma unroll
+  for (int i = 1; i < 13; ++i) {
+    c += (int64_t)u[i] * f + (int64_t)v[i] * g + (int64_t)k * (int32_t)P30[i];
+    r[i - 1] = (int32_t)((uint32_t)c & M30);
+    c >>= 30;
+  }
+  r[12] = (int32_t)c;  // r in (-p, 2p)
+  // r < 0: r += p
+  int32_t s = r[12] >> 31;
+  int32_t cc = 0;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    const int32_t t = r[i] + ((int32_t)P30[i] & s) + cc;
+    r[i] = i < 12 ? (t & (int32_t)M30) : t;
+    cc = t >> 30;
+  }
+  // r >= p: r -= p
+  int32_t d[13];
+  cc = 0;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    const int32_t t = r[i] - (int32_t)P30[i] + cc;
+    d[i] = i < 12 ? (t & (int32_t)M30) : t;
+    cc = t >> 30;
+  }
+  s = d[12] >> 31;  // borrow: keep r
+#pragma unroll
+  for (int i = 0; i < 13; ++i) r[i] = (int32_t)bfi((uint32_t)s, (uint32_t)r[i], (uint32_t)d[i]);
+}
+}  // namespace gcd30
+
+BLS_HD BLS_CALL void fp_inv(fp& r, const fp& a_in) {
+  using namespace gcd30;
+  int32_t a[13], b[13], u[13], v[13];
+  to30(a, a_in.v);
+#pragma unroll
+  for (int i = 0; i < 13; ++i) {
+    b[i] = (int32_t)P30[i];
+    u[i] = i == 0;
+    v[i] = 0;
+  }
+  for (int it = 0; it < ITERS; ++it) {
+    // n = max(len(a), len(b), 62): bits [n-32, n) of a and b, and their low 30 bits
+    uint32_t top = 0;
+    int hi = 0;
+#pragma unroll
+    for (int i = 0; i < 13; ++i) {
+      const uint32_t t = (uint32_t)(a[i] | b[i]);
+      hi = t ? i : hi;
+      top = t ? t : top;
+    }
+    int n = 30 * hi + (32 - __builtin_clz(top | 1u));
+    n = n < 62 ? 62 : n;
+    const int pos = n - 32, L = (pos * 2185) >> 16, sh = pos - 30 * L;
+    uint32_t wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0;  // 64-bit windows of a and b starting at limb L
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {  // a, b <= p < 2^381: the window starts in limb 11 at most
+      const uint32_t m = mask_eq((uint32_t)i, (uint32_t)L);
+      uint64_t xa = (uint64_t)(uint32_t)a[i] | ((uint64_t)(uint32_t)a[i + 1] << 30);
+      uint64_t xb = (uint64_t)(uint32_t)b[i] | ((uint64_t)(uint32_t)b[i + 1] << 30);
+      if (i + 2 < 13) {
+        xa |= (uint64_t)(uint32_t)a[i + 2] << 60;
+        xb |= (uint64_t)(uint32_t)b[i + 2] << 60;
+      }
+      wa0 = bfi(m, (uint32_t)xa, wa0);
+      wa1 = bfi(m, (uint32_t)(xa >> 32), wa1);
+      wb0 = bfi(m, (uint32_t)xb, wb0);
+      wb1 = bfi(m, (uint32_t)(xb >> 32), wb1);
+    }
+    const uint64_t wa = (uint64_t)wa1 << 32 | wa0, wb = (uint64_t)wb1 << 32 | wb0;
+    const uint64_t ab = (uint64_t)(uint32_t)(wa >> sh) << 30 | (uint32_t)a[0];
+    const uint64_t bb = (uint64_t)(uint32_t)(wb >> sh) << 30 | (uint32_t)b[0];
+    uint32_t al = (uint32_t)ab, ah = (uint32_t)(ab >> 32), bl = (uint32_t)bb, bh = (uint32_t)(bb >> 32);
+    uint32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll 5
+    for (int j = 0; j < 30; ++j) divstep(al, ah, bl, bh, f0, g0, f1, g1);
+    int32_t na[13], nb[13];
+    lin_shift(na, a, b, f0, g0);
+    lin_shift(nb, a, b, f1, g1);
+    const int32_t sa = cond_neg(na), sb = cond_neg(nb);
+    f0 = (f0 ^ sa) - sa;
+    g0 = (g0 ^ sa) - sa;
+    f1 = (f1 ^ sb) - sb;
+    g1 = (g1 ^ sb) - sb;
+    int32_t nu[13], nv[13];
+    lin_mod(nu, u, v, f0, g0);
+    lin_mod(nv, u, v, f1, g1);
+#pragma unroll
+    for (int i = 0; i < 13; ++i) {
+      a[i] = na[i];
+      b[i] = nb[i];
+      u[i] = nu[i];
+      v[i] = nv[i];
+    }
+  }
+  fp y, r3;
+  from30(y.v, v);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r3.v[i] = R3_LIMBS[i];
+  fp_mul(r, y, r3);
+}
+
+// Fermat inverse (kept for the host tests that cross-check the binary GCD)
+BLS_HD BLS_INLINE void fp_inv_pow(fp& r, const fp& a) { fp_pow(r, a, EXP_P_MINUS_2, 380); }
 
 // Returns true and r = sqrt(a) when a is a square (p = 3 mod 4: r = a^((p+1)/4)).
 BLS_HD BLS_INLINE bool fp_sqrt(fp& r, const fp& a) {

@@ -353,6 +353,98 @@ def _gen_sop(w, X, Y, Z, Wd, M):
     w("v_mov_b32 %s, v50" % M(N32 - 1))
 
 
+def _gen_prod(w, X, Y, M, R=None):
+    """Appends r = X*Y/2^384 mod p, in [0, 2p), to the stream w (gen_mul's column schedule on named registers):
+    quotient digits in M(i), result limb j over M(j) or, with R = X, over X(j) (both are dead from column
+    j + 12 on)."""
+    R = R or M
+    first = [True]
+    src2 = ["v[48:49]"]
+
+    def mac(x, y):
+        w("v_mad_u64_u32 v[48:49], vcc, %s, %s, %s" % (x, y, src2[0]))
+        src2[0] = "v[48:49]"
+        if first[0]:
+            w("v_addc_co_u32_e64 v51, vcc, 0, 0, vcc")
+            first[0] = False
+        else:
+            w("v_addc_co_u32_e32 v51, vcc, 0, v51, vcc")
+
+    def shift():
+        w("v_mov_b32 v50, v49")
+        src2[0] = "v[50:51]"
+        first[0] = True
+
+    Sp = lambda j: "s%d" % (16 + j)
+    w("v_mad_u64_u32 v[48:49], vcc, %s, %s, 0" % (X(0), Y(0)))
+    w("v_mov_b32 v51, 0")
+    w("v_mul_lo_u32 %s, v48, s28" % M(0))
+    mac(M(0), "s16")
+    shift()
+    for i in range(1, N32):
+        for j in range(i):
+            mac(X(j), Y(i - j))
+            mac(M(j), Sp(i - j))
+        mac(X(i), Y(0))
+        w("v_mul_lo_u32 %s, v48, s28" % M(i))
+        mac(M(i), "s16")
+        shift()
+    for i in range(N32, 2 * N32 - 1):
+        for j in range(i - N32 + 1, N32):
+            mac(X(j), Y(i - j))
+            mac(M(j), Sp(i - j))
+        w("v_mov_b32 %s, v48" % R(i - N32))
+        shift()
+    w("v_mov_b32 %s, v50" % R(N32 - 1))
+
+
+# Fp2 squaring: c0 = (a0 + a1)(a0 + p - a1)/R, c1 = a0 (a1 + a1)/R.  The three operand sums stay unreduced
+# (< 2p each, products < 4p^2 < pR) and the doubling of c1 moves onto an operand, so the routine is two products,
+# three 12-word add/sub chains and two final subtractions.  a0 = v[0:11], a1 = v[12:23] (clobbered); c0 -> v[24:35],
+# c1 -> v[36:47]; v48-v63, s16-s28, vcc clobbered.
+FP2S_A0, FP2S_A1, FP2S_C0, FP2S_C1 = 0, 12, 24, 36
+
+
+def gen_fp2_sqr():
+    PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
+    PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    V = lambda base: (lambda j: "v%d" % (base + j))
+    A0, A1, C0, C1 = V(FP2S_A0), V(FP2S_A1), V(FP2S_C0), V(FP2S_C1)
+    out = []
+    w = out.append
+    for j in range(N32):
+        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
+    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    # d = (p - a1) + a0 into C1 (p staged in C0 first), s = a0 + a1 into C0, a1 <- 2 a1
+    for j in range(N32):
+        w("v_mov_b32 %s, s%d" % (C0(j), 16 + j))
+    w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (C1(0), C0(0), A1(0)))
+    for j in range(1, N32):
+        w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (C1(j), C0(j), A1(j)))
+    w("v_add_co_u32_e32 %s, vcc, %s, %s" % (C1(0), C1(0), A0(0)))
+    for j in range(1, N32):
+        w("v_addc_co_u32_e32 %s, vcc, %s, %s, vcc" % (C1(j), C1(j), A0(j)))
+    w("v_add_co_u32_e32 %s, vcc, %s, %s" % (C0(0), A0(0), A1(0)))
+    for j in range(1, N32):
+        w("v_addc_co_u32_e32 %s, vcc, %s, %s, vcc" % (C0(j), A0(j), A1(j)))
+    w("v_add_co_u32_e32 %s, vcc, %s, %s" % (A1(0), A1(0), A1(0)))
+    for j in range(1, N32):
+        w("v_addc_co_u32_e32 %s, vcc, %s, %s, vcc" % (A1(j), A1(j), A1(j)))
+    T = V(52)
+    _gen_prod(w, C0, C1, T, R=C0)                      # c0 = s d (raw) over s; digits in v52..v63
+    _gen_prod(w, A0, A1, C1)                           # c1 = a0 (2 a1) (raw); digits and result over d
+    for j in range(N32):
+        w("v_mov_b32 %s, s%d" % (A0(j), 16 + j))
+    for C in (C0, C1):                                 # canonical: keep c when c - p borrows
+        w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), A0(0)))
+        for j in range(1, N32):
+            w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (T(j), C(j), A0(j)))
+        w("v_subb_co_u32_e64 %s, vcc, 0, 0, vcc" % A1(0))
+        for j in range(N32):
+            w("v_bfi_b32 %s, %s, %s, %s" % (C(j), A1(0), C(j), T(j)))
+    return out
+
+
 def gen_fp2_mul():
     PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
     PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
@@ -543,6 +635,10 @@ def emulate(body, a, b, regs=None):
             r = rd(o[2]) + rd(o[3]) + rd(o[4])
             wr(o[0], r)
             s["vcc"] = r >> 32
+        elif op == "v_add_co_u32_e32":
+            r = rd(o[2]) + rd(o[3])
+            wr(o[0], r)
+            s["vcc"] = r >> 32
         elif op == "v_sub_co_u32_e32":
             r = rd(o[2]) - rd(o[3])
             wr(o[0], r)
@@ -631,6 +727,8 @@ def emit_header(path, bodies, extra=()):
     lines.append("#define BLS_FP_MUL_ASM_CLOBBERS %s" % clob)
     clob2 = ", ".join('"v%d"' % r for r in range(48, 52)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
     lines.append("#define BLS_FP2_MUL_ASM_CLOBBERS %s" % clob2)
+    clob3 = ", ".join('"v%d"' % r for r in range(48, 64)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
+    lines.append("#define BLS_FP2_SQR_ASM_CLOBBERS %s" % clob3)
     for name, body in extra:
         lines.append("")
         lines.append("// %s: %d instructions, positional operands (see tools/gen_fp_asm.py)" % (name, len(body)))
@@ -648,7 +746,8 @@ def main():
     check(mul, mont=1 << 384, canonical=True)
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "fp_asm_gfx950.h")
     fp2 = gen_fp2_mul()
-    emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul), ("BLS_FP2_MUL_ASM_BODY", fp2)],
+    fp2s = gen_fp2_sqr()
+    emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul), ("BLS_FP2_MUL_ASM_BODY", fp2), ("BLS_FP2_SQR_ASM_BODY", fp2s)],
                 extra=[("BLS_FP_ADD_ASM", gen_add()), ("BLS_FP_SUB_ASM", gen_sub()), ("BLS_FP_NEG_ASM", gen_sub(neg=True)),
                        ("BLS_FP_ADD_LAZY_ASM", gen_add_lazy()), ("BLS_FP_SUB_LAZY_ASM", gen_sub_lazy())])
     print("wrote %s: %d instructions" % (path, len(mul)))

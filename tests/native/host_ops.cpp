@@ -468,3 +468,14 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
   mark(5);
   return 0;
 }
+
+// ---- binary-GCD inversion (field.h fp_inv) against the Fermat power, on plain-limb inputs ------------------
+extern "C" void ht_fp_inv(const uint32_t* x12, int gcd, uint32_t* out12) {
+  fp x, r;
+  for (int i = 0; i < 12; ++i) x.v[i] = x12[i];
+  if (gcd)
+    fp_inv(r, x);
+  else
+    fp_inv_pow(r, x);
+  for (int i = 0; i < 12; ++i) out12[i] = r.v[i];
+}

@@ -134,3 +134,21 @@ def test_fp2_product_routine():
         c1 = _val([regs[g.FP2_C1 + j] for j in range(12)])
         assert c0 == (a0 * b0 - a1 * b1) * R_INV % g.P, (t, hex(a0), hex(a1), hex(b0), hex(b1))
         assert c1 == (a0 * b1 + a1 * b0) * R_INV % g.P, (t, hex(a0), hex(a1), hex(b0), hex(b1))
+
+
+def test_fp2_square_routine():
+    """The device fp2_sqr routine (BLS_FP2_SQR_ASM_BODY, gen_fp2_sqr): c0 = (a0^2 - a1^2)/R, c1 = 2 a0 a1/R mod p,
+    canonical, on canonical operands with edges."""
+    body = _macro_body("BLS_FP2_SQR_ASM_BODY")
+    assert body == g.gen_fp2_sqr(), "fp_asm_gfx950.h is stale: rerun charon_amd/tools/gen_fp_asm.py"
+    cases = _cases(60, 51)
+    rnd = random.Random(52)
+    for t in range(300):
+        a0, a1 = rnd.choice(cases), rnd.choice(cases)
+        regs = {g.FP2S_A0 + j: v for j, v in enumerate(_limbs(a0))}
+        regs.update({g.FP2S_A1 + j: v for j, v in enumerate(_limbs(a1))})
+        g.emulate(body, None, None, regs)
+        c0 = _val([regs[g.FP2S_C0 + j] for j in range(12)])
+        c1 = _val([regs[g.FP2S_C1 + j] for j in range(12)])
+        assert c0 == (a0 * a0 - a1 * a1) * R_INV % g.P, (t, hex(a0), hex(a1))
+        assert c1 == 2 * a0 * a1 * R_INV % g.P, (t, hex(a0), hex(a1))

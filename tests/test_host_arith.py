@@ -228,3 +228,31 @@ def test_fixtures_verify_host(L):
         msg = bytes.fromhex(c["msg"])
         st = L.ht_verify(bytes.fromhex(c["pk"]), msg, len(msg), bytes.fromhex(c["sig"]))
         assert st == c["status"], c["note"]
+
+
+def test_binary_gcd_inverse(L):
+    """field.h fp_inv (Pornin's binary GCD, 27 x 30 divsteps) equals the Fermat power x^(p-2) and the oracle's
+    inverse on Montgomery-form inputs: 0 (inverse 0), 1, p - 1, powers of two, near-p values, Fibonacci-like
+    inputs (the slowest-converging GCD inputs) and random values."""
+    import ctypes
+    import random as _r
+    P = bls.P
+    R = 1 << 384
+    rng = _r.Random(11)
+    fib = [1, 1]
+    while fib[-1] < P:
+        fib.append(fib[-1] + fib[-2])
+    xs = [0, 1, 2, P - 1, P - 2, (P - 1) // 2] + [(1 << k) % P for k in range(0, 381, 17)] + fib[-12:] + \
+        [f % P for f in fib[-12:]] + [rng.randrange(P) for _ in range(300)]
+    fn = L.ht_fp_inv
+    for x in xs:
+        x %= P
+        xm = x * R % P  # Montgomery form of x
+        inp = (ctypes.c_uint32 * 12)(*[(xm >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+        outs = []
+        for gcd in (1, 0):
+            o = (ctypes.c_uint32 * 12)()
+            fn(inp, gcd, o)
+            outs.append(sum(v << (32 * i) for i, v in enumerate(o)))
+        want = (pow(x, P - 2, P) * R) % P
+        assert outs[0] == outs[1] == want, hex(x)
