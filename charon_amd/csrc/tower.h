@@ -338,9 +338,19 @@ BLS_HD BLS_FP6_CALL void fp6_mul_1(fp6& r, const fp6& a_in, const fp2& b1_in) {
   r.c2 = c2;
 }
 
-BLS_HD BLS_CALL void fp12_mul(fp12& r, const fp12& a_in, const fp12& b_in) {
+// Operands read where they are needed rather than copied in at entry: the 288-dword copy made the allocator spill
+// (op_probe: fp12_mul 242k -> 218k cycles, final_exponentiation -3.5 %).
+#ifndef BLS_FP12_MUL_COPYIN
+#define BLS_FP12_MUL_COPYIN 0
+#endif
+BLS_HD BLS_INLINE void fp12_mul_inl(fp12& r, const fp12& a_in, const fp12& b_in) {
+#if BLS_FP12_MUL_COPYIN
   const fp12 a = a_in;
   const fp12 b = b_in;
+#else
+  const fp12& a = a_in;
+  const fp12& b = b_in;
+#endif
   fp6 t0, t1, s0, s1;
   fp6_mul(t0, a.c0, b.c0);
   fp6_mul(t1, a.c1, b.c1);
@@ -354,6 +364,7 @@ BLS_HD BLS_CALL void fp12_mul(fp12& r, const fp12& a_in, const fp12& b_in) {
   fp6_add(r.c0, t0, t1);
   r.c1 = c1;
 }
+BLS_HD BLS_CALL void fp12_mul(fp12& r, const fp12& a_in, const fp12& b_in) { fp12_mul_inl(r, a_in, b_in); }
 BLS_HD BLS_INLINE void fp12_sqr_inl(fp12& r, const fp12& a_in) {
   // complex squaring: c0 = (a0+a1)(a0+v a1) - t - v t, c1 = 2t, t = a0 a1
   const fp12 a = a_in;

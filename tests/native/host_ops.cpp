@@ -180,6 +180,8 @@ void ht_fp12_op(int op, const uint8_t* a576, const uint8_t* b576, uint8_t* out57
     case 5: fp12_frobenius(r, a, 3); break;
     case 6: fp12_cyclotomic_sqr(r, a); break;
     case 7: fp12_mul_line(a, b.c0.c0, b.c0.c1, b.c1.c1); r = a; break;
+    case 8: fp12_cyc_exp_xabs_karabina(r, a); break;
+    case 9: fp12_cyc_exp_xabs_gs(r, a); break;
     default: r = a;
   }
   const fp* d = &r.c0.c0.c0;

@@ -256,3 +256,28 @@ def test_binary_gcd_inverse(L):
             outs.append(sum(v << (32 * i) for i, v in enumerate(o)))
         want = (pow(x, P - 2, P) * R) % P
         assert outs[0] == outs[1] == want, hex(x)
+
+
+def test_compressed_cyclotomic_exponentiation(L):
+    """a^|x| by Karabina's compressed squarings + batch decompression (pairing.h) == Granger-Scott == the oracle's
+    power, on cyclotomic elements; the degenerate inputs (the identity, an Fp2 element's easy-part image) take the
+    Granger-Scott fallback and still give the exact power; and final_exponentiation of 1 and of Fp2 elements is 1."""
+    rng = random.Random(17)
+    out = buf(576)
+    X_ABS = 0xD201000000010000
+    one = bls.F12_ONE
+    cases = []
+    for _ in range(3):
+        a = rand_f12(rng)
+        c = bls.f12_mul(bls.f12_conj(a), bls.f12_inv(a))
+        cases.append(bls.f12_mul(bls.f12_pow(c, P * P), c))
+    cases.append(one)
+    for c in cases:
+        want = bls.f12_pow(c, X_ABS)
+        for op in (8, 9):
+            L.ht_fp12_op(op, f12_bytes(c), f12_bytes(c), out)
+            assert f12_from(out.raw) == want, op
+    z = (0, 0)
+    for f in (one, (((rng.randrange(P), rng.randrange(P)), z, z), (z, z, z))):
+        L.ht_final_exp(f12_bytes(f), out)
+        assert f12_from(out.raw) == one
