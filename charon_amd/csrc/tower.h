@@ -144,8 +144,10 @@ BLS_HD BLS_INLINE void fp12_conj(fp12& r, const fp12& a) {
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // Device: one asm routine (tools/gen_fp_asm.py gen_fp2_mul): each coefficient is a single Montgomery reduction of
-// a sum of two products, c1 = (a0 b1 + a1 b0)/R and c0 = (a0 b0 + a1 (p - b1))/R -- no Fp additions and two final
-// subtractions instead of Karatsuba's three reduced products, three subtractions and two sums.
+// a sum of two products, c1 = (a0 b1 + a1 b0)/R and c0 = (a0 b0 + a1 (2p - b1))/R -- no Fp additions and two final
+// subtractions instead of Karatsuba's three reduced products, three subtractions and two sums.  Operands may be
+// unreduced sums in [0, 2p) (fp2_add_lazy); the result is canonical.  (The routine leaves a0, a1, b0 intact, but
+// declaring them input-only crashes this compiler's register allocator, so they are in/out operands here.)
 BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
   u32x12 a0 = fp_to_vec(a.c0), a1 = fp_to_vec(a.c1), b0 = fp_to_vec(b.c0), b1 = fp_to_vec(b.c1), c0, c1;
   asm volatile(BLS_ASM_CALL("bls_fp2_mul_rt")
@@ -211,25 +213,32 @@ BLS_HD BLS_CALL void fp2_inv(fp2& r, const fp2& a_in) {
   fp_neg(r.c1, t0);
 }
 
+// a + b left unreduced in [0, 2p) for canonical a, b: only ever an operand of fp2_mul (device), which reduces it.
+BLS_HD BLS_INLINE void fp2_add_lazy(fp2& r, const fp2& a, const fp2& b) {
+  fp_add_lazy(r.c0, a.c0, b.c0);
+  fp_add_lazy(r.c1, a.c1, b.c1);
+}
+
 BLS_HD BLS_FP6_CALL void fp6_mul(fp6& r, const fp6& a_in, const fp6& b_in) {
-  // Karatsuba over Fp2 (6 Fp2 products).  Operands are copied in once: referenced operands live in the
-  // caller's frame, and re-reading them around every product exposes a flat-load round trip each time.
+  // Karatsuba over Fp2 (6 Fp2 products); a, b canonical.  Operands are copied in once: referenced operands live in
+  // the caller's frame, and re-reading them around every product exposes a flat-load round trip each time.  The
+  // Karatsuba sums only feed products, so they stay unreduced.
   const fp6 a = a_in, b = b_in;
   fp2 t0, t1, t2, s0, s1, u0, u1, u2;
   fp2_mul(t0, a.c0, b.c0);
   fp2_mul(t1, a.c1, b.c1);
   fp2_mul(t2, a.c2, b.c2);
   // c0 = t0 + xi((a1+a2)(b1+b2) - t1 - t2)
-  fp2_add(s0, a.c1, a.c2);
-  fp2_add(s1, b.c1, b.c2);
+  fp2_add_lazy(s0, a.c1, a.c2);
+  fp2_add_lazy(s1, b.c1, b.c2);
   fp2_mul(u0, s0, s1);
   fp2_sub(u0, u0, t1);
   fp2_sub(u0, u0, t2);
   fp2_mul_xi(u0, u0);
   fp2_add(u0, u0, t0);
   // c1 = (a0+a1)(b0+b1) - t0 - t1 + xi t2
-  fp2_add(s0, a.c0, a.c1);
-  fp2_add(s1, b.c0, b.c1);
+  fp2_add_lazy(s0, a.c0, a.c1);
+  fp2_add_lazy(s1, b.c0, b.c1);
   fp2_mul(u1, s0, s1);
   fp2_sub(u1, u1, t0);
   fp2_sub(u1, u1, t1);
@@ -237,8 +246,8 @@ BLS_HD BLS_FP6_CALL void fp6_mul(fp6& r, const fp6& a_in, const fp6& b_in) {
   fp2_mul_xi(x2, t2);
   fp2_add(u1, u1, x2);
   // c2 = (a0+a2)(b0+b2) - t0 - t2 + t1
-  fp2_add(s0, a.c0, a.c2);
-  fp2_add(s1, b.c0, b.c2);
+  fp2_add_lazy(s0, a.c0, a.c2);
+  fp2_add_lazy(s1, b.c0, b.c2);
   fp2_mul(u2, s0, s1);
   fp2_sub(u2, u2, t0);
   fp2_sub(u2, u2, t2);
@@ -312,8 +321,8 @@ BLS_HD BLS_FP6_CALL void fp6_mul_01(fp6& r, const fp6& a_in, const fp2& b0_in, c
   fp2_mul_xi(u, u);
   fp2_add(c0, u, t0);
   // c1 = (a0+a1)(b0+b1) - t0 - t1
-  fp2_add(s0, a.c0, a.c1);
-  fp2_add(s1, b0, b1);
+  fp2_add_lazy(s0, a.c0, a.c1);
+  fp2_add(s1, b0, b1);  // full: b1 may itself be a sum (fp12_mul_line's g1 + h1)
   fp2_mul(c1, s0, s1);
   fp2_sub(c1, c1, t0);
   fp2_sub(c1, c1, t1);
@@ -430,21 +439,21 @@ BLS_HD BLS_INLINE void fp12_mul_line2_inl(fp12& f_in, const fp2& ga0_in, const f
   fp2_mul(p00, ga0, gb0);
   fp2_mul(p11, ga1, gb1);
   fp2_mul(phh, ha1, hb1);
-  fp2_add(sa, ga0, ga1);
-  fp2_add(sb, gb0, gb1);
+  fp2_add_lazy(sa, ga0, ga1);
+  fp2_add_lazy(sb, gb0, gb1);
   fp2_mul(t, sa, sb);
   fp2_sub(t, t, p00);
   fp2_sub(L0.c1, t, p11);   // ga0 gb1 + ga1 gb0
   fp2_mul_xi(t, phh);
   fp2_add(L0.c0, p00, t);   // ga0 gb0 + xi ha1 hb1
   L0.c2 = p11;              // ga1 gb1
-  fp2_add(sa, ga0, ha1);
-  fp2_add(sb, gb0, hb1);
+  fp2_add_lazy(sa, ga0, ha1);
+  fp2_add_lazy(sb, gb0, hb1);
   fp2_mul(x, sa, sb);
   fp2_sub(x, x, p00);
   fp2_sub(x, x, phh);       // ga0 hb1 + ha1 gb0
-  fp2_add(sa, ga1, ha1);
-  fp2_add(sb, gb1, hb1);
+  fp2_add_lazy(sa, ga1, ha1);
+  fp2_add_lazy(sb, gb1, hb1);
   fp2_mul(y, sa, sb);
   fp2_sub(y, y, p11);
   fp2_sub(y, y, phh);       // ga1 hb1 + ha1 gb1
@@ -457,8 +466,8 @@ BLS_HD BLS_INLINE void fp12_mul_line2_inl(fp12& f_in, const fp2& ga0_in, const f
     fp2_mul(m1, a.c1, x);
     fp2_mul(m2, a.c2, y);
     fp2_mul(m0, a.c0, x);
-    fp2_add(u, a.c1, a.c2);
-    fp2_add(w2, x, y);
+    fp2_add_lazy(u, a.c1, a.c2);
+    fp2_add_lazy(w2, x, y);
     fp2_mul(u, u, w2);
     fp2_sub(u, u, m1);
     fp2_sub(u, u, m2);
@@ -486,8 +495,8 @@ BLS_HD BLS_INLINE void fp12_line_pair(fp12& f, const fp2& ga0, const fp2& ga1, c
   fp2_mul(p00, ga0, gb0);
   fp2_mul(p11, ga1, gb1);
   fp2_mul(phh, ha1, hb1);
-  fp2_add(sa, ga0, ga1);
-  fp2_add(sb, gb0, gb1);
+  fp2_add_lazy(sa, ga0, ga1);
+  fp2_add_lazy(sb, gb0, gb1);
   fp2_mul(t, sa, sb);
   fp2_sub(t, t, p00);
   fp2_sub(f.c0.c1, t, p11);
@@ -495,13 +504,13 @@ BLS_HD BLS_INLINE void fp12_line_pair(fp12& f, const fp2& ga0, const fp2& ga1, c
   fp2_add(f.c0.c0, p00, t);
   f.c0.c2 = p11;
   fp2_set_zero(f.c1.c0);
-  fp2_add(sa, ga0, ha1);
-  fp2_add(sb, gb0, hb1);
+  fp2_add_lazy(sa, ga0, ha1);
+  fp2_add_lazy(sb, gb0, hb1);
   fp2_mul(t, sa, sb);
   fp2_sub(t, t, p00);
   fp2_sub(f.c1.c1, t, phh);
-  fp2_add(sa, ga1, ha1);
-  fp2_add(sb, gb1, hb1);
+  fp2_add_lazy(sa, ga1, ha1);
+  fp2_add_lazy(sb, gb1, hb1);
   fp2_mul(t, sa, sb);
   fp2_sub(t, t, p11);
   fp2_sub(f.c1.c2, t, phh);

@@ -296,13 +296,14 @@ gen_mul32 = gen_mul  # name used by tools/gen_probe_bodies.py
 # ---------------------------------------------------------------- Fp2 product as two sums of products
 # (a0 + a1 u)(b0 + b1 u) = (a0 b0 - a1 b1) + (a0 b1 + a1 b0) u.  Each coefficient is ONE Montgomery reduction
 # of a sum of two 768-bit products (product scanning, reduction interleaved per column, as gen_mul):
-#   c1 = (a0 b1 + a1 b0) / R,   c0 = (a0 b0 + a1 (p - b1)) / R   (mod p)
+#   c1 = (a0 b1 + a1 b0) / R,   c0 = (a0 b0 + a1 (2p - b1)) / R   (mod p)
 # 2 x 432 mads instead of the 3 x 288 of Karatsuba with three reduced products, and no Fp additions: the
-# Karatsuba sums, the three subtractions and one of the three final subtractions disappear.  For canonical
-# inputs each sum is < 2p^2 < pR, so one conditional subtraction makes each output canonical.
-# Registers: a0 = v[0:11], a1 = v[12:23], b0 = v[24:35], b1 = v[36:47] (all clobbered); c1 -> v[52:63],
-# c0 -> v[64:75]; v48-v51, s16-s28 and vcc clobbered.
-FP2_A0, FP2_A1, FP2_B0, FP2_B1, FP2_C1, FP2_C0 = 0, 12, 24, 36, 52, 64
+# Karatsuba sums, the three subtractions and one of the three final subtractions disappear.  Operands may be
+# unreduced sums in [0, 2p): each sum of products is then < 8p^2 and (T + mp)/R < 8p^2/R + p < 1.82p, so one
+# conditional subtraction still makes each output canonical.
+# Registers: a0 = v[0:11], a1 = v[12:23], b0 = v[24:35] (preserved), b1 = v[36:47] (clobbered); c1 -> v[52:63],
+# c0 -> v[64:75]; v48-v51, v76-v87, s16-s28 and vcc clobbered.
+FP2_A0, FP2_A1, FP2_B0, FP2_B1, FP2_C1, FP2_C0, FP2_T = 0, 12, 24, 36, 52, 64, 76
 
 
 def _gen_sop(w, X, Y, Z, Wd, M):
@@ -455,22 +456,24 @@ def gen_fp2_mul():
     for j in range(N32):
         w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
     w("s_mov_b32 s28, 0x%08x" % PINV32)
+    P2L = [((2 * P) >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    T = V(FP2_T)
     _gen_sop(w, A0, B1, A1, B0, C1)                    # c1 (raw, < 2p) in v[52:63]
-    for j in range(N32):                               # p into VGPRs (the carry chain reads vcc: one
-        w("v_mov_b32 %s, s%d" % (C0(j), 16 + j))       # constant-bus operand only)
+    for j in range(N32):                               # 2p into VGPRs (the carry chain reads vcc: one
+        w("v_mov_b32 %s, 0x%08x" % (C0(j), P2L[j]))    # constant-bus operand only)
     w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (B1(0), C0(0), B1(0)))
-    for j in range(1, N32):                            # b1 <- p - b1 in (0, p]
+    for j in range(1, N32):                            # b1 <- 2p - b1 in (0, 2p]
         w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (B1(j), C0(j), B1(j)))
     _gen_sop(w, A0, B0, A1, B1, C0)                    # c0 (raw) in v[64:75]
-    for j in range(N32):
-        w("v_mov_b32 %s, s%d" % (A0(j), 16 + j))
+    for j in range(N32):                               # p over the dead 2p - b1; a0, a1, b0 stay intact
+        w("v_mov_b32 %s, s%d" % (B1(j), 16 + j))
     for C in (C1, C0):                                 # canonical: keep c when c - p borrows
-        w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (A1(0), C(0), A0(0)))
+        w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), B1(0)))
         for j in range(1, N32):
-            w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (A1(j), C(j), A0(j)))
-        w("v_subb_co_u32_e64 %s, vcc, 0, 0, vcc" % B0(0))
+            w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (T(j), C(j), B1(j)))
+        w("v_subb_co_u32_e64 v48, vcc, 0, 0, vcc")
         for j in range(N32):
-            w("v_bfi_b32 %s, %s, %s, %s" % (C(j), B0(0), C(j), A1(j)))
+            w("v_bfi_b32 %s, v48, %s, %s" % (C(j), C(j), T(j)))
     return out
 
 
@@ -725,7 +728,8 @@ def emit_header(path, bodies, extra=()):
         lines.append("")
     clob = ", ".join('"v%d"' % r for r in range(24, 40)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
     lines.append("#define BLS_FP_MUL_ASM_CLOBBERS %s" % clob)
-    clob2 = ", ".join('"v%d"' % r for r in range(48, 52)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
+    clob2 = ", ".join('"v%d"' % r for r in list(range(48, 52)) + list(range(76, 88))) + ', "vcc", ' + \
+        ", ".join('"s%d"' % r for r in range(16, 29))
     lines.append("#define BLS_FP2_MUL_ASM_CLOBBERS %s" % clob2)
     clob3 = ", ".join('"v%d"' % r for r in range(48, 64)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
     lines.append("#define BLS_FP2_SQR_ASM_CLOBBERS %s" % clob3)

@@ -119,12 +119,13 @@ def test_lazy_add_sub_blocks(kind):
 def test_fp2_product_routine():
     """The device fp2_mul routine (BLS_FP2_MUL_ASM_BODY, gen_fp2_mul): emitted text == generator, and the interpreted
     stream gives c0 = (a0 b0 - a1 b1)/R, c1 = (a0 b1 + a1 b0)/R mod p, canonical, on canonical operands with edges
-    (0, 1, p - 1: the p - b1 = p operand and the final-subtraction boundaries)."""
+    (0, 1, p - 1: the final-subtraction boundaries), and on unreduced operands in [0, 2p) (lazy sums: p, 2p - 1);
+    a0, a1, b0 come back unchanged (the C++ declares them input-only)."""
     body = _macro_body("BLS_FP2_MUL_ASM_BODY")
     assert body == g.gen_fp2_mul(), "fp_asm_gfx950.h is stale: rerun charon_amd/tools/gen_fp_asm.py"
-    cases = _cases(60, 41)
+    cases = _cases(60, 41) + [g.P, g.P + 1, 2 * g.P - 1, 2 * g.P - 2, g.P + (1 << 300)]
     rnd = random.Random(42)
-    for t in range(250):
+    for t in range(300):
         a0, a1, b0, b1 = (rnd.choice(cases) for _ in range(4))
         regs = {}
         for base, x in ((g.FP2_A0, a0), (g.FP2_A1, a1), (g.FP2_B0, b0), (g.FP2_B1, b1)):
@@ -134,6 +135,8 @@ def test_fp2_product_routine():
         c1 = _val([regs[g.FP2_C1 + j] for j in range(12)])
         assert c0 == (a0 * b0 - a1 * b1) * R_INV % g.P, (t, hex(a0), hex(a1), hex(b0), hex(b1))
         assert c1 == (a0 * b1 + a1 * b0) * R_INV % g.P, (t, hex(a0), hex(a1), hex(b0), hex(b1))
+        for base, x in ((g.FP2_A0, a0), (g.FP2_A1, a1), (g.FP2_B0, b0)):
+            assert _val([regs[base + j] for j in range(12)]) == x
 
 
 def test_fp2_square_routine():
