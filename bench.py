@@ -32,7 +32,7 @@ METRIC = "verified BLS partial sigs/sec (node) + threshold aggregates/sec, 1/2/4
 # Counted by the instrumented host build of the same kernels (tests/test_work_counts.py keeps
 # this in sync).  Inversions are binary-GCD divsteps (field.h fp_inv), which are not products and are not
 # counted: ~33k VALU each, about 49 products' worth of issue time.  See DESIGN.md "Roofline".
-FPMUL_PER_VERIFY = 25486
+FPMUL_PER_VERIFY = 24247
 MADS_PER_FPMUL = 300
 # RLC BatchVerify stages (charon_amd/csrc/rlc.h), same unit and source (tests/test_work_counts.py):
 # stage 1 per item, stage 2 per distinct message, stage 3 per window of 8 with 2 messages (one per

@@ -29,6 +29,34 @@ BLS_HD BLS_CALL bool pairing_check_verify(const g1a& pk, const g2a& hm, const g2
   return fp12_is_one(e);
 }
 
+// The same check with the signature's G2 membership taken from the Miller loop's [|x|] sig (pairing.h
+// g2_subgroup_from_miller) instead of a separate 63-doubling scalar multiplication.  sig is on the curve and not
+// infinity.  Returns HIPBLS_OK, HIPBLS_ERR_SIGNATURE (sig not in G2: herumi's deserialization error, which wins over
+// the pairing's verdict) or HIPBLS_ERR_VERIFY.
+BLS_HD BLS_CALL int pairing_check_verify_sig(const g1a& pk, const g2a& hm, const g2a& sig) {
+  g1a P1;
+  P1.x = G1_GEN_X;
+  P1.y = G1_NEG_GEN_Y;
+  fp12 f, e;
+  g2j T1;
+  miller_loop_2(f, pk, hm, P1, sig, &T1);
+  const bool in_g2 = g2_subgroup_from_miller(T1, sig);
+  final_exponentiation(e, f);
+  if (!in_g2) return HIPBLS_ERR_SIGNATURE;
+  return fp12_is_one(e) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+}
+
+// Statuses for the infinity cases (herumi: a valid infinity key or signature fails KeyValidate / the check), once the
+// signature decoded with its membership still pending: a non-G2 signature is still a deserialization error.
+BLS_HD BLS_INLINE int verify_inf_status(int ds, const g2a& sig) {
+  if (ds == DEC_OK) {
+    g2j sj;
+    jac_from_aff(sj, sig);
+    if (!g2_in_subgroup(sj)) return HIPBLS_ERR_SIGNATURE;
+  }
+  return HIPBLS_ERR_VERIFY;
+}
+
 // Full tbls.Verify for one item (used by the fused kernel and host-side instrumentation).
 
 // sigma = sk * H(msg); returns HIPBLS_OK or HIPBLS_ERR_SECRET
@@ -60,14 +88,14 @@ BLS_HD BLS_CALL int op_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t 
   const int dp = g1_decompress(pk, pk48, true);
   if (dp == DEC_BAD) return HIPBLS_ERR_PUBKEY;
   g2a sig;
-  const int ds = g2_decompress(sig, sig96, true);
+  const int ds = g2_decompress(sig, sig96, false);  // G2 membership: from the Miller loop below
   if (ds == DEC_BAD) return HIPBLS_ERR_SIGNATURE;
-  if (dp == DEC_INF || ds == DEC_INF) return HIPBLS_ERR_VERIFY;  // KeyValidate / e(pk,H) != 1
+  if (dp == DEC_INF || ds == DEC_INF) return verify_inf_status(ds, sig);  // KeyValidate / e(pk,H) != 1
   g2j hj;
   hash_to_g2(hj, msg, msg_len, DST_POP, 43);
   g2a hm;
   jac_to_aff(hm, hj);
-  return pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+  return pairing_check_verify_sig(pk, hm, sig);
 }
 
 BLS_HD BLS_CALL int op_sign(uint8_t* out96, const uint8_t* sk32, const uint8_t* msg, uint32_t msg_len) {

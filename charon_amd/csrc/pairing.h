@@ -138,7 +138,10 @@ BLS_HD BLS_CALL void miller_dbl2_line2(fp12& f_io, g2j& T0_io, g2j& T1_io, const
 
 // The 2-pair loop of Verify (both pairs live) on its own: one code path for the register allocator, T0/T1/f/P in the
 // loop's registers, and the first step's f = 1 * la * lb formed from the line product alone (6 Fp2 products, not 23).
-BLS_HD BLS_CALL void miller_loop_2(fp12& f_out, const g1a& P0_in, const g2a& Q0, const g1a& P1_in, const g2a& Q1) {
+// T1_out (when given) receives the second pair's final T = [|x|] Q1 in homogeneous coordinates, with Z = 0 if any
+// step was exceptional (see g2_subgroup_from_miller).
+BLS_HD BLS_CALL void miller_loop_2(fp12& f_out, const g1a& P0_in, const g2a& Q0, const g1a& P1_in, const g2a& Q1,
+                                   g2j* T1_out = nullptr) {
   const g1a P0 = P0_in, P1 = P1_in;
   g2j T0, T1;
   T0.x = Q0.x;
@@ -170,6 +173,26 @@ BLS_HD BLS_CALL void miller_loop_2(fp12& f_out, const g1a& P0_in, const g2a& Q0,
     }
   }
   fp12_conj(f_out, f);
+  if (T1_out) *T1_out = T1;
+}
+
+// The signature's G2 membership from the Miller loop's by-product (Scott 2021: Q in G2 iff psi(Q) = [x] Q).  The loop
+// runs T over |x|'s bits from T = Q, so without an exceptional step T ends as [|x|] Q = -[x] Q.  The homogeneous
+// steps are exceptional exactly when their Z comes out 0 (doubling: Y = 0 or Z = 0; addition: T = +-Q, lambda = 0),
+// and Z stays 0 afterwards; an exceptional step means [k]Q in {O, +-Q} for some k < 2^64, i.e. Q of small order, not in
+// G2.  So Q (affine, not infinity) is in G2 iff Z != 0 and T = -psi(Q): X = psi_x Z, Y = -psi_y Z.  This replaces the
+// 63-doubling scalar multiplication of g2_in_subgroup for Verify's signature.
+BLS_HD BLS_INLINE bool g2_subgroup_from_miller(const g2j& T, const g2a& Q) {
+  g2j q, ps;
+  jac_from_aff(q, Q);
+  g2_psi(ps, q);  // affine in, z = 1 out
+  fp2 t;
+  bool ok = !fp2_is_zero(T.z);
+  fp2_mul(t, ps.x, T.z);
+  ok = ok && fp2_eq(t, T.x);
+  fp2_mul(t, ps.y, T.z);
+  fp2_add(t, t, T.y);
+  return ok && fp2_is_zero(t);
 }
 
 BLS_HD BLS_CALL void miller_loop_n(fp12& f, const g1a* P, const g2a* Q, const bool* skip, int n) {

@@ -173,14 +173,14 @@ BLS_HD BLS_CALL int op_verify_decoded_pk(int dp, const g1a& pk, const uint8_t* m
                                          const uint8_t* sig96) {
   if (dp == DEC_BAD) return HIPBLS_ERR_PUBKEY;
   g2a sig;
-  const int ds = g2_decompress(sig, sig96, true);
+  const int ds = g2_decompress(sig, sig96, false);  // G2 membership from the Miller loop (ops.h)
   if (ds == DEC_BAD) return HIPBLS_ERR_SIGNATURE;
-  if (dp == DEC_INF || ds == DEC_INF) return HIPBLS_ERR_VERIFY;
+  if (dp == DEC_INF || ds == DEC_INF) return verify_inf_status(ds, sig);
   g2j hj;
   hash_to_g2(hj, msg, msg_len, DST_POP, 43);
   g2a hm;
   jac_to_aff(hm, hj);
-  return pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+  return pairing_check_verify_sig(pk, hm, sig);
 }
 
 // Multi-Miller loop over up to MAXN pairs with one shared Fp12 squaring chain (pairing.h steps).
