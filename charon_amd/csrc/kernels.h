@@ -44,11 +44,11 @@ __global__ void __launch_bounds__(kBlock) k_verify_prep(const uint8_t* __restric
   if (dp == DEC_BAD) {
     st = HIPBLS_ERR_PUBKEY;
   } else {
-    const int ds = g2_decompress(sig, sigs + 96 * i, true);
+    const int ds = g2_decompress(sig, sigs + 96 * i, false);  // G2 membership: from the pair's Miller loop
     if (ds == DEC_BAD)
       st = HIPBLS_ERR_SIGNATURE;
     else if (dp == DEC_INF || ds == DEC_INF)
-      st = HIPBLS_ERR_VERIFY;  // KeyValidate / e(pk,H) != 1
+      st = verify_inf_status(ds, sig);  // KeyValidate / e(pk,H) != 1
   }
   if (st == RLC_PENDING) {
     const uint64_t o0 = offs[i], o1 = offs[i + 1];
@@ -64,24 +64,33 @@ __global__ void __launch_bounds__(kBlock) k_verify_prep(const uint8_t* __restric
 }
 
 // Stage 2, lanes 2i and 2i+1 per item: e(pk, H(m)) * e(-g1, sig) == 1 with the two Miller loops side by side
-// and the final exponentiation split across the pair.
+// and the final exponentiation split across the pair.  The odd lane's loop runs over the signature, so its final T
+// = [|x|] sig also decides the signature's G2 membership (pairing.h g2_subgroup_from_miller; the prep stage skipped
+// the separate check): a signature outside G2 is herumi's deserialization error, whatever the pairing says.
 __global__ void __launch_bounds__(kBlock) k_verify_pair_lg2(const uint32_t* __restrict__ ws, uint64_t n,
                                                             int32_t* __restrict__ status) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t i = t >> 1;
   const uint32_t m = (t & 1) ? ~0u : 0u;
   if (i >= n || status[i] != RLC_PENDING) return;  // same decision on both lanes of the pair
-  const bool ok = pairing_check_lg2<1>(2, m, [&](int k, g1a& P, g2a& Q) {
-    if (k == 0) {
-      soa_load<24>(&P.x.v[0], ws, n, i);
-      soa_load<48>(&Q.x.c0.v[0], ws + 24 * n, n, i);
-    } else {
-      P.x = G1_GEN_X;
-      P.y = G1_NEG_GEN_Y;
-      soa_load<48>(&Q.x.c0.v[0], ws + 72 * n, n, i);
-    }
-  });
-  if (!m) status[i] = ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+  g1a P[1];
+  g2a Q[1];
+  if (!m) {
+    soa_load<24>(&P[0].x.v[0], ws, n, i);
+    soa_load<48>(&Q[0].x.c0.v[0], ws + 24 * n, n, i);
+  } else {
+    P[0].x = G1_GEN_X;
+    P[0].y = G1_NEG_GEN_Y;
+    soa_load<48>(&Q[0].x.c0.v[0], ws + 72 * n, n, i);
+  }
+  fp12 f;
+  g2j T;
+  miller_loop_multi<1>(f, P, Q, 1, &T);
+  const uint32_t in_g2 = g2_subgroup_from_miller(T, Q[0]) ? 1u : 0u;  // meaningful on the odd lane
+  const uint32_t other = pair_swap(in_g2);  // both lanes of the pair take part in the exchange
+  const uint32_t sig_in_g2 = m ? in_g2 : other;
+  const bool ok = lg2_finish(f, m);
+  if (!m) status[i] = !sig_in_g2 ? HIPBLS_ERR_SIGNATURE : (ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY);
 }
 
 __global__ void __launch_bounds__(kBlock) k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restrict__ msgs,

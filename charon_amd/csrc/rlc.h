@@ -185,7 +185,8 @@ BLS_HD BLS_CALL int op_verify_decoded_pk(int dp, const g1a& pk, const uint8_t* m
 
 // Multi-Miller loop over up to MAXN pairs with one shared Fp12 squaring chain (pairing.h steps).
 template <int MAXN>
-BLS_HD BLS_CALL void miller_loop_multi(fp12& f, const g1a* P, const g2a* Q, int n) {
+// T0_out (when given) receives the first pair's final T = [|x|] Q[0] (pairing.h g2_subgroup_from_miller).
+BLS_HD BLS_CALL void miller_loop_multi(fp12& f, const g1a* P, const g2a* Q, int n, g2j* T0_out = nullptr) {
   g2j T[MAXN];
   for (int k = 0; k < n; ++k) {
     T[k].x = Q[k].x;
@@ -223,6 +224,7 @@ BLS_HD BLS_CALL void miller_loop_multi(fp12& f, const g1a* P, const g2a* Q, int 
     }
   }
   fp12_conj(f, f);
+  if (T0_out) *T0_out = T[0];
 }
 
 // Stage 3, one lane per window [i0, i1): sum the scaled keys per run of equal message index and
