@@ -343,8 +343,11 @@ BLS_HD BLS_INLINE void fp_sqr(fp& r, const fp& a) { r = fp_sqr_v(a); }
 // exponents used here (p-2, (p+1)/4, (p-3)/4, Hamming weight ~229) that is ~380 squarings + ~80
 // products instead of ~380 + 229.  The exponent is the same for every lane, so every branch and
 // table index is wave-uniform.
+#ifndef BLS_POW_W
+#define BLS_POW_W 5
+#endif
 BLS_HD BLS_CALL void fp_pow(fp& r, const fp& a, const uint32_t* e, int top_bit) {
-  constexpr int W = 5;
+  constexpr int W = BLS_POW_W;
   fp tbl[1 << (W - 1)];
   fp a2;
   tbl[0] = a;
@@ -376,11 +379,14 @@ BLS_HD BLS_CALL void fp_pow(fp& r, const fp& a, const uint32_t* e, int top_bit) 
     w = tbl[k];         \
     break;
       BLS_POW_CASE(0) BLS_POW_CASE(1) BLS_POW_CASE(2) BLS_POW_CASE(3) BLS_POW_CASE(4) BLS_POW_CASE(5)
-      BLS_POW_CASE(6) BLS_POW_CASE(7) BLS_POW_CASE(8) BLS_POW_CASE(9) BLS_POW_CASE(10) BLS_POW_CASE(11)
+      BLS_POW_CASE(6)
+#if BLS_POW_W == 5
+      BLS_POW_CASE(7) BLS_POW_CASE(8) BLS_POW_CASE(9) BLS_POW_CASE(10) BLS_POW_CASE(11)
       BLS_POW_CASE(12) BLS_POW_CASE(13) BLS_POW_CASE(14)
+#endif
 #undef BLS_POW_CASE
       default:
-        w = tbl[15];
+        w = tbl[(1 << (W - 1)) - 1];
         break;
     }
     if (started) {
