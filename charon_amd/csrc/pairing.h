@@ -364,7 +364,12 @@ BLS_HD BLS_INLINE void cyc_decompress(fp12& r, const cyc_c& c, const fp2& z1) {
 }
 BLS_HD BLS_CALL void fp12_cyc_exp_xabs_gs(fp12& r, const fp12& a_in);
 // r = a^|x| for a in the cyclotomic subgroup, by compressed squarings
-BLS_HD BLS_CALL void fp12_cyc_exp_xabs_karabina(fp12& r, const fp12& a_in) {
+// Inlined into the final exponentiation's five call sites it measured slower (C2 1.710M -> 1.685M verifies/s; with
+// the nine FE products inlined too 1.666M, profiles/r02_sched_variants.txt), so it stays a call.
+#ifndef BLS_KAR_EXP_CALL
+#define BLS_KAR_EXP_CALL BLS_CALL
+#endif
+BLS_HD BLS_KAR_EXP_CALL void fp12_cyc_exp_xabs_karabina(fp12& r, const fp12& a_in) {
   static_assert(X_ABS == 0xd201000000010000ull, "the squaring counts below are |x|'s set bits");
   cyc_c st[6];  // a^(2^k) for k = 16, 48, 57, 60, 62, 63
   cyc_c c;
