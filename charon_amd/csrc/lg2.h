@@ -8,8 +8,8 @@
 //     lane owns c1 (Fp12 = Fp6[w]).  Halves are exchanged with DPP quad_perm [1,0,3,2] moves (one VALU instruction
 //     per dword, no LDS), which need both lanes of a pair active: every exchange sits in pair-uniform control flow.
 //   * The final exponentiation runs on the split value: each lane computes its own half of every product
-//     (Fp12 products: two Fp6 products per lane, schoolbook; cyclotomic squarings: five Fp2 squarings per lane
-//     instead of nine), so its latency is roughly halved.  The inversion of the easy part is computed redundantly
+//     (Fp12 products: two Fp6 products per lane, schoolbook; the exponentiations by |x| as Karabina's compressed
+//     squarings with three Fp2 squarings per lane instead of six), so its latency is roughly halved.  The inversion of the easy part is computed redundantly
 //     on both lanes from the gathered value.
 //
 // Semantics are those of pairing_check_verify / the RLC checks (ops.h, rlc.h): the same formulas, the same e^3
@@ -190,6 +190,114 @@ BLS_CALL __device__ void fp12h_exp_xabs(fp6& r, const fp6& a_in, uint32_t m) {
   r = acc;
 }
 
+// Karabina's compressed squarings on a lane pair (pairing.h fp12_cyc_exp_xabs_karabina).  Both lanes carry the same
+// compressed state (z2..z5).  Per squaring the even lane squares z2, z3, z2 + z3 and the odd lane z4, z5, z4 + z5
+// (three Fp2 squarings per lane instead of Granger-Scott's five), each forms A = 2 z z' and B = z^2 + xi z'^2 of its
+// pair, the pair swaps (A, B), and both lanes form the new state:
+//   z2' = 2 z2 + 3 xi (2 z4 z5),  z3' = 3 (z4^2 + xi z5^2) - 2 z3,  z4' = 3 (z2^2 + xi z3^2) - 2 z4,  z5' = 2 z5 + 3 (2 z2 z3).
+// The state is bit-identical on both lanes, so every branch below is pair-uniform (DPP needs both lanes).
+__device__ __forceinline__ void cyc_sqr_compressed_pair(cyc_c& c, uint32_t m) {
+  const fp2 x = sel(m, c.z4, c.z2), y = sel(m, c.z5, c.z3);
+  fp2 xy, sx, sy, sxy;
+  fp2_add(xy, x, y);
+  BLS_KAR_FP2_SQR(sx, x);
+  BLS_KAR_FP2_SQR(sy, y);
+  BLS_KAR_FP2_SQR(sxy, xy);
+  fp2 A, B;
+  fp2_sub(A, sxy, sx);
+  fp2_sub(A, A, sy);  // even 2 z2 z3 | odd 2 z4 z5
+  fp2_mul_xi(B, sy);
+  fp2_add(B, B, sx);  // even z2^2 + xi z3^2 | odd z4^2 + xi z5^2
+  fp2 Ao, Bo;
+  pair_swap(Ao, A);
+  pair_swap(Bo, B);
+  const fp2 p45 = sel(m, A, Ao), q45 = sel(m, B, Bo);  // 2 z4 z5, z4^2 + xi z5^2
+  const fp2 p23 = sel(m, Ao, A), q23 = sel(m, Bo, B);  // 2 z2 z3, z2^2 + xi z3^2
+  fp2 t, v;
+  fp2_mul_xi(t, p45);
+  fp2_add(v, c.z2, t);
+  fp2_add(v, v, v);
+  fp2_add(c.z2, v, t);
+  fp2_sub(v, q45, c.z3);
+  fp2_add(v, v, v);
+  fp2_add(c.z3, v, q45);
+  fp2_sub(v, q23, c.z4);
+  fp2_add(v, v, v);
+  fp2_add(c.z4, v, q23);
+  fp2_add(v, c.z5, p23);
+  fp2_add(v, v, v);
+  fp2_add(c.z5, v, p23);
+}
+
+// r = a^|x| (split) by compressed squarings; the six saved powers are decompressed on both lanes (one batch
+// inversion) and multiplied as split values.  Degenerate inputs (a denominator 0) take fp12h_exp_xabs.
+BLS_CALL __device__ void fp12h_exp_xabs_karabina(fp6& r, const fp6& a_in, uint32_t m) {
+  static_assert(X_ABS == 0xd201000000010000ull, "the squaring counts below are |x|'s set bits");
+  cyc_c c;
+  {
+    const fp6 h = a_in;
+    fp6 o;
+    pair_swap(o, h);  // even h = (z0, z4, z3), o = (z2, z1, z5); odd the other way round
+    c.z2 = sel(m, h.c0, o.c0);
+    c.z3 = sel(m, o.c2, h.c2);
+    c.z4 = sel(m, o.c1, h.c1);
+    c.z5 = sel(m, h.c2, o.c2);
+  }
+  cyc_c st[6];
+  int s = 0;
+#pragma unroll 1
+  for (int k = 1; k <= 63; ++k) {
+    cyc_sqr_compressed_pair(c, m);
+    if (k == 16 || k == 48 || k == 57 || k == 60 || k == 62 || k == 63) st[s++] = c;
+  }
+  fp2 num[6], den[6], pre[6];
+#pragma unroll 1
+  for (s = 0; s < 6; ++s) cyc_z1_parts(num[s], den[s], st[s]);
+  pre[0] = den[0];
+#pragma unroll 1
+  for (s = 1; s < 6; ++s) fp2_mul(pre[s], pre[s - 1], den[s]);
+  if (fp2_is_zero(pre[5])) {  // same on both lanes
+    fp12h_exp_xabs(r, a_in, m);
+    return;
+  }
+  fp2 inv;
+  fp2_inv(inv, pre[5]);
+  fp6 acc;
+#pragma unroll 1
+  for (s = 5; s >= 0; --s) {
+    fp2 is, z1;
+    if (s > 0) {
+      fp2_mul(is, inv, pre[s - 1]);  // 1 / den[s]
+      fp2_mul(inv, inv, den[s]);
+    } else {
+      is = inv;
+    }
+    fp2_mul(z1, num[s], is);
+    fp12 d;
+    cyc_decompress(d, st[s], z1);
+    const fp6 dh = sel(m, d.c1, d.c0);
+    if (s == 5) {
+      acc = dh;
+    } else {
+      fp6 x = acc, y;
+      fp12h_mul(y, x, dh, m);
+      acc = y;
+    }
+  }
+  r = acc;
+}
+
+#ifndef BLS_LG2_KARABINA
+#define BLS_LG2_KARABINA 1
+#endif
+__device__ __forceinline__ void fp12h_exp(fp6& r, const fp6& a_in, uint32_t m) {
+#if BLS_LG2_KARABINA
+  fp12h_exp_xabs_karabina(r, a_in, m);
+#else
+  fp12h_exp_xabs(r, a_in, m);
+#endif
+}
+
 // final_exponentiation (pairing.h) on a split value: same formula, split operations.
 BLS_CALL __device__ void final_exponentiation_split(fp6& r, const fp6& f_in, uint32_t m) {
   const fp6 f = f_in;
@@ -204,18 +312,18 @@ BLS_CALL __device__ void final_exponentiation_split(fp6& r, const fp6& f_in, uin
   fp12h_frobenius(t, mm, 2, m);
   fp12h_mul(mm, t, mm, m);
   // hard part
-  fp12h_exp_xabs(t0, mm, m);
+  fp12h_exp(t0, mm, m);
   fp12h_mul(t0, t0, mm, m);
   fp12h_conj(t0, t0, m);
-  fp12h_exp_xabs(u, t0, m);
+  fp12h_exp(u, t0, m);
   fp12h_mul(u, u, t0, m);
   fp12h_conj(t0, u, m);
-  fp12h_exp_xabs(u, t0, m);
+  fp12h_exp(u, t0, m);
   fp12h_conj(u, u, m);
   fp12h_frobenius(t1, t0, 1, m);
   fp12h_mul(t1, t1, u, m);
-  fp12h_exp_xabs(u, t1, m);
-  fp12h_exp_xabs(u, u, m);
+  fp12h_exp(u, t1, m);
+  fp12h_exp(u, u, m);
   fp12h_frobenius(t2, t1, 2, m);
   fp12h_mul(t2, t2, u, m);
   fp12h_conj(u, t1, m);
