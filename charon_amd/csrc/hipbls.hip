@@ -255,7 +255,7 @@ int launch_verify(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d
     });
   HIP_TRY(ws.ensure(n * 120 * 4));
   int rc = timed("verify_prep", s, [&] {
-    hipLaunchKernelGGL(k_verify_prep, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs,
+    hipLaunchKernelGGL(k_verify_prep, dim3((unsigned)(2 * grid_for(n))), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs,
                        n, (uint32_t*)ws.p, d_status);
   });
   if (rc) return rc;

@@ -27,16 +27,29 @@ __global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restri
 }
 
 // ---------------------------------------------------------------- lane-pair Verify (lg2.h)
-// Stage 1, one lane per item: decode + subgroup-check pk and sig, hash the message; the points go to SoA
-// (pk 24 words, H(m) 48, sig 48 per item: `ws` holds 120 words x n) and the status is final or RLC_PENDING.
-// Status order is op_verify's.
+// Stage 1, two waves per 64 items: the first grid_for(n) blocks decode + check pk and sig and set the status (final or
+// RLC_PENDING), the next grid_for(n) blocks hash the messages.  The roles are per workgroup (kBlock = one wave), so
+// the two run side by side on different SIMDs and the stage's latency is the hash alone, not hash + decode (the
+// batches that take lane pairs leave SIMDs free).  Every message is hashed, whatever its item's status.  The points
+// go to SoA (pk 24 words, H(m) 48, sig 48 per item: `ws` holds 120 words x n).  Status order is op_verify's.
 __global__ void __launch_bounds__(kBlock) k_verify_prep(const uint8_t* __restrict__ pks,
                                                         const uint8_t* __restrict__ msgs,
                                                         const uint64_t* __restrict__ offs,
                                                         const uint8_t* __restrict__ sigs, uint64_t n,
                                                         uint32_t* __restrict__ ws, int32_t* __restrict__ status) {
-  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t nb = (n + kBlock - 1) / kBlock;
+  const bool hash_role = blockIdx.x >= nb;  // uniform per workgroup
+  const uint64_t i = (blockIdx.x - (hash_role ? nb : 0)) * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (hash_role) {
+    const uint64_t o0 = offs[i], o1 = offs[i + 1];
+    g2j hj;
+    hash_to_g2(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43);
+    g2a hm;
+    jac_to_aff(hm, hj);
+    soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);
+    return;
+  }
   g1a pk;
   g2a sig;
   int st = RLC_PENDING;
@@ -51,13 +64,7 @@ __global__ void __launch_bounds__(kBlock) k_verify_prep(const uint8_t* __restric
       st = verify_inf_status(ds, sig);  // KeyValidate / e(pk,H) != 1
   }
   if (st == RLC_PENDING) {
-    const uint64_t o0 = offs[i], o1 = offs[i + 1];
-    g2j hj;
-    hash_to_g2(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43);
-    g2a hm;
-    jac_to_aff(hm, hj);
     soa_store<24>(ws, n, i, &pk.x.v[0]);
-    soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);
     soa_store<48>(ws + 72 * n, n, i, &sig.x.c0.v[0]);
   }
   status[i] = st;

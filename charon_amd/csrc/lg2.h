@@ -70,7 +70,7 @@ BLS_CALL __device__ void fp12h_mul_full(fp6& r, const fp12& a_in, const fp12& b_
 }
 
 // Own half of a*b for split a, b.
-BLS_CALL __device__ void fp12h_mul(fp6& r, const fp6& ah_in, const fp6& bh_in, uint32_t m) {
+__device__ __forceinline__ void fp12h_mul_inl(fp6& r, const fp6& ah_in, const fp6& bh_in, uint32_t m) {
   const fp6 ah = ah_in, bh = bh_in;
   fp6 ao, bo;
   pair_swap(ao, ah);
@@ -84,6 +84,7 @@ BLS_CALL __device__ void fp12h_mul(fp6& r, const fp6& ah_in, const fp6& bh_in, u
   const fp6 q = sel(m, p2, vp2);
   fp6_add(r, p1, q);
 }
+BLS_CALL __device__ void fp12h_mul(fp6& r, const fp6& ah_in, const fp6& bh_in, uint32_t m) { fp12h_mul_inl(r, ah_in, bh_in, m); }
 
 // conj: c1 -> -c1 (odd lane negates)
 __device__ __forceinline__ void fp12h_conj(fp6& r, const fp6& h, uint32_t m) {
@@ -229,6 +230,9 @@ __device__ __forceinline__ void cyc_sqr_compressed_pair(cyc_c& c, uint32_t m) {
   fp2_add(c.z5, v, p23);
 }
 
+#ifndef BLS_LG2_KAR_MUL
+#define BLS_LG2_KAR_MUL fp12h_mul_inl  // inlined: n = 10,000 lane-pair Verify 27.82 -> 27.52 ms, C3 +0.9 %
+#endif
 // r = a^|x| (split) by compressed squarings; the six saved powers are decompressed on both lanes (one batch
 // inversion) and multiplied as split values.  Degenerate inputs (a denominator 0) take fp12h_exp_xabs.
 BLS_CALL __device__ void fp12h_exp_xabs_karabina(fp6& r, const fp6& a_in, uint32_t m) {
@@ -280,7 +284,7 @@ BLS_CALL __device__ void fp12h_exp_xabs_karabina(fp6& r, const fp6& a_in, uint32
       acc = dh;
     } else {
       fp6 x = acc, y;
-      fp12h_mul(y, x, dh, m);
+      BLS_LG2_KAR_MUL(y, x, dh, m);
       acc = y;
     }
   }
