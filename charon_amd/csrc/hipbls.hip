@@ -177,6 +177,8 @@ int ws_end(hipStream_t s) {
 }
 
 uint64_t grid_for(uint64_t n) { return (n + kBlock - 1) / kBlock; }
+// Verify batches up to this size hash each message on a lane pair in the prep stage (k_verify_prep pair_hash).
+constexpr uint64_t kPairHashMaxVerify = 16384;
 
 // wait = false: only events that have completed are folded in (never blocks a launch).
 void drain_timing(TimingSlot& t, bool wait) {
@@ -255,8 +257,9 @@ int launch_verify(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d
     });
   HIP_TRY(ws.ensure(n * 120 * 4));
   int rc = timed("verify_prep", s, [&] {
-    hipLaunchKernelGGL(k_verify_prep, dim3((unsigned)(2 * grid_for(n))), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs,
-                       n, (uint32_t*)ws.p, d_status);
+    const int pair_hash = n <= kPairHashMaxVerify ? 1 : 0;
+    hipLaunchKernelGGL(k_verify_prep, dim3((unsigned)((pair_hash ? 3 : 2) * grid_for(n))), dim3(kBlock), 0, s, d_pks,
+                       d_msgs, d_offs, d_sigs, n, (uint32_t*)ws.p, d_status, pair_hash);
   });
   if (rc) return rc;
   return timed("verify_pair_lg2", s, [&] {

@@ -32,13 +32,31 @@ __global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restri
 // the two run side by side on different SIMDs and the stage's latency is the hash alone, not hash + decode (the
 // batches that take lane pairs leave SIMDs free).  Every message is hashed, whatever its item's status.  The points
 // go to SoA (pk 24 words, H(m) 48, sig 48 per item: `ws` holds 120 words x n).  Status order is op_verify's.
+// pair_hash: the hash workgroups are 2 grid_for(n) and a lane pair hashes each message (small batches, where the
+// extra waves still find idle SIMDs).
 __global__ void __launch_bounds__(kBlock) k_verify_prep(const uint8_t* __restrict__ pks,
                                                         const uint8_t* __restrict__ msgs,
                                                         const uint64_t* __restrict__ offs,
                                                         const uint8_t* __restrict__ sigs, uint64_t n,
-                                                        uint32_t* __restrict__ ws, int32_t* __restrict__ status) {
+                                                        uint32_t* __restrict__ ws, int32_t* __restrict__ status,
+                                                        int pair_hash) {
   const uint64_t nb = (n + kBlock - 1) / kBlock;
   const bool hash_role = blockIdx.x >= nb;  // uniform per workgroup
+  if (hash_role && pair_hash) {  // lanes 2i, 2i+1 hash item i together (lg2.h hash_to_g2_pair)
+    const uint64_t t = (blockIdx.x - nb) * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t i = t >> 1;
+    if (i >= n) return;  // same on both lanes of the pair
+    const uint32_t m = (t & 1) ? ~0u : 0u;
+    const uint64_t o0 = offs[i], o1 = offs[i + 1];
+    g2j hj;
+    hash_to_g2_pair(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43, m);
+    if (!m) {
+      g2a hm;
+      jac_to_aff(hm, hj);
+      soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);
+    }
+    return;
+  }
   const uint64_t i = (blockIdx.x - (hash_role ? nb : 0)) * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (hash_role) {
