@@ -121,9 +121,97 @@ def main():
     add_group(bad, "undecodable partial")
     add_group({1: good[1], 2: non_subgroup_g2(rng)}, "partial not in G2")
 
+    small = small_order_cases(random.Random(SEED + 13))
+
     with open(OUT, "w") as f:
-        json.dump({"seed": SEED, "verify": cases, "threshold_aggregate": tagg}, f, indent=1)
-    print("wrote %s: %d verify, %d tagg" % (OUT, len(cases), len(tagg)))
+        json.dump({"seed": SEED, "verify": cases, "threshold_aggregate": tagg, "small_order": small}, f, indent=1)
+    print("wrote %s: %d verify, %d tagg, %d small-order" % (OUT, len(cases), len(tagg), len(small["verify"])))
+
+
+# ---------------------------------------------------------------- points of small order (cofactor torsion)
+# Verify decides the signature's G2 membership from its own Miller loop (charon_amd/csrc/pairing.h
+# g2_subgroup_from_miller): the loop runs T over |x|'s bits from T = sig, and a point of small order makes a doubling
+# or addition step exceptional (Z = 0).  herumi rejects such a signature at deserialization (tbls/herumi.go:291-294),
+# status 2, whatever the key.  These cases pin that on every device layout.  Public keys of small order (G1 cofactor
+# torsion: orders 3 and 11) exercise the phi subgroup test the same way (herumi.go:286-289, status 1).
+X = -bls.X_ABS
+H1 = (X - 1) ** 2 // 3
+H2 = (X ** 8 - 4 * X ** 7 + 5 * X ** 6 - 4 * X ** 4 + 6 * X ** 3 - 4 * X ** 2 - 4 * X + 13) // 9
+
+
+def _rand_g2(rng):
+    while True:
+        px = (rng.randrange(bls.P), rng.randrange(bls.P))
+        py = bls.f2_sqrt(bls.f2_add(bls.f2_mul(bls.f2_sqr(px), px), bls.B2))
+        if py is not None:
+            return (px, py)
+
+
+def _rand_g1(rng):
+    while True:
+        px = rng.randrange(bls.P)
+        py = bls.fp_sqrt((px ** 3 + 4) % bls.P)
+        if py is not None:
+            return (px, py)
+
+
+def _of_order(rng, q, n_total, rand_pt, mul):
+    """A point of order exactly q: the q-primary part of a random point, multiplied down to order q."""
+    m = n_total
+    while m % q == 0:
+        m //= q
+    while True:
+        pt = mul(rand_pt(rng), m)
+        if pt is None:
+            continue
+        while mul(pt, q) is not None:
+            pt = mul(pt, q)
+        assert mul(pt, q) is None
+        return pt
+
+
+def small_order_cases(rng):
+    sks = [rng.randrange(1, bls.R).to_bytes(32, "big") for _ in range(2)]
+    pks = [bls.secret_to_public_key(s) for s in sks]
+    msgs = [rng.randbytes(32) for _ in range(2)]
+    sig = bls.sign(sks[0], msgs[0])
+    sig_pt = bls.g2_decompress(sig)
+    pk_pt = bls.g1_decompress(pks[0])
+    inf_pk = bls.g1_compress(None)
+    sigs, pkeys = [], []
+    for q in (13, 23):
+        s = _of_order(rng, q, H2 * bls.R, _rand_g2, bls.g2_mul)
+        sigs.append((bls.g2_compress(s), "signature of order %d" % q))
+        sigs.append((bls.g2_compress(bls.g2_add(sig_pt, s)), "honest signature + order-%d point" % q))
+    for q in (3, 11):
+        p = _of_order(rng, q, H1 * bls.R, _rand_g1, bls.g1_mul)
+        pkeys.append((bls.g1_compress(p), "public key of order %d" % q))
+        pkeys.append((bls.g1_compress(bls.g1_add(pk_pt, p)), "public key + order-%d point" % q))
+    cases = []
+
+    def add(pk, msg, s, note):
+        cases.append({"pk": pk.hex(), "msg": msg.hex(), "sig": s.hex(), "status": bls.verify_status(pk, msg, s),
+                      "note": note})
+
+    for s, note in sigs:
+        add(pks[0], msgs[0], s, note + ", signer's key")
+        add(pks[0], msgs[1], s, note + ", wrong message")
+        add(pks[1], msgs[0], s, note + ", other key")
+        add(inf_pk, msgs[0], s, note + ", infinity key")
+    for p, note in pkeys:
+        add(p, msgs[0], sig, note + ", honest signature")
+        add(p, msgs[0], sigs[0][0], note + ", order-13 signature")
+    add(pks[0], msgs[0], sig, "honest control")
+    assert [c["status"] for c in cases[:16]] == [2] * 16 and [c["status"] for c in cases[16:24]] == [1] * 8
+    # threshold aggregation with a small-order partial (herumi deserializes every partial first: status 2)
+    secret = rng.randrange(1, bls.R)
+    shares = bls.threshold_split_poly(secret, [rng.randrange(bls.R)], 3)
+    parts = {i: bls.sign(shares[i], msgs[0]) for i in (1, 2)}
+    tagg = [{"parts": {"1": parts[1].hex(), "2": s.hex()}, "note": note} for s, note in sigs]
+    tagg.append({"parts": {str(k): v.hex() for k, v in parts.items()}, "note": "honest 2-of-3",
+                 "out": bls.threshold_aggregate(parts).hex()})
+    return {"verify": cases, "threshold_aggregate": tagg, "msg": msgs[0].hex(), "sk": sks[0].hex(),
+            "pk": pks[0].hex()}
 
 
 if __name__ == "__main__":

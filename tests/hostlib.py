@@ -26,6 +26,28 @@ def build():
     if _stale():
         subprocess.check_call(["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-o", LIB, SRC])
     build_cpu_baseline()
+    build_gpu_units()
+
+
+GU_SRC = os.path.join(HERE, "native", "gpu_units.hip")
+GU_LIB = os.path.join(HERE, "native", "libgpu_units.so")
+
+
+def build_gpu_units():
+    """Test-only device entry points into single kernel building blocks (tests/test_gpu_units.py), gfx950."""
+    deps = [GU_SRC] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    if not os.path.exists(GU_LIB) or any(os.path.getmtime(d) > os.path.getmtime(GU_LIB) for d in deps):
+        subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                               "-I" + CSRC, "-I" + os.path.join(os.path.dirname(HERE), "include"),
+                               "-o", GU_LIB + ".tmp", GU_SRC])
+        os.replace(GU_LIB + ".tmp", GU_LIB)
+
+
+def gpu_units_lib():
+    """ctypes handle on tests/native/libgpu_units.so (built by __graft_entry__.build(); -m gpu tests only)."""
+    if not os.path.exists(GU_LIB):
+        raise RuntimeError("tests/native/libgpu_units.so not built (run __graft_entry__.build())")
+    return ctypes.CDLL(GU_LIB)
 
 
 def build_cpu_baseline():

@@ -294,8 +294,9 @@ def test_queue_async_in_flight_throughput(impl):
     b1, _ = impl.queue_stats()
     assert got == want
     rate = n / dt
+    # the rate is reported, not gated: it depends on the host's Python threads and ctypes, not on parity
     print("\nqueue: %d n=1 Verify calls from 64 threads in %.3f s = %.0f Verify/s, %d batches" % (n, dt, rate, b1 - b0))
-    assert rate > 40000  # measured 50.7k/s on MI355X
+    assert b1 - b0 < n // 64, (b1 - b0, n)  # coalesced: far fewer launches than calls
 
 
 # ---------------------------------------------------------------- cross-stream workspace ordering
