@@ -1,19 +1,24 @@
 // hipbls: C-ABI host runtime (include/hipbls.h) over the gfx950 kernels in kernels.h.
 //
-// Execution model: one process per GPU (charon runs one node process; bench.py one rank per GPU).  The
-// process has one device context: the device index, a library stream, reusable device workspaces and a
-// mutex.  The C-ABI is called concurrently from many goroutines (tbls/tbls.go:79-141), and a goroutine can
-// move between OS threads between two calls, so every entry point binds the context's device on the calling
-// thread (hipSetDevice is per host thread in HIP) before it touches memory or streams.
+// Execution model: ONE process drives every GPU of the node.  charon is one Go process per node that wires every
+// component through one global tbls implementation (/root/reference/app/app.go:127, tbls/tbls.go:11-14), so the
+// library keeps one device context per GPU it was given (hipbls_init_devices; hipbls_init(d) is the one-device
+// case).  A context owns its device index, a library stream, reusable device workspaces, the resident pubshare
+// table, the H(m) cache, its submission-queue worker and a mutex.
 //
-//   * Host-buffer entry points copy in, launch, copy out and synchronize, holding the context lock.
-//   * *_device entry points only enqueue on the caller's stream.  Calls that share a workspace are ordered on
-//     the device: each waits for the previous workspace user's completion event (ws_done) before its first
-//     kernel and records the event after its last, so two calls on different streams never see each other's
-//     H(m) table, fallback list or partial sums.
-//   * hipbls_verify / hipbls_verify_submit go through the submission queue (VerifyQueue): concurrent n = 1
-//     calls from many threads are coalesced into one launch per batch; the queue's worker thread owns its own
-//     stream and buffers, and no caller holds a lock while the GPU runs.
+//   * Host-buffer entry points split the batch into contiguous ranges (items, or whole validator groups / message
+//     runs: SURVEY.md §8e shards by validator index) across the contexts, one host thread per range, and each
+//     range copies in, launches, copies out and synchronizes on its own device under its own context lock.  The
+//     results land directly in the caller's arrays; nothing crosses devices (no RCCL inside one process).  Small
+//     batches stay on one context, picked round robin, so concurrent callers spread over the GPUs.
+//   * *_device entry points run on the context of the device that owns the caller's memory and only enqueue.
+//     Calls that share a workspace are ordered on the device: each waits for the previous workspace user's
+//     completion event (ws_done) before its first kernel and records the event after its last.
+//   * hipbls_verify / hipbls_verify_submit go through the submission queues: each item goes to the context its
+//     message hashes to (all partials of one signing root, i.e. of one validator duty, meet on one GPU and share
+//     one H(m)), where a worker thread coalesces concurrent n = 1 calls into batched launches.
+//   * A goroutine can move between OS threads between two calls, and hipSetDevice is per host thread, so every
+//     entry point binds its context's device on the calling thread before it touches memory or streams.
 #include <hip/hip_runtime.h>
 
 #include <array>
@@ -32,11 +37,13 @@
 #include <unordered_map>
 #include <vector>
 
+#include <sys/random.h>
+
 #include "kernels.h"
 
 namespace {
 
-// ============================================================================ device context
+// ============================================================================ device contexts
 thread_local std::string g_last_error;
 
 struct DevBuf {
@@ -74,8 +81,38 @@ struct HCache {
   uint64_t hits = 0, misses = 0;
 };
 
+// One open or running batch of the submission queue.
+struct VBatch {
+  std::vector<uint8_t> pk, sig, msg;
+  std::vector<uint64_t> off{0};
+  std::vector<int32_t> status;
+  int rc = HIPBLS_OK;
+  bool done = false;
+  uint64_t n() const { return off.size() - 1; }
+};
+
+// Per-context submission queue (worker, stream and buffers of its own).
+struct VerifyQueue {
+  std::mutex mu;
+  std::condition_variable cv_work, cv_done;
+  std::deque<std::shared_ptr<VBatch>> open;  // accepting (back) / waiting for the worker (front)
+  std::unordered_map<uint64_t, std::pair<std::shared_ptr<VBatch>, uint32_t>> tickets;
+  uint64_t next_ticket = 1;
+  std::thread worker;
+  bool started = false, stop = false;
+  uint64_t batches = 0, items = 0, keyed = 0;
+  hipStream_t stream = nullptr;
+  DevBuf d_pk, d_sig, d_msg, d_off, d_st, d_ws, d_kidx, d_midx, d_slot, d_mlist, d_rlc_st;
+  // host staging of the keyed path (reused across batches)
+  std::vector<uint32_t> kidx, midx, order, slot, miss;
+  std::vector<uint8_t> sig_sorted, umsg;
+  std::vector<uint64_t> uoff;
+  std::vector<int32_t> st_sorted;
+};
+
 struct Context {
   int device = -1;
+  int slot = 0;  // index in the context list
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevBuf b_pk, b_msg, b_off, b_sig, b_st, b_out, b_ids, b_pts, b_pst, b_aux, b_part, b_bad;
@@ -83,15 +120,18 @@ struct Context {
   DevBuf t_code, t_tab, b_kidx;                                            // resident pubshare table + key indices
   DevBuf v_ws;                                                             // lane-pair Verify points (SoA)
   uint64_t t_size = 0;
-  // RLC sub-batches in flight.  The process gets GPU_MAX_HW_QUEUES = 4 hardware queues, shared by the caller's
-  // stream (which also hashes the messages), the library stream and these; a kernel trace
+  // pubshare bytes -> table index (host side), for the submission queue's keyed path
+  std::unordered_map<std::string, uint32_t> t_index;
+  // RLC sub-batches in flight.  The process gets GPU_MAX_HW_QUEUES = 4 hardware queues per device, shared by the
+  // caller's stream (which also hashes the messages), the library stream and these; a kernel trace
   // (profiles/r01_rlc_trace.txt) showed a third sub-stream landing on an occupied queue and serializing behind
   // it, so two sub-batches.
   static constexpr int kSub = 2;
   hipStream_t sub[kSub] = {};
   hipEvent_t ev_fork = nullptr, ev_hash = nullptr, ev_join[kSub] = {};
   hipEvent_t ws_done = nullptr;  // last workspace user's completion (cross-stream ordering)
-  uint64_t r_windows = 0;        // window count of the last RLC call (hipbls_rlc_stats)
+  uint64_t r_windows = 0;        // window count of this context's last RLC call (hipbls_rlc_stats)
+  uint64_t r_call = 0;           // entry-point call that call belonged to
   // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
   DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_FS, m_flag;
   // Verdicts come back through a ring of pinned slots, one per batch check in flight, so a launch only waits
@@ -101,19 +141,27 @@ struct Context {
   hipEvent_t rlcb_ev[kRlcbSlots] = {};
   hipEvent_t rlcb_ev_items = nullptr, rlcb_ev_msm = nullptr;
   bool rlcb_pending[kRlcbSlots] = {};
-  uint64_t rlcb_seq[kRlcbSlots] = {};  // launch order of the check in each slot
+  uint64_t rlcb_seq[kRlcbSlots] = {};   // launch order of the check in each slot
+  uint64_t rlcb_call[kRlcbSlots] = {};  // entry-point call of the check in each slot
   uint64_t rlcb_next_seq = 0, rlcb_last_seq = 0;
-  int rlcb_last = -1;                 // newest verdict read back: -1 none, 0 failed, 1 passed
-  int rlcb_skipped = 0;               // AUTO: calls run windows-only since the last failed batch check
+  int rlcb_last = -1;                   // newest verdict read back: -1 none, 0 failed, 1 passed
+  uint64_t rlcb_last_call = 0;          // entry-point call of that verdict
+  int rlcb_skipped = 0;                 // AUTO: calls run windows-only since the last failed batch check
   uint64_t rlcb_attempted = 0, rlcb_passed = 0;
   HCache hcache;
   std::mutex tmu;                            // timing table (also used by the queue worker)
   std::map<std::string, TimingSlot> timing;  // per kernel name: HIP events on the launch stream
-  std::atomic<bool> timing_enabled{false};
+  VerifyQueue q;
 };
 
-Context g_ctx;
+// The context list is written once, under g_init_mu, before g_nctx is published; contexts live for the process.
+std::vector<Context*> g_ctxs;
+std::atomic<int> g_nctx{0};
 std::mutex g_init_mu;
+std::atomic<bool> g_timing{false};
+std::atomic<uint64_t> g_rr{0};        // round-robin context for single-range calls
+std::atomic<uint64_t> g_call_seq{0};  // RLC entry-point calls (hipbls_rlc_stats / hipbls_rlc_batch_stats)
+constexpr int kMaxContexts = 64;
 
 int set_err(const char* what, hipError_t e) {
   g_last_error = std::string(what) + ": " + hipGetErrorString(e);
@@ -130,50 +178,203 @@ int arg_err(const char* what) {
     if (_e != hipSuccess) return set_err(#expr, _e); \
   } while (0)
 
-int init_locked(int device) {
+int nctx() { return g_nctx.load(std::memory_order_acquire); }
+Context& ctx(int k) { return *g_ctxs[k]; }
+
+int init_locked(const std::vector<int>& ids) {
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0) return set_err("hipGetDeviceCount (no GPU)", e == hipSuccess ? hipErrorNoDevice : e);
-  if (device < 0) HIP_TRY(hipGetDevice(&device));
-  if (device >= ndev) return arg_err("device index out of range");
-  HIP_TRY(hipSetDevice(device));
-  HIP_TRY(hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking));
-  HIP_TRY(hipEventCreateWithFlags(&g_ctx.ws_done, hipEventDisableTiming));
-  const char* t = getenv("HIPBLS_TIMING");
-  if (t && t[0] == '1') g_ctx.timing_enabled = true;
-  g_ctx.device = device;
-  return HIPBLS_OK;
-}
-
-// Binds the context's device on the calling thread (initializing on first use).
-int bind_device() {
-  if (g_ctx.device < 0) {
-    std::lock_guard<std::mutex> lk(g_init_mu);
-    if (g_ctx.device < 0) {
-      const int rc = init_locked(-1);
-      if (rc) return rc;
-    }
+  if (ids.empty() || ids.size() > (size_t)kMaxContexts) return arg_err("device list empty or longer than 64");
+  for (int d : ids)
+    if (d < 0 || d >= ndev) return arg_err("device index out of range");
+  std::vector<Context*> made;
+  for (size_t k = 0; k < ids.size(); ++k) {
+    Context* c = new Context();
+    c->device = ids[k];
+    c->slot = (int)k;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming));
+    made.push_back(c);
   }
-  HIP_TRY(hipSetDevice(g_ctx.device));
+  const char* t = getenv("HIPBLS_TIMING");
+  if (t && t[0] == '1') g_timing = true;
+  g_ctxs = made;
+  g_nctx.store((int)made.size(), std::memory_order_release);
   return HIPBLS_OK;
 }
 
-// Entry-point prologue: device bound on this thread, context lock held for the scope.
-#define ENTER()                                   \
-  int _brc = bind_device();                       \
-  if (_brc) return _brc;                          \
-  std::lock_guard<std::mutex> _lk(g_ctx.mu)
+// HIPBLS_DEVICES = "all" | "0,2,5" picks the devices of a process that never calls hipbls_init*; otherwise the
+// calling thread's current device.
+int default_devices(std::vector<int>& ids) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  const char* env = getenv("HIPBLS_DEVICES");
+  if (env && env[0]) {
+    if (!strcmp(env, "all")) {
+      for (int d = 0; d < ndev; ++d) ids.push_back(d);
+    } else {
+      const char* p = env;
+      while (*p) {
+        char* end = nullptr;
+        const long v = strtol(p, &end, 10);
+        if (end == p) return arg_err("HIPBLS_DEVICES: expected 'all' or a comma-separated device list");
+        ids.push_back((int)v);
+        p = *end == ',' ? end + 1 : end;
+        if (*end && *end != ',') return arg_err("HIPBLS_DEVICES: expected 'all' or a comma-separated device list");
+      }
+    }
+    return HIPBLS_OK;
+  }
+  int d = 0;
+  HIP_TRY(hipGetDevice(&d));
+  ids.push_back(d);
+  return HIPBLS_OK;
+}
 
-hipStream_t pick(void* stream) { return stream ? (hipStream_t)stream : g_ctx.stream; }
+int ensure_init() {
+  if (nctx()) return HIPBLS_OK;
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (nctx()) return HIPBLS_OK;
+  std::vector<int> ids;
+  const int rc = default_devices(ids);
+  if (rc) return rc;
+  return init_locked(ids);
+}
+
+int bind(Context& c) {
+  HIP_TRY(hipSetDevice(c.device));
+  return HIPBLS_OK;
+}
+
+// Entry-point prologue for one context: device bound on this thread, context lock held for the scope.
+#define ENTER_CTX(c)          \
+  int _brc = bind(c);         \
+  if (_brc) return _brc;      \
+  std::lock_guard<std::mutex> _lk((c).mu)
+
+#define ENSURE_INIT()              \
+  do {                             \
+    int _irc = ensure_init();      \
+    if (_irc) return _irc;         \
+  } while (0)
+
+// The context of the device that owns a caller's device pointer (the *_device entry points): the first context on
+// that device; the first context when the pointer is unknown to HIP.
+Context& ctx_of(const void* p) {
+  const int n = nctx();
+  if (n > 1 && p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) == hipSuccess)
+      for (int k = 0; k < n; ++k)
+        if (ctx(k).device == a.device) return ctx(k);
+    (void)hipGetLastError();
+  }
+  return ctx(0);
+}
+
+hipStream_t pick(Context& c, void* stream) { return stream ? (hipStream_t)stream : c.stream; }
 
 // Workspace ordering: the call's stream waits for the previous workspace user, and publishes its own end.
-int ws_begin(hipStream_t s) {
-  HIP_TRY(hipStreamWaitEvent(s, g_ctx.ws_done, 0));
+int ws_begin(Context& c, hipStream_t s) {
+  HIP_TRY(hipStreamWaitEvent(s, c.ws_done, 0));
   return HIPBLS_OK;
 }
-int ws_end(hipStream_t s) {
-  HIP_TRY(hipEventRecord(g_ctx.ws_done, s));
+int ws_end(Context& c, hipStream_t s) {
+  HIP_TRY(hipEventRecord(c.ws_done, s));
   return HIPBLS_OK;
+}
+
+// ============================================================================ splitting a batch across contexts
+// Contiguous ranges: bounds[0] = 0 < ... < bounds[parts] = n, as equal as possible.  With run keys (e.g. the message
+// index of each item, equal for all partials of one validator), an inner bound moves forward to the start of the
+// next run, so a run never straddles two devices, unless that would move it by more than half a share.
+std::vector<uint64_t> plan_ranges(uint64_t n, uint64_t parts, const uint32_t* keys) {
+  if (parts < 1) parts = 1;
+  if (parts > n && n > 0) parts = n;
+  std::vector<uint64_t> b(parts + 1);
+  b[0] = 0;
+  b[parts] = n;
+  const uint64_t share = parts ? n / parts : 0;
+  for (uint64_t k = 1; k < parts; ++k) {
+    uint64_t x = (uint64_t)((unsigned __int128)n * k / parts);
+    if (keys && x > 0 && x < n) {
+      const uint64_t lim = x + share / 2;
+      uint64_t y = x;
+      while (y < n && y < lim && keys[y] == keys[y - 1]) ++y;
+      if (y == n || keys[y] != keys[y - 1]) x = y;  // the next run start, within half a share
+    }
+    b[k] = x < b[k - 1] ? b[k - 1] : x;
+  }
+  return b;
+}
+
+// How many ranges a batch of n units gets: one per context, but never ranges below min_per units.
+uint64_t parts_for(uint64_t n, uint64_t min_per) {
+  const uint64_t k = (uint64_t)nctx();
+  if (k <= 1 || n < 2 * min_per) return 1;
+  const uint64_t p = n / min_per;
+  return p < k ? p : k;
+}
+
+// Runs fn(context, lo, hi) for every range [bounds[j], bounds[j+1]): range j on context j, each on its own host
+// thread (the first on the calling one), with the context's device bound and its lock held.  A single range runs on
+// a round-robin context.  The first failing range's status and error text are returned.
+template <class F>
+int run_ranges(const std::vector<uint64_t>& b, F fn) {
+  const size_t k = b.size() - 1;
+  if (k == 1) {
+    const int n = nctx();
+    Context& c = n == 1 ? ctx(0) : ctx((int)(g_rr.fetch_add(1) % (uint64_t)n));
+    ENTER_CTX(c);
+    return fn(c, b[0], b[1]);
+  }
+  std::vector<int> rc(k, HIPBLS_OK);
+  std::vector<std::string> err(k);
+  auto one = [&](size_t j) {
+    if (b[j] == b[j + 1]) return;
+    Context& c = ctx((int)j);
+    int r = bind(c);
+    if (!r) {
+      std::lock_guard<std::mutex> lk(c.mu);
+      r = fn(c, b[j], b[j + 1]);
+    }
+    rc[j] = r;
+    if (r) err[j] = g_last_error;
+  };
+  std::vector<std::thread> th;
+  th.reserve(k - 1);
+  for (size_t j = 1; j < k; ++j) th.emplace_back(one, j);
+  one(0);
+  for (auto& t : th) t.join();
+  for (size_t j = 0; j < k; ++j)
+    if (rc[j]) {
+      g_last_error = err[j];
+      return rc[j];
+    }
+  return HIPBLS_OK;
+}
+
+// Runs fn(context) on every context (table loads, cache configuration), in parallel.
+template <class F>
+int run_all(F fn) {
+  const int n = nctx();
+  std::vector<uint64_t> b(n + 1);
+  for (int k = 0; k <= n; ++k) b[k] = (uint64_t)k;
+  if (n == 1) {
+    ENTER_CTX(ctx(0));
+    return fn(ctx(0));
+  }
+  return run_ranges(b, [&](Context& c, uint64_t, uint64_t) -> int { return fn(c); });
+}
+
+// Message offsets of items [lo, hi) relative to the range's first message byte.
+const uint64_t* rebase(const uint64_t* offs, uint64_t lo, uint64_t hi, std::vector<uint64_t>& tmp) {
+  if (offs[lo] == 0) return offs + lo;
+  tmp.resize(hi - lo + 1);
+  for (uint64_t i = lo; i <= hi; ++i) tmp[i - lo] = offs[i] - offs[lo];
+  return tmp.data();
 }
 
 uint64_t grid_for(uint64_t n) { return (n + kBlock - 1) / kBlock; }
@@ -204,9 +405,9 @@ void drain_timing(TimingSlot& t, bool wait) {
 // duration per launch is read back through hipbls_kernel_timing).  Off by default: production launches create
 // no events and never wait.
 template <class Launch>
-int timed(const char* name, hipStream_t s, Launch launch) {
+int timed(Context& c, const char* name, hipStream_t s, Launch launch) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  const bool on = g_ctx.timing_enabled.load();
+  const bool on = g_timing.load();
   if (on) {
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -216,8 +417,8 @@ int timed(const char* name, hipStream_t s, Launch launch) {
   HIP_TRY(hipGetLastError());
   if (on) {
     HIP_TRY(hipEventRecord(e1, s));
-    std::lock_guard<std::mutex> lk(g_ctx.tmu);
-    TimingSlot& t = g_ctx.timing[name];
+    std::lock_guard<std::mutex> lk(c.tmu);
+    TimingSlot& t = c.timing[name];
     t.pending.emplace_back(e0, e1);
     if (t.pending.size() > 256) drain_timing(t, false);
   }
@@ -247,41 +448,48 @@ bool use_pairs(uint64_t units, uint64_t auto_max) {
 
 // Verify: fused (one lane per item) or prep + lane-pair check; `ws` is the caller's SoA workspace for the latter
 // (120 words per item), so the library stream and the queue worker never share one.
-int launch_verify(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_offs, const uint8_t* d_sigs,
-                  uint64_t n, int32_t* d_status, hipStream_t s, DevBuf& ws) {
+int launch_verify(Context& c, const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_offs,
+                  const uint8_t* d_sigs, uint64_t n, int32_t* d_status, hipStream_t s, DevBuf& ws) {
   if (n == 0) return HIPBLS_OK;
   if (!use_pairs(n, kLg2MaxVerify))
-    return timed("verify", s, [&] {
+    return timed(c, "verify", s, [&] {
       hipLaunchKernelGGL(k_verify_fused, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs,
                          d_sigs, n, d_status);
     });
   HIP_TRY(ws.ensure(n * 120 * 4));
-  int rc = timed("verify_prep", s, [&] {
+  int rc = timed(c, "verify_prep", s, [&] {
     const int pair_hash = n <= kPairHashMaxVerify ? 1 : 0;
     hipLaunchKernelGGL(k_verify_prep, dim3((unsigned)((pair_hash ? 3 : 2) * grid_for(n))), dim3(kBlock), 0, s, d_pks,
                        d_msgs, d_offs, d_sigs, n, (uint32_t*)ws.p, d_status, pair_hash);
   });
   if (rc) return rc;
-  return timed("verify_pair_lg2", s, [&] {
+  return timed(c, "verify_pair_lg2", s, [&] {
     hipLaunchKernelGGL(k_verify_pair_lg2, dim3((unsigned)grid_for(2 * n)), dim3(kBlock), 0, s,
                        (const uint32_t*)ws.p, n, d_status);
   });
 }
 
-bool use_rlc_batch(uint64_t n);
-int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n,
+bool use_rlc_batch(Context& c, uint64_t n);
+int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n,
                      const uint8_t* d_msgs, const uint64_t* d_offs, uint64_t n_msgs, const rlc_seed& seed,
                      int32_t* d_status, hipStream_t s, const uint32_t* d_kidx, uint32_t* d_H, uint64_t hstride,
                      const uint32_t* d_hslot, const uint32_t* d_mlist, uint64_t n_hash);
 
-int ensure_rlc_streams() {
-  Context& c = g_ctx;
+int ensure_rlc_streams(Context& c) {
   if (c.ev_fork) return HIPBLS_OK;
   for (int k = 0; k < Context::kSub; ++k) HIP_TRY(hipStreamCreateWithFlags(&c.sub[k], hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&c.ev_hash, hipEventDisableTiming));
   for (int k = 0; k < Context::kSub; ++k) HIP_TRY(hipEventCreateWithFlags(&c.ev_join[k], hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
   return HIPBLS_OK;
+}
+
+rlc_seed parse_seed(const uint8_t* seed32) {
+  rlc_seed seed;
+  for (int k = 0; k < 8; ++k)
+    seed.w[k] = (uint32_t)seed32[4 * k] << 24 | (uint32_t)seed32[4 * k + 1] << 16 | (uint32_t)seed32[4 * k + 2] << 8 |
+                (uint32_t)seed32[4 * k + 3];
+  return seed;
 }
 
 // RLC BatchVerify: the batch is cut into up to kSub window-aligned sub-batches, each running items -> window ->
@@ -291,24 +499,21 @@ int ensure_rlc_streams() {
 // back, so the call stays stream-ordered.
 // H table: H(m) of message m is at column hslot[m] (identity when hslot == nullptr) of an affine SoA table with
 // `hstride` columns; k_rlc_hash fills the columns of the n_hash messages listed in mlist (all when nullptr).
-int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n, const uint8_t* d_msgs,
-               const uint64_t* d_offs, uint64_t n_msgs, const uint8_t* seed32, int32_t* d_status, hipStream_t s,
-               const uint32_t* d_kidx = nullptr, uint32_t* d_H = nullptr, uint64_t hstride = 0,
-               const uint32_t* d_hslot = nullptr, const uint32_t* d_mlist = nullptr, uint64_t n_hash = 0) {
-  Context& c = g_ctx;
+int launch_rlc(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n,
+               const uint8_t* d_msgs, const uint64_t* d_offs, uint64_t n_msgs, const rlc_seed& seed,
+               int32_t* d_status, hipStream_t s, uint64_t call, const uint32_t* d_kidx = nullptr,
+               uint32_t* d_H = nullptr, uint64_t hstride = 0, const uint32_t* d_hslot = nullptr,
+               const uint32_t* d_mlist = nullptr, uint64_t n_hash = 0) {
   // d_pks == nullptr: keys from the resident table
   const uint64_t T = c.t_size;
   const int32_t* tcode = (const int32_t*)c.t_code.p;
   const uint32_t* tab = (const uint32_t*)c.t_tab.p;
   c.r_windows = 0;
+  c.r_call = call;
   if (n == 0) return HIPBLS_OK;
   if (n > 0xffffffffull) return arg_err("RLC batch larger than 2^32 items");  // fallback list holds 32-bit indices
-  int rc = ensure_rlc_streams();
+  int rc = ensure_rlc_streams(c);
   if (rc) return rc;
-  rlc_seed seed;
-  for (int k = 0; k < 8; ++k)
-    seed.w[k] = (uint32_t)seed32[4 * k] << 24 | (uint32_t)seed32[4 * k + 1] << 16 | (uint32_t)seed32[4 * k + 2] << 8 |
-                (uint32_t)seed32[4 * k + 3];
   const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
   HIP_TRY(c.r_pk.ensure(n * 36 * 4));
   HIP_TRY(c.r_sig.ensure(n * 72 * 4));
@@ -323,9 +528,9 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
   HIP_TRY(c.r_win.ensure(n_win * 4));
   HIP_TRY(c.r_list.ensure(n * 4));
   HIP_TRY(c.r_cnt.ensure(Context::kSub * 4));
-  if (use_rlc_batch(n))
-    return launch_rlc_batch(d_pks, d_sigs, d_midx, n, d_msgs, d_offs, n_msgs, seed, d_status, s, d_kidx, d_H, hstride,
-                            d_hslot, d_mlist, n_hash);
+  if (use_rlc_batch(c, n))
+    return launch_rlc_batch(c, d_pks, d_sigs, d_midx, n, d_msgs, d_offs, n_msgs, seed, d_status, s, d_kidx, d_H,
+                            hstride, d_hslot, d_mlist, n_hash);
   uint32_t* rpk = (uint32_t*)c.r_pk.p;
   uint32_t* rsig = (uint32_t*)c.r_sig.p;
   int32_t* win = (int32_t*)c.r_win.p;
@@ -338,12 +543,12 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
   if (nsub < 1) nsub = 1;
   const uint64_t win_per = (n_win + nsub - 1) / nsub;
 
-  rc = ws_begin(s);
+  rc = ws_begin(c, s);
   if (rc) return rc;
   HIP_TRY(hipMemsetAsync(cnt, 0, Context::kSub * 4, s));
   HIP_TRY(hipEventRecord(c.ev_fork, s));
   if (n_hash) {
-    rc = timed("rlc_hash", s, [&] {
+    rc = timed(c, "rlc_hash", s, [&] {
       hipLaunchKernelGGL(k_rlc_hash, dim3((unsigned)grid_for(n_hash)), dim3(kBlock), 0, s, d_msgs, d_offs, n_hash,
                          d_mlist, d_H, hstride, d_hslot);
     });
@@ -356,20 +561,20 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
     if (w0 >= w1) continue;
     const uint64_t i0 = w0 * RLC_W, i1 = w1 * RLC_W < n ? w1 * RLC_W : n;
     HIP_TRY(hipStreamWaitEvent(ss, c.ev_fork, 0));
-    rc = timed("rlc_items", ss, [&] {
+    rc = timed(c, "rlc_items", ss, [&] {
       hipLaunchKernelGGL(k_rlc_items, dim3((unsigned)grid_for(i1 - i0)), dim3(kBlock), 0, ss, i0, i1, d_pks, d_sigs,
                          d_midx, n, n_msgs, seed, rpk, rsig, d_status, d_kidx, T, tcode, tab);
     });
     if (rc) return rc;
     HIP_TRY(hipStreamWaitEvent(ss, c.ev_hash, 0));
     if (use_pairs(w1 - w0, kLg2MaxWindows))
-      rc = timed("rlc_window_lg2", ss, [&] {
+      rc = timed(c, "rlc_window_lg2", ss, [&] {
         hipLaunchKernelGGL(k_rlc_window_lg2, dim3((unsigned)grid_for(2 * (w1 - w0))), dim3(kBlock), 0, ss, w0, w1, n,
                            d_midx, (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
                            d_status, win, list + i0, cnt + k);
       });
     else
-      rc = timed("rlc_window", ss, [&] {
+      rc = timed(c, "rlc_window", ss, [&] {
         hipLaunchKernelGGL(k_rlc_window, dim3((unsigned)grid_for(w1 - w0)), dim3(kBlock), 0, ss, w0, w1, n, d_midx,
                            (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
                            d_status, win, list + i0, cnt + k);
@@ -378,13 +583,13 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
     // The list length is only known on the device: launch for the worst case, idle lanes exit.  The list is short
     // (failed windows only) and latency-bound, so lane pairs unless the caller forced single lanes.
     if (g_pair_mode.load() != HIPBLS_PAIR_SINGLE)
-      rc = timed("rlc_fallback_lg2", ss, [&] {
+      rc = timed(c, "rlc_fallback_lg2", ss, [&] {
         hipLaunchKernelGGL(k_rlc_fallback_lg2, dim3((unsigned)grid_for(2 * (i1 - i0))), dim3(kBlock), 0, ss,
                            (const uint32_t*)(list + i0), (const uint32_t*)(cnt + k), i1 - i0, d_pks, d_sigs, d_midx,
                            (const uint32_t*)d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
       });
     else
-      rc = timed("rlc_fallback", ss, [&] {
+      rc = timed(c, "rlc_fallback", ss, [&] {
         hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(i1 - i0)), dim3(kBlock), 0, ss,
                            (const uint32_t*)(list + i0), (const uint32_t*)(cnt + k), i1 - i0, d_pks, d_sigs, d_midx,
                            (const uint32_t*)d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
@@ -394,26 +599,27 @@ int launch_rlc(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_mi
     HIP_TRY(hipStreamWaitEvent(s, c.ev_join[k], 0));
   }
   c.r_windows = n_win;
-  return ws_end(s);
+  return ws_end(c, s);
 }
 
 // ============================================================================ batch-wide RLC check (rlcb.h)
 // Policy (hipbls_rlc_set_mode): WINDOWS = rlc.h only; BATCH = the batch-wide check first, windows for whatever it
-// leaves pending; AUTO (default) = BATCH for batches of >= 1,024 items unless the last batch check failed, in
-// which case the next 8 calls run windows only (a cluster that sends invalid partials keeps sending them; one
-// whose batches pass keeps the cheap path).  The verdict comes back asynchronously (pinned copy + event), so the
-// policy never blocks a launch.
+// leaves pending; AUTO (default) = BATCH for batches of >= 1,024 items unless the last batch check of this context
+// failed, in which case its next 8 calls run windows only (a cluster that sends invalid partials keeps sending
+// them; one whose batches pass keeps the cheap path).  The verdict comes back asynchronously (pinned copy +
+// event), so the policy never blocks a launch.
 std::atomic<int> g_rlc_mode{HIPBLS_RLC_AUTO};
 constexpr uint64_t kRlcbMinItems = 1024;
 constexpr int kRlcbBackoff = 8;
 
 // Reads back every verdict whose copy has landed; with wait_slot >= 0 (or wait_all) blocks on that slot first.
-void rlcb_poll(int wait_slot, bool wait_all = false) {
-  Context& c = g_ctx;
+// A failed wait on wait_slot is an error: the slot is about to be reused and its verdict would be lost.
+int rlcb_poll(Context& c, int wait_slot, bool wait_all = false) {
   for (int k = 0; k < Context::kRlcbSlots; ++k) {
     if (!c.rlcb_pending[k]) continue;
     if (wait_all || k == wait_slot) {
-      if (hipEventSynchronize(c.rlcb_ev[k]) != hipSuccess) continue;
+      const hipError_t e = hipEventSynchronize(c.rlcb_ev[k]);
+      if (e != hipSuccess) return set_err("hipEventSynchronize (batch-check verdict)", e);
     } else if (hipEventQuery(c.rlcb_ev[k]) != hipSuccess) {
       continue;
     }
@@ -423,17 +629,18 @@ void rlcb_poll(int wait_slot, bool wait_all = false) {
     if (c.rlcb_seq[k] >= c.rlcb_last_seq) {
       c.rlcb_last_seq = c.rlcb_seq[k];
       c.rlcb_last = v;
+      c.rlcb_last_call = c.rlcb_call[k];
       if (!v) c.rlcb_skipped = 0;
     }
   }
+  return HIPBLS_OK;
 }
 
-bool use_rlc_batch(uint64_t n) {
-  Context& c = g_ctx;
+bool use_rlc_batch(Context& c, uint64_t n) {
   const int mode = g_rlc_mode.load();
   if (mode == HIPBLS_RLC_WINDOWS) return false;
   if (mode == HIPBLS_RLC_BATCH) return true;
-  rlcb_poll(-1);
+  (void)rlcb_poll(c, -1);
   if (n < kRlcbMinItems) return false;
   if (c.rlcb_last == 0 && c.rlcb_skipped < kRlcbBackoff) {
     ++c.rlcb_skipped;
@@ -444,11 +651,10 @@ bool use_rlc_batch(uint64_t n) {
 
 // Stages 1-6 of rlcb.h on stream s, then the window/fallback stages of rlc.h for the items still pending (none
 // when the batch check passed: those kernels then find nothing to do).  Shares launch_rlc's H(m) table setup.
-int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n,
+int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx, uint64_t n,
                      const uint8_t* d_msgs, const uint64_t* d_offs, uint64_t n_msgs, const rlc_seed& seed,
                      int32_t* d_status, hipStream_t s, const uint32_t* d_kidx, uint32_t* d_H, uint64_t hstride,
                      const uint32_t* d_hslot, const uint32_t* d_mlist, uint64_t n_hash) {
-  Context& c = g_ctx;
   const uint64_t T = c.t_size;
   const int32_t* tcode = (const int32_t*)c.t_code.p;
   const uint32_t* tab = (const uint32_t*)c.t_tab.p;
@@ -461,10 +667,11 @@ int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_items, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_msm, hipEventDisableTiming));
   }
-  int rc = ensure_rlc_streams();
+  int rc = ensure_rlc_streams(c);
   if (rc) return rc;
   const int slot = (int)(c.rlcb_next_seq % Context::kRlcbSlots);
-  rlcb_poll(slot);  // only blocks when kRlcbSlots verdicts are still in flight
+  rc = rlcb_poll(c, slot);  // only blocks when kRlcbSlots verdicts are still in flight
+  if (rc) return rc;
   HIP_TRY(c.m_pts.ensure(npts * 48 * 4));
   HIP_TRY(c.m_sc.ensure(npts * 4));
   HIP_TRY(c.m_cnt.ensure((uint64_t)MSM_WINDOWS * MSM_NB * 4));
@@ -487,13 +694,13 @@ int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t
   // sub[1] runs the chunk Miller loops and their product once the items and the hash are done; s joins both for
   // the verdict and the window stages.
   hipStream_t s0 = c.sub[0], s1 = c.sub[1];
-  rc = ws_begin(s);
+  rc = ws_begin(c, s);
   if (rc) return rc;
   HIP_TRY(hipMemsetAsync(c.m_cnt.p, 0, (size_t)MSM_WINDOWS * MSM_NB * 4, s));
   HIP_TRY(hipMemsetAsync(c.r_cnt.p, 0, 4, s));
   HIP_TRY(hipEventRecord(c.ev_fork, s));
   if (n_hash) {
-    rc = timed("rlc_hash", s, [&] {
+    rc = timed(c, "rlc_hash", s, [&] {
       hipLaunchKernelGGL(k_rlc_hash, dim3((unsigned)grid_for(n_hash)), dim3(kBlock), 0, s, d_msgs, d_offs, n_hash,
                          d_mlist, d_H, hstride, d_hslot);
     });
@@ -501,13 +708,13 @@ int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t
   }
   HIP_TRY(hipEventRecord(c.ev_hash, s));
   HIP_TRY(hipStreamWaitEvent(s0, c.ev_fork, 0));
-  rc = timed("rlcb_items", s0, [&] {
+  rc = timed(c, "rlcb_items", s0, [&] {
     hipLaunchKernelGGL(k_rlcb_items, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s0, n, d_pks, d_sigs, d_midx, n_msgs,
                        seed, rpk, pts, sc, d_status, d_kidx, T, tcode, tab);
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.rlcb_ev_items, s0));
-  rc = timed("rlcb_msm", s0, [&] {
+  rc = timed(c, "rlcb_msm", s0, [&] {
     hipStream_t s = s0;
     const unsigned g256 = (unsigned)((npts + 255) / 256);
     hipLaunchKernelGGL(k_msm_hist, dim3(g256), dim3(256), 0, s, npts, (const uint32_t*)sc, (uint32_t*)c.m_cnt.p);
@@ -524,14 +731,14 @@ int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t
                        (uint32_t*)c.m_W.p);
   });
   if (rc) return rc;
-  rc = timed("rlcb_sfactor", s0, [&] {
+  rc = timed(c, "rlcb_sfactor", s0, [&] {
     hipLaunchKernelGGL(k_rlcb_sfactor, dim3(1), dim3(kBlock), 0, s0, (const uint32_t*)c.m_W.p, (uint32_t*)c.m_FS.p);
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.rlcb_ev_msm, s0));
   HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_items, 0));
   HIP_TRY(hipStreamWaitEvent(s1, c.ev_hash, 0));
-  rc = timed("rlcb_chunks", s1, [&] {
+  rc = timed(c, "rlcb_chunks", s1, [&] {
     hipLaunchKernelGGL(k_rlcb_chunks, dim3((unsigned)grid_for(nch)), dim3(kBlock), 0, s1, n, (const int32_t*)d_status,
                        d_midx, (const uint32_t*)rpk, (const uint32_t*)d_H, hstride, d_hslot, (uint32_t*)c.m_F.p, nch);
   });
@@ -539,7 +746,7 @@ int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t
   uint32_t* src = (uint32_t*)c.m_F.p;
   uint32_t* dst = (uint32_t*)c.m_F2.p;
   uint64_t cur = nch;
-  rc = timed("rlcb_product", s1, [&] {
+  rc = timed(c, "rlcb_product", s1, [&] {
     while (cur > 1) {
       const uint64_t nxt = (cur + 15) / 16;
       hipLaunchKernelGGL(k_fp12_prod, dim3((unsigned)grid_for(nxt)), dim3(kBlock), 0, s1, (const uint32_t*)src, cur,
@@ -554,11 +761,11 @@ int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));
   HIP_TRY(hipStreamWaitEvent(s, c.rlcb_ev_msm, 0));
   HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
-  rc = timed("rlcb_final", s, [&] {
+  rc = timed(c, "rlcb_final", s, [&] {
     hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, (const uint32_t*)c.m_FS.p, flag);
   });
   if (rc) return rc;
-  rc = timed("rlcb_mark", s, [&] {
+  rc = timed(c, "rlcb_mark", s, [&] {
     hipLaunchKernelGGL(k_rlcb_mark, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, n, (const int32_t*)flag, d_status,
                        (const uint32_t*)pts, (const uint32_t*)sc, rsig);
   });
@@ -567,72 +774,71 @@ int launch_rlc_batch(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t
   HIP_TRY(hipEventRecord(c.rlcb_ev[slot], s));
   c.rlcb_pending[slot] = true;
   c.rlcb_seq[slot] = ++c.rlcb_next_seq;
+  c.rlcb_call[slot] = c.r_call;
   c.rlcb_attempted += 1;
   // window + fallback stages over whatever is still pending (nothing when the batch check passed)
   int32_t* win = (int32_t*)c.r_win.p;
   uint32_t* list = (uint32_t*)c.r_list.p;
   uint32_t* cnt = (uint32_t*)c.r_cnt.p;
   if (use_pairs(n_win, kLg2MaxWindows))
-    rc = timed("rlc_window_lg2", s, [&] {
+    rc = timed(c, "rlc_window_lg2", s, [&] {
       hipLaunchKernelGGL(k_rlc_window_lg2, dim3((unsigned)grid_for(2 * n_win)), dim3(kBlock), 0, s, (uint64_t)0, n_win,
                          n, d_midx, (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
                          d_status, win, list, cnt);
     });
   else
-    rc = timed("rlc_window", s, [&] {
+    rc = timed(c, "rlc_window", s, [&] {
       hipLaunchKernelGGL(k_rlc_window, dim3((unsigned)grid_for(n_win)), dim3(kBlock), 0, s, (uint64_t)0, n_win, n,
                          d_midx, (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
                          d_status, win, list, cnt);
     });
   if (rc) return rc;
   if (g_pair_mode.load() != HIPBLS_PAIR_SINGLE)
-    rc = timed("rlc_fallback_lg2", s, [&] {
+    rc = timed(c, "rlc_fallback_lg2", s, [&] {
       hipLaunchKernelGGL(k_rlc_fallback_lg2, dim3((unsigned)grid_for(2 * n)), dim3(kBlock), 0, s,
                          (const uint32_t*)list, (const uint32_t*)cnt, n, d_pks, d_sigs, d_midx, (const uint32_t*)d_H,
                          hstride, d_hslot, d_status, d_kidx, T, tab);
     });
   else
-    rc = timed("rlc_fallback", s, [&] {
+    rc = timed(c, "rlc_fallback", s, [&] {
       hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, (const uint32_t*)list,
                          (const uint32_t*)cnt, n, d_pks, d_sigs, d_midx, (const uint32_t*)d_H, hstride, d_hslot,
                          d_status, d_kidx, T, tab);
     });
   if (rc) return rc;
   c.r_windows = n_win;
-  return ws_end(s);
+  return ws_end(c, s);
 }
 
-int launch_tagg(const uint8_t* d_sigs, const int64_t* d_ids, const uint64_t* d_goffs, uint64_t n_groups,
+int launch_tagg(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, const uint64_t* d_goffs, uint64_t n_groups,
                 uint64_t n_parts, uint8_t* d_out, int32_t* d_status, hipStream_t s) {
   if (n_groups == 0) return HIPBLS_OK;
-  HIP_TRY(g_ctx.b_pts.ensure((n_parts ? n_parts : 1) * 72 * 4));
-  HIP_TRY(g_ctx.b_pst.ensure((n_parts ? n_parts : 1) * 4));
-  int rc = ws_begin(s);
+  HIP_TRY(c.b_pts.ensure((n_parts ? n_parts : 1) * 72 * 4));
+  HIP_TRY(c.b_pst.ensure((n_parts ? n_parts : 1) * 4));
+  int rc = ws_begin(c, s);
   if (rc) return rc;
   if (n_parts) {
-    rc = timed("tagg_scale", s, [&] {
+    rc = timed(c, "tagg_scale", s, [&] {
       hipLaunchKernelGGL(k_tagg_scale, dim3((unsigned)grid_for(n_parts)), dim3(kBlock), 0, s, d_sigs, d_ids, d_goffs,
-                         n_groups, n_parts, (uint32_t*)g_ctx.b_pts.p, (int32_t*)g_ctx.b_pst.p);
+                         n_groups, n_parts, (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);
     });
     if (rc) return rc;
   }
-  rc = timed("tagg_sum", s, [&] {
-    hipLaunchKernelGGL(k_tagg_sum, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s,
-                       (const uint32_t*)g_ctx.b_pts.p, (const int32_t*)g_ctx.b_pst.p, d_goffs, n_groups, n_parts, d_out,
-                       d_status);
+  rc = timed(c, "tagg_sum", s, [&] {
+    hipLaunchKernelGGL(k_tagg_sum, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s, (const uint32_t*)c.b_pts.p,
+                       (const int32_t*)c.b_pst.p, d_goffs, n_groups, n_parts, d_out, d_status);
   });
   if (rc) return rc;
-  return ws_end(s);
+  return ws_end(c, s);
 }
 
 // sigagg in one call: ThresholdAggregate on sub[0] while sub[1] decodes the validators' root keys and hashes their
 // messages; the caller's stream joins both and runs the pairing checks on the aggregates (kernels.h, k_tagg_sum_v).
-int launch_tagg_verify(const uint8_t* d_sigs, const int64_t* d_ids, const uint64_t* d_goffs, uint64_t n_groups,
-                       uint64_t n_parts, const uint8_t* d_dvpks, const uint8_t* d_msgs, const uint64_t* d_moffs,
-                       uint8_t* d_out, int32_t* d_astatus, int32_t* d_vstatus, hipStream_t s) {
-  Context& c = g_ctx;
+int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, const uint64_t* d_goffs,
+                       uint64_t n_groups, uint64_t n_parts, const uint8_t* d_dvpks, const uint8_t* d_msgs,
+                       const uint64_t* d_moffs, uint8_t* d_out, int32_t* d_astatus, int32_t* d_vstatus, hipStream_t s) {
   if (n_groups == 0) return HIPBLS_OK;
-  int rc = ensure_rlc_streams();
+  int rc = ensure_rlc_streams(c);
   if (rc) return rc;
   HIP_TRY(c.b_pts.ensure((n_parts ? n_parts : 1) * 72 * 4));
   HIP_TRY(c.b_pst.ensure((n_parts ? n_parts : 1) * 4));
@@ -641,26 +847,26 @@ int launch_tagg_verify(const uint8_t* d_sigs, const int64_t* d_ids, const uint64
   uint32_t* ws = (uint32_t*)c.v_ws.p;
   int32_t* agg_inf = (int32_t*)c.b_aux.p;
   hipStream_t s0 = c.sub[0], s1 = c.sub[1];
-  rc = ws_begin(s);
+  rc = ws_begin(c, s);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(s0, c.ev_fork, 0));
   HIP_TRY(hipStreamWaitEvent(s1, c.ev_fork, 0));
   if (n_parts) {
-    rc = timed("tagg_scale", s0, [&] {
+    rc = timed(c, "tagg_scale", s0, [&] {
       hipLaunchKernelGGL(k_tagg_scale, dim3((unsigned)grid_for(n_parts)), dim3(kBlock), 0, s0, d_sigs, d_ids, d_goffs,
                          n_groups, n_parts, (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);
     });
     if (rc) return rc;
   }
-  rc = timed("tagg_sum", s0, [&] {
+  rc = timed(c, "tagg_sum", s0, [&] {
     hipLaunchKernelGGL(k_tagg_sum_v, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s0,
                        (const uint32_t*)c.b_pts.p, (const int32_t*)c.b_pst.p, d_goffs, n_groups, n_parts, d_out,
                        d_astatus, ws, agg_inf);
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_join[0], s0));
-  rc = timed("tv_prep_pk", s1, [&] {
+  rc = timed(c, "tv_prep_pk", s1, [&] {
     hipLaunchKernelGGL(k_tv_prep_pk, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s1, d_dvpks, d_msgs, d_moffs,
                        n_groups, ws, d_vstatus);
   });
@@ -672,41 +878,40 @@ int launch_tagg_verify(const uint8_t* d_sigs, const int64_t* d_ids, const uint64
                      (const int32_t*)d_astatus, (const int32_t*)agg_inf, d_vstatus);
   HIP_TRY(hipGetLastError());
   if (use_pairs(n_groups, kLg2MaxVerify))
-    rc = timed("verify_pair_lg2", s, [&] {
+    rc = timed(c, "verify_pair_lg2", s, [&] {
       hipLaunchKernelGGL(k_verify_pair_lg2, dim3((unsigned)grid_for(2 * n_groups)), dim3(kBlock), 0, s,
                          (const uint32_t*)ws, n_groups, d_vstatus);
     });
   else
-    rc = timed("verify_pair_single", s, [&] {
+    rc = timed(c, "verify_pair_single", s, [&] {
       hipLaunchKernelGGL(k_verify_pair_single, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s,
                          (const uint32_t*)ws, n_groups, d_vstatus);
     });
   if (rc) return rc;
-  return ws_end(s);
+  return ws_end(c, s);
 }
 
-int launch_fav(const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_goff, uint64_t n_groups, const uint8_t* d_sigs,
-               const uint8_t* d_msgs, const uint64_t* d_moffs, int32_t* d_status, hipStream_t s) {
-  Context& c = g_ctx;
+int launch_fav(Context& c, const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_goff, uint64_t n_groups,
+               const uint8_t* d_sigs, const uint8_t* d_msgs, const uint64_t* d_moffs, int32_t* d_status,
+               hipStream_t s) {
   if (n_groups == 0) return HIPBLS_OK;
   HIP_TRY(c.b_pts.ensure((nkeys ? nkeys : 1) * 24 * 4));
   HIP_TRY(c.b_pst.ensure((nkeys ? nkeys : 1) * 4));
-  int rc = ws_begin(s);
+  int rc = ws_begin(c, s);
   if (rc) return rc;
   if (nkeys)
     hipLaunchKernelGGL(k_g1_decode, dim3((unsigned)grid_for(nkeys)), dim3(kBlock), 0, s, d_pks, nkeys,
                        (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);
-  rc = timed("fav", s, [&] {
+  rc = timed(c, "fav", s, [&] {
     hipLaunchKernelGGL(k_fav_batch, dim3((unsigned)n_groups), dim3(kFavBlock), 0, s, (const uint32_t*)c.b_pts.p,
                        (const int32_t*)c.b_pst.p, nkeys, d_goff, d_sigs, d_msgs, d_moffs, d_status);
   });
   if (rc) return rc;
-  return ws_end(s);
+  return ws_end(c, s);
 }
 
 // Aggregate: decode in parallel, per-workgroup partial sums, one final workgroup (kernels.h).
-int launch_aggregate(const uint8_t* d_sigs, uint64_t n, uint8_t* d_out, int32_t* d_status, hipStream_t s) {
-  Context& c = g_ctx;
+int launch_aggregate(Context& c, const uint8_t* d_sigs, uint64_t n, uint8_t* d_out, int32_t* d_status, hipStream_t s) {
   const uint64_t per_wg = 8 * (uint64_t)kSumBlock;  // points folded per lane before the tree
   uint64_t nwg = (n + per_wg - 1) / per_wg;
   if (nwg < 1) nwg = 1;
@@ -715,7 +920,7 @@ int launch_aggregate(const uint8_t* d_sigs, uint64_t n, uint8_t* d_out, int32_t*
   HIP_TRY(c.b_pst.ensure((n ? n : 1) * 4));
   HIP_TRY(c.b_part.ensure(nwg * 72 * 4));
   HIP_TRY(c.b_bad.ensure(4));
-  int rc = ws_begin(s);
+  int rc = ws_begin(c, s);
   if (rc) return rc;
   HIP_TRY(hipMemsetAsync(c.b_bad.p, 0, 4, s));
   if (n)
@@ -726,7 +931,7 @@ int launch_aggregate(const uint8_t* d_sigs, uint64_t n, uint8_t* d_out, int32_t*
   hipLaunchKernelGGL(k_g2_sum_final, dim3(1), dim3(kSumBlock), 0, s, (const uint32_t*)c.b_part.p, nwg,
                      (const int32_t*)c.b_bad.p, d_out, d_status);
   HIP_TRY(hipGetLastError());
-  return ws_end(s);
+  return ws_end(c, s);
 }
 
 bool mul_overflows(uint64_t a, uint64_t b) { return b != 0 && a > UINT64_MAX / b; }
@@ -738,142 +943,11 @@ bool offsets_ok(const uint64_t* offs, uint64_t n) {
   return true;
 }
 
-// ============================================================================ submission queue
-// Coalesces concurrent single-item Verify calls (tbls.Verify from parsigex / validatorapi / sigagg goroutines,
-// core/parsigex/parsigex.go:86-91, core/validatorapi/validatorapi.go:246-283) into batched launches.  A batch
-// is launched as soon as the worker is free and work is pending: while one batch runs on the GPU, arrivals
-// accumulate into the next, so the batch size follows the offered load.  An idle worker waits gather_us for
-// company before launching a small batch.  The worker owns its stream and buffers; callers block only on their
-// own batch's completion, never on a lock held across GPU work.
-struct VBatch {
-  std::vector<uint8_t> pk, sig, msg;
-  std::vector<uint64_t> off{0};
-  std::vector<int32_t> status;
-  int rc = HIPBLS_OK;
-  bool done = false;
-  uint64_t n() const { return off.size() - 1; }
-};
-
-struct VerifyQueue {
-  std::mutex mu;
-  std::condition_variable cv_work, cv_done;
-  std::deque<std::shared_ptr<VBatch>> open;  // accepting (back) / waiting for the worker (front)
-  std::unordered_map<uint64_t, std::pair<std::shared_ptr<VBatch>, uint32_t>> tickets;
-  uint64_t next_ticket = 1;
-  std::thread worker;
-  bool started = false, stop = false;
-  uint64_t max_batch = 65536;
-  uint32_t gather_us = 200;
-  uint64_t batches = 0, items = 0;
-  hipStream_t stream = nullptr;
-  DevBuf d_pk, d_sig, d_msg, d_off, d_st, d_ws;
-};
-VerifyQueue g_q;
-
-int run_batch(VBatch& b) {
-  VerifyQueue& q = g_q;
-  const uint64_t n = b.n();
-  b.status.assign(n, HIPBLS_ERR_DEVICE);
-  HIP_TRY(q.d_pk.ensure(n * 48));
-  HIP_TRY(q.d_sig.ensure(n * 96));
-  HIP_TRY(q.d_msg.ensure(b.msg.size() ? b.msg.size() : 1));
-  HIP_TRY(q.d_off.ensure((n + 1) * 8));
-  HIP_TRY(q.d_st.ensure(n * 4));
-  HIP_TRY(hipMemcpyAsync(q.d_pk.p, b.pk.data(), n * 48, hipMemcpyHostToDevice, q.stream));
-  HIP_TRY(hipMemcpyAsync(q.d_sig.p, b.sig.data(), n * 96, hipMemcpyHostToDevice, q.stream));
-  if (b.msg.size()) HIP_TRY(hipMemcpyAsync(q.d_msg.p, b.msg.data(), b.msg.size(), hipMemcpyHostToDevice, q.stream));
-  HIP_TRY(hipMemcpyAsync(q.d_off.p, b.off.data(), (n + 1) * 8, hipMemcpyHostToDevice, q.stream));
-  int rc = launch_verify((const uint8_t*)q.d_pk.p, (const uint8_t*)q.d_msg.p, (const uint64_t*)q.d_off.p,
-                         (const uint8_t*)q.d_sig.p, n, (int32_t*)q.d_st.p, q.stream, q.d_ws);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(b.status.data(), q.d_st.p, n * 4, hipMemcpyDeviceToHost, q.stream));
-  HIP_TRY(hipStreamSynchronize(q.stream));
-  return HIPBLS_OK;
-}
-
-void queue_worker() {
-  VerifyQueue& q = g_q;
-  const bool dev_ok = hipSetDevice(g_ctx.device) == hipSuccess &&
-                      hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) == hipSuccess;
-  std::unique_lock<std::mutex> lk(q.mu);
-  for (;;) {
-    q.cv_work.wait(lk, [&] { return q.stop || (!q.open.empty() && q.open.front()->n() > 0); });
-    if (q.open.empty() || q.open.front()->n() == 0) break;  // stop requested and nothing pending
-    if (q.gather_us && q.open.front()->n() < q.max_batch && !q.stop) {
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(q.gather_us);
-      q.cv_work.wait_until(lk, until, [&] { return q.stop || q.open.front()->n() >= q.max_batch; });
-    }
-    std::shared_ptr<VBatch> b = q.open.front();
-    q.open.pop_front();
-    lk.unlock();
-    const int rc = dev_ok ? run_batch(*b) : HIPBLS_ERR_DEVICE;
-    lk.lock();
-    b->rc = rc;
-    b->done = true;
-    q.batches += 1;
-    q.items += b->n();
-    q.cv_done.notify_all();
-  }
-}
-
-void queue_shutdown() {
-  {
-    std::lock_guard<std::mutex> lk(g_q.mu);
-    if (!g_q.started) return;
-    g_q.stop = true;
-  }
-  g_q.cv_work.notify_all();
-  if (g_q.worker.joinable()) g_q.worker.join();
-  std::lock_guard<std::mutex> lk(g_q.mu);
-  g_q.started = false;
-  g_q.stop = false;
-}
-
-int queue_submit(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, const uint8_t* sig96, uint64_t* ticket) {
-  if (!pk48 || !sig96 || !ticket || (msg_len && !msg) || msg_len > 0xffffffffull) return arg_err("bad verify arguments");
-  int rc = bind_device();
-  if (rc) return rc;
-  VerifyQueue& q = g_q;
-  std::lock_guard<std::mutex> lk(q.mu);
-  if (!q.started) {
-    q.worker = std::thread(queue_worker);
-    q.started = true;
-    static bool hooked = false;
-    if (!hooked) {
-      hooked = true;
-      atexit(queue_shutdown);  // drain the in-flight batch before the HIP runtime tears down
-    }
-  }
-  if (q.open.empty() || q.open.back()->n() >= q.max_batch) q.open.push_back(std::make_shared<VBatch>());
-  VBatch& b = *q.open.back();
-  const uint32_t idx = (uint32_t)b.n();
-  b.pk.insert(b.pk.end(), pk48, pk48 + 48);
-  b.sig.insert(b.sig.end(), sig96, sig96 + 96);
-  if (msg_len) b.msg.insert(b.msg.end(), msg, msg + msg_len);
-  b.off.push_back(b.msg.size());
-  const uint64_t t = q.next_ticket++;
-  q.tickets.emplace(t, std::make_pair(q.open.back(), idx));
-  *ticket = t;
-  q.cv_work.notify_one();
-  return HIPBLS_OK;
-}
-
-int queue_wait(uint64_t ticket, int32_t* status) {
-  if (!status) return arg_err("null status");
-  VerifyQueue& q = g_q;
-  std::unique_lock<std::mutex> lk(q.mu);
-  auto it = q.tickets.find(ticket);
-  if (it == q.tickets.end()) return arg_err("unknown verify ticket");
-  std::shared_ptr<VBatch> b = it->second.first;
-  const uint32_t idx = it->second.second;
-  q.tickets.erase(it);
-  q.cv_done.wait(lk, [&] { return b->done; });
-  if (b->rc) {
-    g_last_error = "verify queue batch failed on the device";
-    return b->rc;
-  }
-  *status = b->status[idx];
-  return HIPBLS_OK;
+bool groups_ok(const uint64_t* goffs, uint64_t n_groups) {
+  if (goffs[0] != 0) return false;
+  for (uint64_t g = 0; g < n_groups; ++g)
+    if (goffs[g + 1] < goffs[g]) return false;
+  return true;
 }
 
 // ============================================================================ H(m) cache
@@ -925,50 +999,554 @@ bool hcache_assign(HCache& hc, const uint8_t* msgs, const uint64_t* offs, uint64
   return true;
 }
 
-// Host-buffer RLC body shared by the wire-format and key-table calls (context lock held).
-int rlc_host(const uint8_t* pks, const uint32_t* key_idx, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
-             const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs, const uint8_t* seed32, int32_t* status) {
-  Context& c = g_ctx;
+// Host-buffer RLC body shared by the wire-format and key-table calls, on one context (lock held), stream `s` with
+// the given workspaces for the inputs.  The H(m) table is the context's cache when enabled, else per call.
+struct RlcBufs {
+  DevBuf *pk, *kidx, *sig, *midx, *msg, *off, *st, *slot, *mlist;
+};
+int rlc_host_on(Context& c, RlcBufs B, hipStream_t s, const uint8_t* pks, const uint32_t* key_idx, const uint8_t* sigs,
+                const uint32_t* msg_idx, uint64_t n, const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs,
+                const rlc_seed& seed, int32_t* status, uint64_t call) {
   const uint64_t msg_total = msg_offsets[n_msgs];
-  if (pks) HIP_TRY(c.b_pk.ensure(n * 48));
-  if (key_idx) HIP_TRY(c.b_kidx.ensure(n * 4));
-  HIP_TRY(c.b_sig.ensure(n * 96));
-  HIP_TRY(c.r_midx.ensure(n * 4));
-  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
-  HIP_TRY(c.b_off.ensure((n_msgs + 1) * 8));
-  HIP_TRY(c.b_st.ensure(n * 4));
-  if (pks) HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
-  if (key_idx) HIP_TRY(hipMemcpyAsync(c.b_kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.r_midx.p, msg_idx, n * 4, hipMemcpyHostToDevice, c.stream));
-  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n_msgs + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  if (pks) HIP_TRY(B.pk->ensure(n * 48));
+  if (key_idx) HIP_TRY(B.kidx->ensure(n * 4));
+  HIP_TRY(B.sig->ensure(n * 96));
+  HIP_TRY(B.midx->ensure(n * 4));
+  HIP_TRY(B.msg->ensure(msg_total ? msg_total : 1));
+  HIP_TRY(B.off->ensure((n_msgs + 1) * 8));
+  HIP_TRY(B.st->ensure(n * 4));
+  if (pks) HIP_TRY(hipMemcpyAsync(B.pk->p, pks, n * 48, hipMemcpyHostToDevice, s));
+  if (key_idx) HIP_TRY(hipMemcpyAsync(B.kidx->p, key_idx, n * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(B.sig->p, sigs, n * 96, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(B.midx->p, msg_idx, n * 4, hipMemcpyHostToDevice, s));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(B.msg->p, msgs, msg_total, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(B.off->p, msg_offsets, (n_msgs + 1) * 8, hipMemcpyHostToDevice, s));
   std::vector<uint32_t> slot, miss;
   uint32_t* dH = nullptr;
   const uint32_t *dslot = nullptr, *dmiss = nullptr;
   uint64_t stride = 0, n_hash = 0;
   if (hcache_assign(c.hcache, msgs, msg_offsets, n_msgs, slot, miss)) {
-    HIP_TRY(c.r_slot.ensure((n_msgs ? n_msgs : 1) * 4));
-    HIP_TRY(c.r_mlist.ensure((miss.size() ? miss.size() : 1) * 4));
-    // the copies run on the library stream behind every earlier workspace user (ws_done)
-    int rc = ws_begin(c.stream);
+    HIP_TRY(B.slot->ensure((n_msgs ? n_msgs : 1) * 4));
+    HIP_TRY(B.mlist->ensure((miss.size() ? miss.size() : 1) * 4));
+    // the copies run on s behind every earlier workspace user (ws_done): the slot table is per call
+    int rc = ws_begin(c, s);
     if (rc) return rc;
-    if (n_msgs) HIP_TRY(hipMemcpyAsync(c.r_slot.p, slot.data(), n_msgs * 4, hipMemcpyHostToDevice, c.stream));
-    if (miss.size()) HIP_TRY(hipMemcpyAsync(c.r_mlist.p, miss.data(), miss.size() * 4, hipMemcpyHostToDevice, c.stream));
+    if (n_msgs) HIP_TRY(hipMemcpyAsync(B.slot->p, slot.data(), n_msgs * 4, hipMemcpyHostToDevice, s));
+    if (miss.size()) HIP_TRY(hipMemcpyAsync(B.mlist->p, miss.data(), miss.size() * 4, hipMemcpyHostToDevice, s));
     dH = (uint32_t*)c.hcache.table.p;
     stride = c.hcache.cap;
-    dslot = (const uint32_t*)c.r_slot.p;
-    dmiss = (const uint32_t*)c.r_mlist.p;
+    dslot = (const uint32_t*)B.slot->p;
+    dmiss = (const uint32_t*)B.mlist->p;
     n_hash = miss.size();
   }
-  int rc = launch_rlc(pks ? (const uint8_t*)c.b_pk.p : nullptr, (const uint8_t*)c.b_sig.p, (const uint32_t*)c.r_midx.p,
-                      n, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p, n_msgs, seed32, (int32_t*)c.b_st.p,
-                      c.stream, key_idx ? (const uint32_t*)c.b_kidx.p : nullptr, dH, stride, dslot, dmiss, n_hash);
+  int rc = launch_rlc(c, pks ? (const uint8_t*)B.pk->p : nullptr, (const uint8_t*)B.sig->p, (const uint32_t*)B.midx->p,
+                      n, (const uint8_t*)B.msg->p, (const uint64_t*)B.off->p, n_msgs, seed, (int32_t*)B.st->p, s, call,
+                      key_idx ? (const uint32_t*)B.kidx->p : nullptr, dH, stride, dslot, dmiss, n_hash);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(status, B.st->p, n * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return HIPBLS_OK;
+}
+
+int rlc_host(Context& c, const uint8_t* pks, const uint32_t* key_idx, const uint8_t* sigs, const uint32_t* msg_idx,
+             uint64_t n, const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs, const rlc_seed& seed,
+             int32_t* status, uint64_t call) {
+  RlcBufs B{&c.b_pk, &c.b_kidx, &c.b_sig, &c.r_midx, &c.b_msg, &c.b_off, &c.b_st, &c.r_slot, &c.r_mlist};
+  return rlc_host_on(c, B, c.stream, pks, key_idx, sigs, msg_idx, n, msgs, msg_offsets, n_msgs, seed, status, call);
+}
+
+// An RLC call over items [lo, hi) of a larger batch: the range's own message table (the messages its items use,
+// renumbered in first-use order) and its own scalars (the seed's last word is mixed with the range start, so two
+// ranges never share scalar streams).
+int rlc_range(Context& c, const uint8_t* pks, const uint32_t* key_idx, const uint8_t* sigs, const uint32_t* msg_idx,
+              uint64_t lo, uint64_t hi, const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs,
+              const uint8_t* seed32, int32_t* status, uint64_t call, bool whole) {
+  rlc_seed seed = parse_seed(seed32);
+  if (whole)
+    return rlc_host(c, pks, key_idx, sigs, msg_idx, hi - lo, msgs, msg_offsets, n_msgs, seed, status, call);
+  seed.w[7] ^= (uint32_t)lo;
+  seed.w[6] ^= (uint32_t)(lo >> 32);
+  const uint64_t n = hi - lo;
+  std::vector<uint32_t> lmidx(n), remap;
+  std::unordered_map<uint32_t, uint32_t> sparse;
+  const bool dense = n_msgs <= 4 * n + 1024;
+  if (dense) remap.assign(n_msgs, UINT32_MAX);
+  std::vector<uint32_t> used;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t m = msg_idx[lo + i];
+    uint32_t l;
+    if (dense) {
+      if (remap[m] == UINT32_MAX) {
+        remap[m] = (uint32_t)used.size();
+        used.push_back(m);
+      }
+      l = remap[m];
+    } else {
+      auto it = sparse.find(m);
+      if (it == sparse.end()) {
+        it = sparse.emplace(m, (uint32_t)used.size()).first;
+        used.push_back(m);
+      }
+      l = it->second;
+    }
+    lmidx[i] = l;
+  }
+  std::vector<uint64_t> loff(used.size() + 1);
+  uint64_t tot = 0;
+  for (size_t k = 0; k < used.size(); ++k) {
+    loff[k] = tot;
+    tot += msg_offsets[used[k] + 1] - msg_offsets[used[k]];
+  }
+  loff[used.size()] = tot;
+  std::vector<uint8_t> lmsg(tot ? tot : 1);
+  for (size_t k = 0; k < used.size(); ++k)
+    memcpy(lmsg.data() + loff[k], msgs + msg_offsets[used[k]], loff[k + 1] - loff[k]);
+  return rlc_host(c, pks ? pks + 48 * lo : nullptr, key_idx ? key_idx + lo : nullptr, sigs + 96 * lo, lmidx.data(), n,
+                  lmsg.data(), loff.data(), used.size(), seed, status + lo, call);
+}
+
+// ============================================================================ submission queue
+// Coalesces concurrent single-item Verify calls (tbls.Verify from parsigex / validatorapi / sigagg goroutines,
+// core/parsigex/parsigex.go:86-91, core/validatorapi/validatorapi.go:246-283) into batched launches.  Each context
+// has its own queue; an item goes to the context its message hashes to, so the t partials of one signing root meet
+// on one device.  A batch is launched as soon as the worker is free and work is pending: while one batch runs on
+// the GPU, arrivals accumulate into the next, so the batch size follows the offered load.  An idle worker waits
+// gather_us for company before launching a small batch.  The worker owns its stream and buffers; callers block only
+// on their own batch's completion, never on a lock held across GPU work.
+//
+// Keyed path: when every key of a batch is in the resident pubshare table (and the batch has at
+// least kQueueKeyedMin items or the H(m) cache is enabled), the batch runs as an
+// RLC BatchVerify with keys by table index (no decode or subgroup test per call, herumi.go:286-289 does both every
+// time) over the batch's DISTINCT messages, through the context's H(m) cache: a root shared by a validator's t
+// partials or by a committee is hashed once, and once across batches while it stays cached.  Statuses are exactly
+// the per-item Verify's (rlc.h).  Batches with a key outside the table take the wire-format Verify.
+std::atomic<uint64_t> g_q_max_batch{65536};
+std::atomic<uint32_t> g_q_gather_us{200};
+constexpr uint64_t kQueueKeyedMin = 8;  // without the H(m) cache, batches below this take the lane-pair Verify
+
+int run_batch_wire(Context& c, VBatch& b) {
+  VerifyQueue& q = c.q;
+  const uint64_t n = b.n();
+  HIP_TRY(q.d_pk.ensure(n * 48));
+  HIP_TRY(q.d_sig.ensure(n * 96));
+  HIP_TRY(q.d_msg.ensure(b.msg.size() ? b.msg.size() : 1));
+  HIP_TRY(q.d_off.ensure((n + 1) * 8));
+  HIP_TRY(q.d_st.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(q.d_pk.p, b.pk.data(), n * 48, hipMemcpyHostToDevice, q.stream));
+  HIP_TRY(hipMemcpyAsync(q.d_sig.p, b.sig.data(), n * 96, hipMemcpyHostToDevice, q.stream));
+  if (b.msg.size()) HIP_TRY(hipMemcpyAsync(q.d_msg.p, b.msg.data(), b.msg.size(), hipMemcpyHostToDevice, q.stream));
+  HIP_TRY(hipMemcpyAsync(q.d_off.p, b.off.data(), (n + 1) * 8, hipMemcpyHostToDevice, q.stream));
+  int rc = launch_verify(c, (const uint8_t*)q.d_pk.p, (const uint8_t*)q.d_msg.p, (const uint64_t*)q.d_off.p,
+                         (const uint8_t*)q.d_sig.p, n, (int32_t*)q.d_st.p, q.stream, q.d_ws);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(b.status.data(), q.d_st.p, n * 4, hipMemcpyDeviceToHost, q.stream));
+  HIP_TRY(hipStreamSynchronize(q.stream));
+  return HIPBLS_OK;
+}
+
+// The keyed path, under the context lock (the table, the H(m) cache and the RLC workspaces are the context's).
+// Items are ordered by message so each message's partials are adjacent (one Miller loop per run per window).
+int run_batch_keyed(Context& c, VBatch& b) {
+  VerifyQueue& q = c.q;
+  const uint64_t n = b.n();
+  // distinct messages in first-use order
+  std::unordered_map<std::string, uint32_t> pos;
+  std::vector<uint32_t> mid(n);
+  q.umsg.clear();
+  q.uoff.assign(1, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    std::string key((const char*)b.msg.data() + b.off[i], b.off[i + 1] - b.off[i]);
+    auto it = pos.find(key);
+    if (it == pos.end()) {
+      it = pos.emplace(std::move(key), (uint32_t)(q.uoff.size() - 1)).first;
+      q.umsg.insert(q.umsg.end(), b.msg.begin() + b.off[i], b.msg.begin() + b.off[i + 1]);
+      q.uoff.push_back(q.umsg.size());
+    }
+    mid[i] = it->second;
+  }
+  const uint64_t n_msgs = q.uoff.size() - 1;
+  // counting sort by message
+  std::vector<uint64_t> start(n_msgs + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) start[mid[i] + 1] += 1;
+  for (uint64_t m = 0; m < n_msgs; ++m) start[m + 1] += start[m];
+  q.order.resize(n);
+  for (uint64_t i = 0; i < n; ++i) q.order[start[mid[i]]++] = (uint32_t)i;
+  q.kidx.resize(n);
+  q.midx.resize(n);
+  q.sig_sorted.resize(n * 96);
+  for (uint64_t j = 0; j < n; ++j) {
+    const uint32_t i = q.order[j];
+    q.kidx[j] = c.t_index.at(std::string((const char*)b.pk.data() + 48 * i, 48));
+    q.midx[j] = mid[i];
+    memcpy(q.sig_sorted.data() + 96 * j, b.sig.data() + 96 * i, 96);
+  }
+  q.st_sorted.resize(n);
+  uint8_t seed32[32];  // the RLC scalars must be unpredictable to whoever made the signatures: kernel CSPRNG
+  if (getrandom(seed32, sizeof seed32, 0) != (ssize_t)sizeof seed32) return arg_err("getrandom failed");
+  const rlc_seed seed = parse_seed(seed32);
+  RlcBufs B{&q.d_pk, &q.d_kidx, &q.d_sig, &q.d_midx, &q.d_msg, &q.d_off, &q.d_rlc_st, &q.d_slot, &q.d_mlist};
+  const int rc = rlc_host_on(c, B, q.stream, nullptr, q.kidx.data(), q.sig_sorted.data(), q.midx.data(), n,
+                             q.umsg.data(), q.uoff.data(), n_msgs, seed, q.st_sorted.data(),
+                             g_call_seq.fetch_add(1) + 1);
+  if (rc) return rc;
+  for (uint64_t j = 0; j < n; ++j) b.status[q.order[j]] = q.st_sorted[j];
+  return HIPBLS_OK;
+}
+
+int run_batch(Context& c, VBatch& b) {
+  const uint64_t n = b.n();
+  b.status.assign(n, HIPBLS_ERR_DEVICE);
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    // small batches take the lower-latency lane-pair Verify, unless the caller enabled the H(m) cache
+    bool keyed = c.t_size > 0 && (n >= kQueueKeyedMin || c.hcache.cap > 0);
+    for (uint64_t i = 0; keyed && i < n; ++i)
+      keyed = c.t_index.count(std::string((const char*)b.pk.data() + 48 * i, 48)) != 0;
+    if (keyed) {
+      c.q.keyed += 1;
+      return run_batch_keyed(c, b);
+    }
+  }
+  return run_batch_wire(c, b);
+}
+
+void queue_worker(Context* cp) {
+  Context& c = *cp;
+  VerifyQueue& q = c.q;
+  const bool dev_ok = hipSetDevice(c.device) == hipSuccess &&
+                      hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) == hipSuccess;
+  std::unique_lock<std::mutex> lk(q.mu);
+  for (;;) {
+    q.cv_work.wait(lk, [&] { return q.stop || (!q.open.empty() && q.open.front()->n() > 0); });
+    if (q.open.empty() || q.open.front()->n() == 0) break;  // stop requested and nothing pending
+    const uint64_t max_batch = g_q_max_batch.load();
+    const uint32_t gather_us = g_q_gather_us.load();
+    if (gather_us && q.open.front()->n() < max_batch && !q.stop) {
+      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(gather_us);
+      q.cv_work.wait_until(lk, until, [&] { return q.stop || q.open.front()->n() >= max_batch; });
+    }
+    std::shared_ptr<VBatch> b = q.open.front();
+    q.open.pop_front();
+    lk.unlock();
+    const int rc = dev_ok ? run_batch(c, *b) : HIPBLS_ERR_DEVICE;
+    lk.lock();
+    b->rc = rc;
+    b->done = true;
+    q.batches += 1;
+    q.items += b->n();
+    q.cv_done.notify_all();
+  }
+}
+
+void queue_shutdown() {
+  const int n = nctx();
+  for (int k = 0; k < n; ++k) {
+    VerifyQueue& q = ctx(k).q;
+    {
+      std::lock_guard<std::mutex> lk(q.mu);
+      if (!q.started) continue;
+      q.stop = true;
+    }
+    q.cv_work.notify_all();
+    if (q.worker.joinable()) q.worker.join();
+    std::lock_guard<std::mutex> lk(q.mu);
+    q.started = false;
+    q.stop = false;
+  }
+}
+
+uint32_t msg_hash(const uint8_t* msg, uint64_t len) {  // FNV-1a: the queue a message goes to
+  uint32_t h = 2166136261u;
+  for (uint64_t i = 0; i < len; ++i) h = (h ^ msg[i]) * 16777619u;
+  return h;
+}
+
+int queue_submit(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, const uint8_t* sig96, uint64_t* ticket) {
+  if (!pk48 || !sig96 || !ticket || (msg_len && !msg) || msg_len > 0xffffffffull) return arg_err("bad verify arguments");
+  ENSURE_INIT();
+  const int n = nctx();
+  Context& c = ctx(n == 1 ? 0 : (int)(msg_hash(msg, msg_len) % (uint32_t)n));
+  int rc = bind(c);
+  if (rc) return rc;
+  VerifyQueue& q = c.q;
+  std::lock_guard<std::mutex> lk(q.mu);
+  if (!q.started) {
+    q.worker = std::thread(queue_worker, &c);
+    q.started = true;
+    static std::once_flag hooked;
+    std::call_once(hooked, [] { atexit(queue_shutdown); });  // drain in-flight batches before HIP tears down
+  }
+  const uint64_t max_batch = g_q_max_batch.load();
+  if (q.open.empty() || q.open.back()->n() >= max_batch) q.open.push_back(std::make_shared<VBatch>());
+  VBatch& b = *q.open.back();
+  const uint32_t idx = (uint32_t)b.n();
+  b.pk.insert(b.pk.end(), pk48, pk48 + 48);
+  b.sig.insert(b.sig.end(), sig96, sig96 + 96);
+  if (msg_len) b.msg.insert(b.msg.end(), msg, msg + msg_len);
+  b.off.push_back(b.msg.size());
+  const uint64_t t = q.next_ticket++ * kMaxContexts + (uint64_t)c.slot;  // the ticket names its queue
+  q.tickets.emplace(t, std::make_pair(q.open.back(), idx));
+  *ticket = t;
+  q.cv_work.notify_one();
+  return HIPBLS_OK;
+}
+
+int queue_wait(uint64_t ticket, int32_t* status) {
+  if (!status) return arg_err("null status");
+  const int n = nctx();
+  const int k = (int)(ticket % kMaxContexts);
+  if (k >= n) return arg_err("unknown verify ticket");
+  VerifyQueue& q = ctx(k).q;
+  std::unique_lock<std::mutex> lk(q.mu);
+  auto it = q.tickets.find(ticket);
+  if (it == q.tickets.end()) return arg_err("unknown verify ticket");
+  std::shared_ptr<VBatch> b = it->second.first;
+  const uint32_t idx = it->second.second;
+  q.tickets.erase(it);
+  q.cv_done.wait(lk, [&] { return b->done; });
+  if (b->rc) {
+    g_last_error = "verify queue batch failed on the device";
+    return b->rc;
+  }
+  *status = b->status[idx];
+  return HIPBLS_OK;
+}
+
+// ============================================================================ host-buffer bodies (one context)
+int verify_host(Context& c, const uint8_t* pks, const uint8_t* msgs, const uint64_t* offs, const uint8_t* sigs,
+                uint64_t n, int32_t* status) {
+  const uint64_t msg_total = offs[n];
+  HIP_TRY(c.b_pk.ensure(n * 48));
+  HIP_TRY(c.b_sig.ensure(n * 96));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_off.ensure((n + 1) * 8));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, offs, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  int rc = ws_begin(c, c.stream);
+  if (rc) return rc;
+  rc = launch_verify(c, (const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p,
+                     (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p, c.stream, c.v_ws);
+  if (rc) return rc;
+  rc = ws_end(c, c.stream);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
   HIP_TRY(hipStreamSynchronize(c.stream));
   return HIPBLS_OK;
 }
+
+int signed_data_host(Context& c, const uint8_t* pks, const uint8_t* object_roots, const uint8_t* domains,
+                     const uint8_t* sigs, uint64_t n, int32_t* status) {
+  HIP_TRY(c.b_pk.ensure(n * 48));
+  HIP_TRY(c.b_sig.ensure(n * 96));
+  HIP_TRY(c.b_aux.ensure(n * 64));
+  HIP_TRY(c.b_msg.ensure(n * 32));
+  HIP_TRY(c.b_off.ensure((n + 1) * 8));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_aux.p, object_roots, n * 32, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync((uint8_t*)c.b_aux.p + n * 32, domains, n * 32, hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(k_signing_roots, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_aux.p,
+                     (const uint8_t*)c.b_aux.p + n * 32, n, (uint8_t*)c.b_msg.p, (uint64_t*)c.b_off.p);
+  HIP_TRY(hipGetLastError());
+  int rc = ws_begin(c, c.stream);
+  if (rc) return rc;
+  rc = launch_verify(c, (const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p,
+                     (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p, c.stream, c.v_ws);
+  if (rc) return rc;
+  rc = ws_end(c, c.stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_zero_sig_status, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream,
+                     (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int tagg_host(Context& c, const uint8_t* sigs, const int64_t* share_idx, const uint64_t* goffs, uint64_t n_groups,
+              uint8_t* out_sigs, int32_t* status) {
+  const uint64_t n_parts = goffs[n_groups];
+  HIP_TRY(c.b_sig.ensure((n_parts ? n_parts : 1) * 96));
+  HIP_TRY(c.b_ids.ensure((n_parts ? n_parts : 1) * 8));
+  HIP_TRY(c.b_off.ensure((n_groups + 1) * 8));
+  HIP_TRY(c.b_out.ensure(n_groups * 96));
+  HIP_TRY(c.b_st.ensure(n_groups * 4));
+  if (n_parts) {
+    HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_parts * 96, hipMemcpyHostToDevice, c.stream));
+    HIP_TRY(hipMemcpyAsync(c.b_ids.p, share_idx, n_parts * 8, hipMemcpyHostToDevice, c.stream));
+  }
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, goffs, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  int rc = launch_tagg(c, (const uint8_t*)c.b_sig.p, (const int64_t*)c.b_ids.p, (const uint64_t*)c.b_off.p, n_groups,
+                       n_parts, (uint8_t*)c.b_out.p, (int32_t*)c.b_st.p, c.stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out_sigs, c.b_out.p, n_groups * 96, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int tagg_verify_host(Context& c, const uint8_t* sigs, const int64_t* share_idx, const uint64_t* goffs,
+                     uint64_t n_groups, const uint8_t* dv_pks, const uint8_t* msgs, const uint64_t* moffs,
+                     uint8_t* out_sigs, int32_t* agg_status, int32_t* verify_status) {
+  const uint64_t n_parts = goffs[n_groups];
+  const uint64_t msg_total = moffs[n_groups];
+  HIP_TRY(c.b_sig.ensure((n_parts ? n_parts : 1) * 96));
+  HIP_TRY(c.b_ids.ensure((n_parts ? n_parts : 1) * 8));
+  HIP_TRY(c.b_off.ensure((n_groups + 1) * 8));
+  HIP_TRY(c.b_pk.ensure(n_groups * 48));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_kidx.ensure((n_groups + 1) * 8));  // message offsets
+  HIP_TRY(c.b_out.ensure(n_groups * 96));
+  HIP_TRY(c.b_st.ensure(n_groups * 8));          // aggregate statuses, then verify statuses
+  if (n_parts) {
+    HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_parts * 96, hipMemcpyHostToDevice, c.stream));
+    HIP_TRY(hipMemcpyAsync(c.b_ids.p, share_idx, n_parts * 8, hipMemcpyHostToDevice, c.stream));
+  }
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, goffs, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_pk.p, dv_pks, n_groups * 48, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_kidx.p, moffs, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  int32_t* ast = (int32_t*)c.b_st.p;
+  int32_t* vst = ast + n_groups;
+  int rc = launch_tagg_verify(c, (const uint8_t*)c.b_sig.p, (const int64_t*)c.b_ids.p, (const uint64_t*)c.b_off.p,
+                              n_groups, n_parts, (const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p,
+                              (const uint64_t*)c.b_kidx.p, (uint8_t*)c.b_out.p, ast, vst, c.stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out_sigs, c.b_out.p, n_groups * 96, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipMemcpyAsync(agg_status, ast, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipMemcpyAsync(verify_status, vst, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int sign_host(Context& c, const uint8_t* sks, const uint8_t* msgs, const uint64_t* offs, uint64_t n, uint8_t* out_sigs,
+              int32_t* status) {
+  const uint64_t msg_total = offs[n];
+  HIP_TRY(c.b_pk.ensure(n * 32));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_off.ensure((n + 1) * 8));
+  HIP_TRY(c.b_out.ensure(n * 96));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_pk.p, sks, n * 32, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, offs, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(k_sign, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_pk.p,
+                     (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p, n, (uint8_t*)c.b_out.p,
+                     (int32_t*)c.b_st.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out_sigs, c.b_out.p, n * 96, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int sk_to_pk_host(Context& c, const uint8_t* sks, uint64_t n, uint8_t* out_pks, int32_t* status) {
+  HIP_TRY(c.b_pk.ensure(n * 32));
+  HIP_TRY(c.b_out.ensure(n * 48));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_pk.p, sks, n * 32, hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(k_sk_to_pk, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_pk.p, n,
+                     (uint8_t*)c.b_out.p, (int32_t*)c.b_st.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out_pks, c.b_out.p, n * 48, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int fav_host(Context& c, const uint8_t* pks, const uint64_t* koffs, uint64_t n_groups, const uint8_t* sigs,
+             const uint8_t* msgs, const uint64_t* moffs, int32_t* status) {
+  const uint64_t nkeys = koffs[n_groups], msg_total = moffs[n_groups];
+  HIP_TRY(c.b_pk.ensure((nkeys ? nkeys : 1) * 48));
+  HIP_TRY(c.b_ids.ensure((n_groups + 1) * 8));
+  HIP_TRY(c.b_sig.ensure(n_groups * 96));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_off.ensure((n_groups + 1) * 8));
+  HIP_TRY(c.b_st.ensure(n_groups * 4));
+  if (nkeys) HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, nkeys * 48, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_ids.p, koffs, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_groups * 96, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, moffs, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  int rc = launch_fav(c, (const uint8_t*)c.b_pk.p, nkeys, (const uint64_t*)c.b_ids.p, n_groups,
+                      (const uint8_t*)c.b_sig.p, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p,
+                      (int32_t*)c.b_st.p, c.stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int aggregate_host(Context& c, const uint8_t* sigs, uint64_t n, uint8_t* out_sig, int32_t* status) {
+  HIP_TRY(c.b_sig.ensure((n ? n : 1) * 96));
+  HIP_TRY(c.b_out.ensure(96));
+  HIP_TRY(c.b_st.ensure(4));
+  if (n) HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
+  int rc = launch_aggregate(c, (const uint8_t*)c.b_sig.p, n, (uint8_t*)c.b_out.p, (int32_t*)c.b_st.p, c.stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out_sig, c.b_out.p, 96, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int verify_keys_host(Context& c, const uint32_t* key_idx, const uint8_t* msgs, const uint64_t* offs,
+                     const uint8_t* sigs, uint64_t n, int32_t* status) {
+  const uint64_t msg_total = offs[n];
+  HIP_TRY(c.b_kidx.ensure(n * 4));
+  HIP_TRY(c.b_sig.ensure(n * 96));
+  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
+  HIP_TRY(c.b_off.ensure((n + 1) * 8));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
+  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(c.b_off.p, offs, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  int rc = timed(c, "verify_keys", c.stream, [&] {
+    hipLaunchKernelGGL(k_verify_keys, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream,
+                       (const uint32_t*)c.b_kidx.p, c.t_size, (const int32_t*)c.t_code.p, (const uint32_t*)c.t_tab.p,
+                       (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p, (const uint8_t*)c.b_sig.p, n,
+                       (int32_t*)c.b_st.p);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return HIPBLS_OK;
+}
+
+int table_load_host(Context& c, const uint8_t* pks, uint64_t n, int32_t* status) {
+  HIP_TRY(hipDeviceSynchronize());  // no call may still read the old table
+  c.t_size = 0;
+  c.t_index.clear();
+  if (n == 0) return HIPBLS_OK;
+  HIP_TRY(c.b_pk.ensure(n * 48));
+  HIP_TRY(c.b_st.ensure(n * 4));
+  HIP_TRY(c.t_code.ensure(n * 4));
+  HIP_TRY(c.t_tab.ensure(n * PUBTAB_WORDS * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
+  hipLaunchKernelGGL(k_pubtab_load, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_pk.p, n,
+                     (int32_t*)c.t_code.p, (uint32_t*)c.t_tab.p, (int32_t*)c.b_st.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  c.t_size = n;
+  c.t_index.reserve(n);
+  for (uint64_t k = 0; k < n; ++k) c.t_index.emplace(std::string((const char*)pks + 48 * k, 48), (uint32_t)k);
+  return HIPBLS_OK;
+}
+
+// Minimum units per range before a batch is split across devices (each range must still fill a GPU's SIMDs for a
+// while; below this the call stays on one device and concurrent calls spread round robin).
+constexpr uint64_t kSplitVerify = 4096;   // Verify items
+constexpr uint64_t kSplitRlc = 16384;     // RLC items
+constexpr uint64_t kSplitGroups = 1024;   // ThresholdAggregate groups
+constexpr uint64_t kSplitSign = 4096;     // Sign / SecretToPublicKey items
+constexpr uint64_t kSplitFav = 64;        // FastAggregateVerify groups
+constexpr uint64_t kSplitAgg = 1 << 16;   // Aggregate signatures
 
 }  // namespace
 
@@ -977,14 +1555,30 @@ extern "C" {
 
 int hipbls_abi_version(void) { return HIPBLS_ABI_VERSION; }
 
-int hipbls_init(int device) {
+int hipbls_init_devices(const int32_t* ids, uint32_t n) {
+  if (!ids || n == 0 || n > (uint32_t)kMaxContexts) return arg_err("device list empty or longer than 64");
   std::lock_guard<std::mutex> lk(g_init_mu);
-  if (g_ctx.device >= 0) {
-    if (device >= 0 && device != g_ctx.device) return arg_err("hipbls already bound to another device");
-    HIP_TRY(hipSetDevice(g_ctx.device));
+  const int have = nctx();
+  if (have) {
+    bool same = have == (int)n;
+    for (int k = 0; same && k < have; ++k) same = ctx(k).device == ids[k];
+    if (!same) return arg_err("hipbls already bound to another device list");
+    HIP_TRY(hipSetDevice(ctx(0).device));
     return HIPBLS_OK;
   }
-  return init_locked(device < 0 ? 0 : device);
+  return init_locked(std::vector<int>(ids, ids + n));
+}
+
+int hipbls_init(int device) {
+  {
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    if (device < 0 && nctx()) {
+      HIP_TRY(hipSetDevice(ctx(0).device));
+      return HIPBLS_OK;
+    }
+  }
+  const int32_t d = device < 0 ? 0 : device;
+  return hipbls_init_devices(&d, 1);
 }
 
 int hipbls_device_count(void) {
@@ -993,12 +1587,25 @@ int hipbls_device_count(void) {
   return n;
 }
 
-int hipbls_current_device(void) { return g_ctx.device; }
+int hipbls_current_device(void) { return nctx() ? ctx(0).device : -1; }
+
+int hipbls_device_slots(int32_t* ids, uint32_t cap) {
+  const int n = nctx();
+  for (int k = 0; k < n && ids && (uint32_t)k < cap; ++k) ids[k] = ctx(k).device;
+  return n;
+}
+
+int hipbls_plan_ranges(uint64_t n, uint32_t parts, const uint32_t* run_keys, uint64_t* bounds) {
+  if (!bounds || parts == 0) return arg_err("bad plan arguments");
+  const std::vector<uint64_t> b = plan_ranges(n, parts, run_keys);
+  for (uint32_t k = 0; k <= parts; ++k) bounds[k] = k < b.size() ? b[k] : n;
+  return HIPBLS_OK;
+}
 
 const char* hipbls_last_error(void) { return g_last_error.c_str(); }
 
 int hipbls_set_timing(int enabled) {
-  g_ctx.timing_enabled = enabled != 0;
+  g_timing = enabled != 0;
   return HIPBLS_OK;
 }
 
@@ -1010,11 +1617,28 @@ int hipbls_rlc_set_mode(int mode) {
 
 int hipbls_rlc_batch_stats(uint64_t* attempted, uint64_t* passed, int32_t* last) {
   if (!attempted || !passed || !last) return arg_err("null output");
-  ENTER();
-  rlcb_poll(-1, true);
-  *attempted = g_ctx.rlcb_attempted;
-  *passed = g_ctx.rlcb_passed;
-  *last = g_ctx.rlcb_last;
+  ENSURE_INIT();
+  uint64_t a = 0, p = 0, newest = 0;
+  const int n = nctx();
+  for (int k = 0; k < n; ++k) {
+    Context& c = ctx(k);
+    ENTER_CTX(c);
+    const int rc = rlcb_poll(c, -1, true);
+    if (rc) return rc;
+    a += c.rlcb_attempted;
+    p += c.rlcb_passed;
+    if (c.rlcb_last >= 0 && c.rlcb_last_call > newest) newest = c.rlcb_last_call;
+  }
+  // the newest call's verdict: failed if the check of any of its ranges failed
+  int lst = -1;
+  for (int k = 0; k < n; ++k) {
+    Context& c = ctx(k);
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (c.rlcb_last >= 0 && c.rlcb_last_call == newest) lst = lst < 0 ? c.rlcb_last : (lst & c.rlcb_last);
+  }
+  *attempted = a;
+  *passed = p;
+  *last = lst;
   return HIPBLS_OK;
 }
 
@@ -1029,40 +1653,27 @@ int hipbls_verify_batch(const uint8_t* pks, const uint8_t* msgs, const uint64_t*
   if (n == 0) return HIPBLS_OK;
   if (!pks || !msg_offsets || !sigs || !status || mul_overflows(n, 96)) return arg_err("bad verify arguments");
   if (!offsets_ok(msg_offsets, n)) return arg_err("bad message offsets");
-  const uint64_t msg_total = msg_offsets[n];
-  if (msg_total && !msgs) return arg_err("null messages");
-  ENTER();
-  Context& c = g_ctx;
-  HIP_TRY(c.b_pk.ensure(n * 48));
-  HIP_TRY(c.b_sig.ensure(n * 96));
-  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
-  HIP_TRY(c.b_off.ensure((n + 1) * 8));
-  HIP_TRY(c.b_st.ensure(n * 4));
-  HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
-  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  int rc = ws_begin(c.stream);
-  if (rc) return rc;
-  rc = launch_verify((const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p,
-                     (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p, c.stream, c.v_ws);
-  if (rc) return rc;
-  rc = ws_end(c.stream);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return HIPBLS_OK;
+  if (msg_offsets[n] && !msgs) return arg_err("null messages");
+  ENSURE_INIT();
+  return run_ranges(plan_ranges(n, parts_for(n, kSplitVerify), nullptr), [&](Context& c, uint64_t lo, uint64_t hi) {
+    std::vector<uint64_t> tmp;
+    const uint64_t* offs = rebase(msg_offsets, lo, hi, tmp);
+    return verify_host(c, pks + 48 * lo, msgs ? msgs + msg_offsets[lo] : msgs, offs, sigs + 96 * lo, hi - lo,
+                       status + lo);
+  });
 }
 
 int hipbls_verify_batch_device(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
                                const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream) {
-  ENTER();
-  const hipStream_t s = pick(stream);
-  int rc = ws_begin(s);
+  ENSURE_INIT();
+  Context& c = ctx_of(d_status);
+  ENTER_CTX(c);
+  const hipStream_t s = pick(c, stream);
+  int rc = ws_begin(c, s);
   if (rc) return rc;
-  rc = launch_verify(d_pks, d_msgs, d_msg_offsets, d_sigs, n, d_status, s, g_ctx.v_ws);
+  rc = launch_verify(c, d_pks, d_msgs, d_msg_offsets, d_sigs, n, d_status, s, c.v_ws);
   if (rc) return rc;
-  return ws_end(s);
+  return ws_end(c, s);
 }
 
 int hipbls_verify(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, const uint8_t* sig96, int32_t* status) {
@@ -1081,17 +1692,34 @@ int hipbls_verify_wait(uint64_t ticket, int32_t* status) { return queue_wait(tic
 
 int hipbls_queue_config(uint64_t max_batch, uint32_t gather_us) {
   if (max_batch == 0 || max_batch > (1ull << 24)) return arg_err("max_batch out of range");
-  std::lock_guard<std::mutex> lk(g_q.mu);
-  g_q.max_batch = max_batch;
-  g_q.gather_us = gather_us;
+  g_q_max_batch = max_batch;
+  g_q_gather_us = gather_us;
   return HIPBLS_OK;
 }
 
 int hipbls_queue_stats(uint64_t* batches, uint64_t* items) {
   if (!batches || !items) return arg_err("null output");
-  std::lock_guard<std::mutex> lk(g_q.mu);
-  *batches = g_q.batches;
-  *items = g_q.items;
+  *batches = 0;
+  *items = 0;
+  const int n = nctx();
+  for (int k = 0; k < n; ++k) {
+    VerifyQueue& q = ctx(k).q;
+    std::lock_guard<std::mutex> lk(q.mu);
+    *batches += q.batches;
+    *items += q.items;
+  }
+  return HIPBLS_OK;
+}
+
+int hipbls_queue_keyed_batches(uint64_t* batches) {
+  if (!batches) return arg_err("null output");
+  *batches = 0;
+  const int n = nctx();
+  for (int k = 0; k < n; ++k) {
+    Context& c = ctx(k);
+    std::lock_guard<std::mutex> lk(c.mu);
+    *batches += c.q.keyed;
+  }
   return HIPBLS_OK;
 }
 
@@ -1099,65 +1727,30 @@ int hipbls_verify_signed_data_batch(const uint8_t* pks, const uint8_t* object_ro
                                     const uint8_t* sigs, uint64_t n, int32_t* status) {
   if (n == 0) return HIPBLS_OK;
   if (!pks || !object_roots || !domains || !sigs || !status || mul_overflows(n, 96)) return arg_err("bad arguments");
-  ENTER();
-  Context& c = g_ctx;
-  HIP_TRY(c.b_pk.ensure(n * 48));
-  HIP_TRY(c.b_sig.ensure(n * 96));
-  HIP_TRY(c.b_aux.ensure(n * 64));
-  HIP_TRY(c.b_msg.ensure(n * 32));
-  HIP_TRY(c.b_off.ensure((n + 1) * 8));
-  HIP_TRY(c.b_st.ensure(n * 4));
-  HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_aux.p, object_roots, n * 32, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync((uint8_t*)c.b_aux.p + n * 32, domains, n * 32, hipMemcpyHostToDevice, c.stream));
-  hipLaunchKernelGGL(k_signing_roots, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_aux.p,
-                     (const uint8_t*)c.b_aux.p + n * 32, n, (uint8_t*)c.b_msg.p, (uint64_t*)c.b_off.p);
-  HIP_TRY(hipGetLastError());
-  int rc = ws_begin(c.stream);
-  if (rc) return rc;
-  rc = launch_verify((const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p,
-                     (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p, c.stream, c.v_ws);
-  if (rc) return rc;
-  rc = ws_end(c.stream);
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_zero_sig_status, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream,
-                     (const uint8_t*)c.b_sig.p, n, (int32_t*)c.b_st.p);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return HIPBLS_OK;
+  ENSURE_INIT();
+  return run_ranges(plan_ranges(n, parts_for(n, kSplitVerify), nullptr), [&](Context& c, uint64_t lo, uint64_t hi) {
+    return signed_data_host(c, pks + 48 * lo, object_roots + 32 * lo, domains + 32 * lo, sigs + 96 * lo, hi - lo,
+                            status + lo);
+  });
 }
 
+// Group ranges: whole groups per device; partial offsets rebased to the range's first partial.
 int hipbls_threshold_aggregate_batch(const uint8_t* sigs, const int64_t* share_idx, const uint64_t* group_offsets,
                                      uint64_t n_groups, uint8_t* out_sigs, int32_t* status) {
   if (n_groups == 0) return HIPBLS_OK;
   if (!group_offsets || !out_sigs || !status || mul_overflows(n_groups, 96)) return arg_err("bad arguments");
-  if (group_offsets[0] != 0) return arg_err("group_offsets[0] != 0");
-  for (uint64_t g = 0; g < n_groups; ++g)
-    if (group_offsets[g + 1] < group_offsets[g]) return arg_err("decreasing group offsets");
+  if (!groups_ok(group_offsets, n_groups)) return arg_err("bad group offsets");
   const uint64_t n_parts = group_offsets[n_groups];
   if (n_parts && (!sigs || !share_idx)) return arg_err("null partials");
   if (mul_overflows(n_parts, 288)) return arg_err("too many partials");
-  ENTER();
-  Context& c = g_ctx;
-  HIP_TRY(c.b_sig.ensure((n_parts ? n_parts : 1) * 96));
-  HIP_TRY(c.b_ids.ensure((n_parts ? n_parts : 1) * 8));
-  HIP_TRY(c.b_off.ensure((n_groups + 1) * 8));
-  HIP_TRY(c.b_out.ensure(n_groups * 96));
-  HIP_TRY(c.b_st.ensure(n_groups * 4));
-  if (n_parts) {
-    HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_parts * 96, hipMemcpyHostToDevice, c.stream));
-    HIP_TRY(hipMemcpyAsync(c.b_ids.p, share_idx, n_parts * 8, hipMemcpyHostToDevice, c.stream));
-  }
-  HIP_TRY(hipMemcpyAsync(c.b_off.p, group_offsets, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  int rc = launch_tagg((const uint8_t*)c.b_sig.p, (const int64_t*)c.b_ids.p, (const uint64_t*)c.b_off.p, n_groups,
-                       n_parts, (uint8_t*)c.b_out.p, (int32_t*)c.b_st.p, c.stream);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(out_sigs, c.b_out.p, n_groups * 96, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return HIPBLS_OK;
+  ENSURE_INIT();
+  return run_ranges(plan_ranges(n_groups, parts_for(n_groups, kSplitGroups), nullptr),
+                    [&](Context& c, uint64_t lo, uint64_t hi) {
+                      std::vector<uint64_t> tmp;
+                      const uint64_t p0 = group_offsets[lo];
+                      return tagg_host(c, sigs ? sigs + 96 * p0 : sigs, share_idx ? share_idx + p0 : share_idx,
+                                       rebase(group_offsets, lo, hi, tmp), hi - lo, out_sigs + 96 * lo, status + lo);
+                    });
 }
 
 int hipbls_threshold_aggregate_verify_batch(const uint8_t* sigs, const int64_t* share_idx,
@@ -1168,44 +1761,22 @@ int hipbls_threshold_aggregate_verify_batch(const uint8_t* sigs, const int64_t* 
   if (!group_offsets || !dv_pks || !msg_offsets || !out_sigs || !agg_status || !verify_status ||
       mul_overflows(n_groups, 120 * 4))
     return arg_err("bad arguments");
-  if (group_offsets[0] != 0) return arg_err("group_offsets[0] != 0");
-  for (uint64_t g = 0; g < n_groups; ++g)
-    if (group_offsets[g + 1] < group_offsets[g]) return arg_err("decreasing group offsets");
+  if (!groups_ok(group_offsets, n_groups)) return arg_err("bad group offsets");
   if (!offsets_ok(msg_offsets, n_groups)) return arg_err("bad message offsets");
   const uint64_t n_parts = group_offsets[n_groups];
-  const uint64_t msg_total = msg_offsets[n_groups];
   if (n_parts && (!sigs || !share_idx)) return arg_err("null partials");
-  if (msg_total && !msgs) return arg_err("null messages");
+  if (msg_offsets[n_groups] && !msgs) return arg_err("null messages");
   if (mul_overflows(n_parts, 288)) return arg_err("too many partials");
-  ENTER();
-  Context& c = g_ctx;
-  HIP_TRY(c.b_sig.ensure((n_parts ? n_parts : 1) * 96));
-  HIP_TRY(c.b_ids.ensure((n_parts ? n_parts : 1) * 8));
-  HIP_TRY(c.b_off.ensure((n_groups + 1) * 8));
-  HIP_TRY(c.b_pk.ensure(n_groups * 48));
-  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
-  HIP_TRY(c.b_kidx.ensure((n_groups + 1) * 8));  // message offsets
-  HIP_TRY(c.b_out.ensure(n_groups * 96));
-  HIP_TRY(c.b_st.ensure(n_groups * 8));          // aggregate statuses, then verify statuses
-  if (n_parts) {
-    HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_parts * 96, hipMemcpyHostToDevice, c.stream));
-    HIP_TRY(hipMemcpyAsync(c.b_ids.p, share_idx, n_parts * 8, hipMemcpyHostToDevice, c.stream));
-  }
-  HIP_TRY(hipMemcpyAsync(c.b_off.p, group_offsets, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_pk.p, dv_pks, n_groups * 48, hipMemcpyHostToDevice, c.stream));
-  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_kidx.p, msg_offsets, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  int32_t* ast = (int32_t*)c.b_st.p;
-  int32_t* vst = ast + n_groups;
-  int rc = launch_tagg_verify((const uint8_t*)c.b_sig.p, (const int64_t*)c.b_ids.p, (const uint64_t*)c.b_off.p,
-                              n_groups, n_parts, (const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p,
-                              (const uint64_t*)c.b_kidx.p, (uint8_t*)c.b_out.p, ast, vst, c.stream);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(out_sigs, c.b_out.p, n_groups * 96, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipMemcpyAsync(agg_status, ast, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipMemcpyAsync(verify_status, vst, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return HIPBLS_OK;
+  ENSURE_INIT();
+  return run_ranges(plan_ranges(n_groups, parts_for(n_groups, kSplitGroups), nullptr),
+                    [&](Context& c, uint64_t lo, uint64_t hi) {
+                      std::vector<uint64_t> tg, tm;
+                      const uint64_t p0 = group_offsets[lo];
+                      return tagg_verify_host(c, sigs ? sigs + 96 * p0 : sigs, share_idx ? share_idx + p0 : share_idx,
+                                              rebase(group_offsets, lo, hi, tg), hi - lo, dv_pks + 48 * lo,
+                                              msgs ? msgs + msg_offsets[lo] : msgs, rebase(msg_offsets, lo, hi, tm),
+                                              out_sigs + 96 * lo, agg_status + lo, verify_status + lo);
+                    });
 }
 
 int hipbls_threshold_aggregate_verify_batch_device(const uint8_t* d_sigs, const int64_t* d_share_idx,
@@ -1215,9 +1786,11 @@ int hipbls_threshold_aggregate_verify_batch_device(const uint8_t* d_sigs, const 
                                                    int32_t* d_agg_status, int32_t* d_verify_status, void* stream) {
   if (n_groups == 0) return HIPBLS_OK;
   if (mul_overflows(n_parts, 288) || mul_overflows(n_groups, 120 * 4)) return arg_err("too many items");
-  ENTER();
-  return launch_tagg_verify(d_sigs, d_share_idx, d_group_offsets, n_groups, n_parts, d_dv_pks, d_msgs, d_msg_offsets,
-                            d_out_sigs, d_agg_status, d_verify_status, pick(stream));
+  ENSURE_INIT();
+  Context& c = ctx_of(d_agg_status);
+  ENTER_CTX(c);
+  return launch_tagg_verify(c, d_sigs, d_share_idx, d_group_offsets, n_groups, n_parts, d_dv_pks, d_msgs,
+                            d_msg_offsets, d_out_sigs, d_agg_status, d_verify_status, pick(c, stream));
 }
 
 int hipbls_threshold_aggregate_batch_device(const uint8_t* d_sigs, const int64_t* d_share_idx,
@@ -1225,8 +1798,11 @@ int hipbls_threshold_aggregate_batch_device(const uint8_t* d_sigs, const int64_t
                                             uint8_t* d_out_sigs, int32_t* d_status, void* stream) {
   if (n_groups == 0) return HIPBLS_OK;
   if (mul_overflows(n_parts, 288)) return arg_err("too many partials");
-  ENTER();
-  return launch_tagg(d_sigs, d_share_idx, d_group_offsets, n_groups, n_parts, d_out_sigs, d_status, pick(stream));
+  ENSURE_INIT();
+  Context& c = ctx_of(d_status);
+  ENTER_CTX(c);
+  return launch_tagg(c, d_sigs, d_share_idx, d_group_offsets, n_groups, n_parts, d_out_sigs, d_status,
+                     pick(c, stream));
 }
 
 int hipbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n,
@@ -1234,34 +1810,23 @@ int hipbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* m
   if (n == 0) return HIPBLS_OK;
   if (!sks || !msg_offsets || !out_sigs || !status || mul_overflows(n, 96)) return arg_err("bad sign arguments");
   if (!offsets_ok(msg_offsets, n)) return arg_err("bad message offsets");
-  const uint64_t msg_total = msg_offsets[n];
-  if (msg_total && !msgs) return arg_err("null messages");
-  ENTER();
-  Context& c = g_ctx;
-  HIP_TRY(c.b_pk.ensure(n * 32));
-  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
-  HIP_TRY(c.b_off.ensure((n + 1) * 8));
-  HIP_TRY(c.b_out.ensure(n * 96));
-  HIP_TRY(c.b_st.ensure(n * 4));
-  HIP_TRY(hipMemcpyAsync(c.b_pk.p, sks, n * 32, hipMemcpyHostToDevice, c.stream));
-  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  hipLaunchKernelGGL(k_sign, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_pk.p,
-                     (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p, n, (uint8_t*)c.b_out.p,
-                     (int32_t*)c.b_st.p);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out_sigs, c.b_out.p, n * 96, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return HIPBLS_OK;
+  if (msg_offsets[n] && !msgs) return arg_err("null messages");
+  ENSURE_INIT();
+  return run_ranges(plan_ranges(n, parts_for(n, kSplitSign), nullptr), [&](Context& c, uint64_t lo, uint64_t hi) {
+    std::vector<uint64_t> tmp;
+    return sign_host(c, sks + 32 * lo, msgs ? msgs + msg_offsets[lo] : msgs, rebase(msg_offsets, lo, hi, tmp),
+                     hi - lo, out_sigs + 96 * lo, status + lo);
+  });
 }
 
 int hipbls_sign_batch_device(const uint8_t* d_sks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets, uint64_t n,
                              uint8_t* d_out_sigs, int32_t* d_status, void* stream) {
   if (n == 0) return HIPBLS_OK;
-  ENTER();
-  hipLaunchKernelGGL(k_sign, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, pick(stream), d_sks, d_msgs, d_msg_offsets,
-                     n, d_out_sigs, d_status);
+  ENSURE_INIT();
+  Context& c = ctx_of(d_status);
+  ENTER_CTX(c);
+  hipLaunchKernelGGL(k_sign, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, pick(c, stream), d_sks, d_msgs,
+                     d_msg_offsets, n, d_out_sigs, d_status);
   HIP_TRY(hipGetLastError());
   return HIPBLS_OK;
 }
@@ -1269,26 +1834,19 @@ int hipbls_sign_batch_device(const uint8_t* d_sks, const uint8_t* d_msgs, const 
 int hipbls_secret_to_public_key_batch(const uint8_t* sks, uint64_t n, uint8_t* out_pks, int32_t* status) {
   if (n == 0) return HIPBLS_OK;
   if (!sks || !out_pks || !status || mul_overflows(n, 48)) return arg_err("bad arguments");
-  ENTER();
-  Context& c = g_ctx;
-  HIP_TRY(c.b_pk.ensure(n * 32));
-  HIP_TRY(c.b_out.ensure(n * 48));
-  HIP_TRY(c.b_st.ensure(n * 4));
-  HIP_TRY(hipMemcpyAsync(c.b_pk.p, sks, n * 32, hipMemcpyHostToDevice, c.stream));
-  hipLaunchKernelGGL(k_sk_to_pk, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_pk.p, n,
-                     (uint8_t*)c.b_out.p, (int32_t*)c.b_st.p);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out_pks, c.b_out.p, n * 48, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return HIPBLS_OK;
+  ENSURE_INIT();
+  return run_ranges(plan_ranges(n, parts_for(n, kSplitSign), nullptr), [&](Context& c, uint64_t lo, uint64_t hi) {
+    return sk_to_pk_host(c, sks + 32 * lo, hi - lo, out_pks + 48 * lo, status + lo);
+  });
 }
 
 int hipbls_secret_to_public_key_batch_device(const uint8_t* d_sks, uint64_t n, uint8_t* d_out_pks, int32_t* d_status,
                                              void* stream) {
   if (n == 0) return HIPBLS_OK;
-  ENTER();
-  hipLaunchKernelGGL(k_sk_to_pk, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, pick(stream), d_sks, n, d_out_pks,
+  ENSURE_INIT();
+  Context& c = ctx_of(d_status);
+  ENTER_CTX(c);
+  hipLaunchKernelGGL(k_sk_to_pk, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, pick(c, stream), d_sks, n, d_out_pks,
                      d_status);
   HIP_TRY(hipGetLastError());
   return HIPBLS_OK;
@@ -1298,40 +1856,30 @@ int hipbls_verify_aggregate_batch(const uint8_t* pks, const uint64_t* key_offset
                                   const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_offsets,
                                   int32_t* status) {
   if (n_groups == 0) return HIPBLS_OK;
-  if (!key_offsets || !sigs || !msg_offsets || !status || key_offsets[0] != 0 || mul_overflows(n_groups, 96))
-    return arg_err("bad arguments");
+  if (!key_offsets || !sigs || !msg_offsets || !status || mul_overflows(n_groups, 96)) return arg_err("bad arguments");
+  if (!groups_ok(key_offsets, n_groups)) return arg_err("bad key offsets");
   if (!offsets_ok(msg_offsets, n_groups)) return arg_err("bad message offsets");
-  for (uint64_t g = 0; g < n_groups; ++g)
-    if (key_offsets[g + 1] < key_offsets[g]) return arg_err("decreasing key offsets");
   const uint64_t nkeys = key_offsets[n_groups], msg_total = msg_offsets[n_groups];
   if ((nkeys && !pks) || (msg_total && !msgs) || mul_overflows(nkeys, 96)) return arg_err("bad arguments");
-  ENTER();
-  Context& c = g_ctx;
-  HIP_TRY(c.b_pk.ensure((nkeys ? nkeys : 1) * 48));
-  HIP_TRY(c.b_ids.ensure((n_groups + 1) * 8));
-  HIP_TRY(c.b_sig.ensure(n_groups * 96));
-  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
-  HIP_TRY(c.b_off.ensure((n_groups + 1) * 8));
-  HIP_TRY(c.b_st.ensure(n_groups * 4));
-  if (nkeys) HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, nkeys * 48, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_ids.p, key_offsets, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_groups * 96, hipMemcpyHostToDevice, c.stream));
-  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  int rc = launch_fav((const uint8_t*)c.b_pk.p, nkeys, (const uint64_t*)c.b_ids.p, n_groups, (const uint8_t*)c.b_sig.p,
-                      (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p, (int32_t*)c.b_st.p, c.stream);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return HIPBLS_OK;
+  ENSURE_INIT();
+  return run_ranges(plan_ranges(n_groups, parts_for(n_groups, kSplitFav), nullptr),
+                    [&](Context& c, uint64_t lo, uint64_t hi) {
+                      std::vector<uint64_t> tk, tm;
+                      return fav_host(c, pks ? pks + 48 * key_offsets[lo] : pks, rebase(key_offsets, lo, hi, tk),
+                                      hi - lo, sigs + 96 * lo, msgs ? msgs + msg_offsets[lo] : msgs,
+                                      rebase(msg_offsets, lo, hi, tm), status + lo);
+                    });
 }
 
 int hipbls_verify_aggregate_batch_device(const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_key_offsets,
                                          uint64_t n_groups, const uint8_t* d_sigs, const uint8_t* d_msgs,
                                          const uint64_t* d_msg_offsets, int32_t* d_status, void* stream) {
   if (n_groups == 0) return HIPBLS_OK;
-  ENTER();
-  return launch_fav(d_pks, nkeys, d_key_offsets, n_groups, d_sigs, d_msgs, d_msg_offsets, d_status, pick(stream));
+  ENSURE_INIT();
+  Context& c = ctx_of(d_status);
+  ENTER_CTX(c);
+  return launch_fav(c, d_pks, nkeys, d_key_offsets, n_groups, d_sigs, d_msgs, d_msg_offsets, d_status,
+                    pick(c, stream));
 }
 
 int hipbls_verify_aggregate(const uint8_t* pks, uint64_t n, const uint8_t* sig, const uint8_t* msg, uint64_t msg_len,
@@ -1343,34 +1891,50 @@ int hipbls_verify_aggregate(const uint8_t* pks, uint64_t n, const uint8_t* sig, 
   return hipbls_verify_aggregate_batch(n ? pks : &empty, koff, 1, sig, msg_len ? msg : &empty, moff, status);
 }
 
+// A large Aggregate is summed per device range; the ranges' 96-byte partial sums are then aggregated once more (a
+// compressed sum decodes to the same point, so the total is the same G2 sum; a bad encoding anywhere fails).
 int hipbls_aggregate(const uint8_t* sigs, uint64_t n, uint8_t* out_sig, int32_t* status) {
   if (!out_sig || !status || (n && !sigs) || mul_overflows(n, 192)) return arg_err("bad arguments");
-  ENTER();
-  Context& c = g_ctx;
-  HIP_TRY(c.b_sig.ensure((n ? n : 1) * 96));
-  HIP_TRY(c.b_out.ensure(96));
-  HIP_TRY(c.b_st.ensure(4));
-  if (n) HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
-  int rc = launch_aggregate((const uint8_t*)c.b_sig.p, n, (uint8_t*)c.b_out.p, (int32_t*)c.b_st.p, c.stream);
+  ENSURE_INIT();
+  const std::vector<uint64_t> b = plan_ranges(n, parts_for(n, kSplitAgg), nullptr);
+  const size_t k = b.size() - 1;
+  if (k == 1)
+    return run_ranges(b, [&](Context& c, uint64_t lo, uint64_t hi) {
+      return aggregate_host(c, sigs + 96 * lo, hi - lo, out_sig, status);
+    });
+  std::vector<uint8_t> part(96 * k);
+  std::vector<int32_t> pst(k, HIPBLS_OK);
+  int rc = run_ranges(b, [&](Context& c, uint64_t lo, uint64_t hi) {
+    const size_t j = (size_t)c.slot;  // range j runs on context j
+    return aggregate_host(c, sigs + 96 * lo, hi - lo, part.data() + 96 * j, &pst[j]);
+  });
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(out_sig, c.b_out.p, 96, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return HIPBLS_OK;
+  for (size_t j = 0; j < k; ++j)
+    if (pst[j] != HIPBLS_OK) {
+      *status = pst[j];
+      memset(out_sig, 0, 96);
+      return HIPBLS_OK;
+    }
+  Context& c0 = ctx(0);
+  ENTER_CTX(c0);
+  return aggregate_host(c0, part.data(), k, out_sig, status);
 }
 
 int hipbls_aggregate_device(const uint8_t* d_sigs, uint64_t n, uint8_t* d_out_sig, int32_t* d_status, void* stream) {
   if (mul_overflows(n, 192)) return arg_err("too many signatures");
-  ENTER();
-  return launch_aggregate(d_sigs, n, d_out_sig, d_status, pick(stream));
+  ENSURE_INIT();
+  Context& c = ctx_of(d_status);
+  ENTER_CTX(c);
+  return launch_aggregate(c, d_sigs, n, d_out_sig, d_status, pick(c, stream));
 }
 
 int hipbls_threshold_split(const uint8_t* secret, const uint8_t* poly_tail, uint32_t total, uint32_t threshold,
                            uint8_t* out_shares, int32_t* status) {
   if (!secret || !out_shares || !status || threshold == 0 || total == 0 || (threshold > 1 && !poly_tail))
     return arg_err("bad split arguments");
-  ENTER();
-  Context& c = g_ctx;
+  ENSURE_INIT();
+  Context& c = ctx(0);
+  ENTER_CTX(c);
   HIP_TRY(c.b_aux.ensure(32 * (uint64_t)threshold));
   HIP_TRY(c.b_out.ensure(32 * (uint64_t)total));
   HIP_TRY(c.b_st.ensure(4));
@@ -1391,8 +1955,9 @@ int hipbls_threshold_split(const uint8_t* secret, const uint8_t* poly_tail, uint
 int hipbls_recover_secret(const uint8_t* shares, const int64_t* ids, uint32_t n, uint8_t* out_secret,
                           int32_t* status) {
   if (!out_secret || !status || (n && (!shares || !ids))) return arg_err("bad recover arguments");
-  ENTER();
-  Context& c = g_ctx;
+  ENSURE_INIT();
+  Context& c = ctx(0);
+  ENTER_CTX(c);
   HIP_TRY(c.b_aux.ensure(32 * (uint64_t)(n ? n : 1)));
   HIP_TRY(c.b_ids.ensure(8 * (uint64_t)(n ? n : 1)));
   HIP_TRY(c.b_out.ensure(32));
@@ -1412,32 +1977,53 @@ int hipbls_recover_secret(const uint8_t* shares, const int64_t* ids, uint32_t n,
 
 int hipbls_kernel_timing(const char* name, double* avg_ms, uint64_t* launches) {
   if (!name || !avg_ms || !launches) return arg_err("null argument");
-  int rc = bind_device();
-  if (rc) return rc;
-  std::lock_guard<std::mutex> lk(g_ctx.tmu);
-  auto it = g_ctx.timing.find(name);
-  if (it == g_ctx.timing.end()) {
-    *launches = 0;
-    *avg_ms = 0.0;
-    return HIPBLS_OK;
+  ENSURE_INIT();
+  double total = 0;
+  uint64_t cnt = 0;
+  const int n = nctx();
+  for (int k = 0; k < n; ++k) {
+    Context& c = ctx(k);
+    int rc = bind(c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c.tmu);
+    auto it = c.timing.find(name);
+    if (it == c.timing.end()) continue;
+    drain_timing(it->second, true);
+    total += it->second.total_ms;
+    cnt += it->second.launches;
   }
-  TimingSlot& t = it->second;
-  drain_timing(t, true);
-  *launches = t.launches;
-  *avg_ms = t.launches ? t.total_ms / t.launches : 0.0;
+  *launches = cnt;
+  *avg_ms = cnt ? total / cnt : 0.0;
   return HIPBLS_OK;
 }
 
 int hipbls_kernel_timing_reset(void) {
-  int rc = bind_device();
-  if (rc) return rc;
-  std::lock_guard<std::mutex> lk(g_ctx.tmu);
-  for (auto& kv : g_ctx.timing) {
-    drain_timing(kv.second, true);
-    kv.second.total_ms = 0;
-    kv.second.launches = 0;
+  ENSURE_INIT();
+  const int n = nctx();
+  for (int k = 0; k < n; ++k) {
+    Context& c = ctx(k);
+    int rc = bind(c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c.tmu);
+    for (auto& kv : c.timing) {
+      drain_timing(kv.second, true);
+      kv.second.total_ms = 0;
+      kv.second.launches = 0;
+    }
   }
   return HIPBLS_OK;
+}
+
+// RLC ranges: whole message runs (a validator's partials) per device, each with its own message table and scalars.
+int rlc_entry(const uint8_t* pks, const uint32_t* key_idx, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
+              const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n_msgs, const uint8_t* seed32,
+              int32_t* status) {
+  const uint64_t call = g_call_seq.fetch_add(1) + 1;
+  const std::vector<uint64_t> b = plan_ranges(n, parts_for(n, kSplitRlc), msg_idx);
+  const bool whole = b.size() == 2;
+  return run_ranges(b, [&](Context& c, uint64_t lo, uint64_t hi) {
+    return rlc_range(c, pks, key_idx, sigs, msg_idx, lo, hi, msgs, msg_offsets, n_msgs, seed32, status, call, whole);
+  });
 }
 
 int hipbls_batch_verify_rlc(const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx, uint64_t n,
@@ -1450,8 +2036,8 @@ int hipbls_batch_verify_rlc(const uint8_t* pks, const uint8_t* sigs, const uint3
     if (msg_idx[i] >= n_msgs) return arg_err("message index out of range");
   if (!offsets_ok(msg_offsets, n_msgs)) return arg_err("bad message offsets");
   if (msg_offsets[n_msgs] && !msgs) return arg_err("null messages");
-  ENTER();
-  return rlc_host(pks, nullptr, sigs, msg_idx, n, msgs, msg_offsets, n_msgs, seed32, status);
+  ENSURE_INIT();
+  return rlc_entry(pks, nullptr, sigs, msg_idx, n, msgs, msg_offsets, n_msgs, seed32, status);
 }
 
 int hipbls_batch_verify_rlc_device(const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_msg_idx, uint64_t n,
@@ -1459,58 +2045,61 @@ int hipbls_batch_verify_rlc_device(const uint8_t* d_pks, const uint8_t* d_sigs, 
                                    const uint8_t* seed32, int32_t* d_status, void* stream) {
   if (n == 0) return HIPBLS_OK;
   if (!seed32 || mul_overflows(n, 288)) return arg_err("bad RLC arguments");
-  ENTER();
-  return launch_rlc(d_pks, d_sigs, d_msg_idx, n, d_msgs, d_msg_offsets, n_msgs, seed32, d_status, pick(stream));
+  ENSURE_INIT();
+  Context& c = ctx_of(d_status);
+  ENTER_CTX(c);
+  return launch_rlc(c, d_pks, d_sigs, d_msg_idx, n, d_msgs, d_msg_offsets, n_msgs, parse_seed(seed32), d_status,
+                    pick(c, stream), g_call_seq.fetch_add(1) + 1);
 }
 
 int hipbls_hcache_config(uint64_t capacity) {
   if (capacity > (1ull << 24)) return arg_err("H(m) cache capacity above 2^24");
-  ENTER();
-  HCache& hc = g_ctx.hcache;
-  HIP_TRY(hipDeviceSynchronize());  // no call may still read the old table
-  hc.map.clear();
-  hc.key_of.assign(capacity, std::string());
-  hc.ring = 0;
-  hc.hits = hc.misses = 0;
-  hc.cap = capacity;
-  if (capacity) HIP_TRY(hc.table.ensure(capacity * 48 * 4));
-  return HIPBLS_OK;
+  ENSURE_INIT();
+  return run_all([&](Context& c) -> int {
+    HCache& hc = c.hcache;
+    HIP_TRY(hipDeviceSynchronize());  // no call may still read the old table
+    hc.map.clear();
+    hc.key_of.assign(capacity, std::string());
+    hc.ring = 0;
+    hc.hits = hc.misses = 0;
+    hc.cap = capacity;
+    if (capacity) HIP_TRY(hc.table.ensure(capacity * 48 * 4));
+    return HIPBLS_OK;
+  });
 }
 
 int hipbls_hcache_stats(uint64_t* hits, uint64_t* misses, uint64_t* entries) {
   if (!hits || !misses || !entries) return arg_err("null output");
-  std::lock_guard<std::mutex> lk(g_ctx.mu);
-  *hits = g_ctx.hcache.hits;
-  *misses = g_ctx.hcache.misses;
-  *entries = g_ctx.hcache.map.size();
+  *hits = *misses = *entries = 0;
+  const int n = nctx();
+  for (int k = 0; k < n; ++k) {
+    Context& c = ctx(k);
+    std::lock_guard<std::mutex> lk(c.mu);
+    *hits += c.hcache.hits;
+    *misses += c.hcache.misses;
+    *entries += c.hcache.map.size();
+  }
   return HIPBLS_OK;
 }
 
+// The table is replicated on every device (244 B per key: a whole cluster's pubshares fit many times over).
 int hipbls_pubshare_table_load(const uint8_t* pks, uint64_t n, int32_t* status) {
   if ((n && (!pks || !status)) || mul_overflows(n, 240) || n > 0xffffffffull) return arg_err("bad table arguments");
-  ENTER();
-  Context& c = g_ctx;
-  HIP_TRY(hipDeviceSynchronize());  // no call may still read the old table
-  c.t_size = 0;
-  if (n == 0) return HIPBLS_OK;
-  HIP_TRY(c.b_pk.ensure(n * 48));
-  HIP_TRY(c.b_st.ensure(n * 4));
-  HIP_TRY(c.t_code.ensure(n * 4));
-  HIP_TRY(c.t_tab.ensure(n * PUBTAB_WORDS * 4));
-  HIP_TRY(hipMemcpyAsync(c.b_pk.p, pks, n * 48, hipMemcpyHostToDevice, c.stream));
-  hipLaunchKernelGGL(k_pubtab_load, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_pk.p, n,
-                     (int32_t*)c.t_code.p, (uint32_t*)c.t_tab.p, (int32_t*)c.b_st.p);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  c.t_size = n;
+  ENSURE_INIT();
+  const int nc = nctx();
+  std::vector<std::vector<int32_t>> st(nc, std::vector<int32_t>(n ? n : 1));
+  int rc = run_all([&](Context& c) -> int { return table_load_host(c, pks, n, st[c.slot].data()); });
+  if (rc) return rc;
+  if (n) memcpy(status, st[0].data(), n * 4);
   return HIPBLS_OK;
 }
 
 int hipbls_pubshare_table_size(uint64_t* n) {
   if (!n) return arg_err("null output");
-  std::lock_guard<std::mutex> lk(g_ctx.mu);
-  *n = g_ctx.t_size;
+  ENSURE_INIT();
+  Context& c = ctx(0);
+  std::lock_guard<std::mutex> lk(c.mu);
+  *n = c.t_size;
   return HIPBLS_OK;
 }
 
@@ -1519,40 +2108,30 @@ int hipbls_verify_batch_keys(const uint32_t* key_idx, const uint8_t* msgs, const
   if (n == 0) return HIPBLS_OK;
   if (!key_idx || !msg_offsets || !sigs || !status || mul_overflows(n, 96)) return arg_err("bad arguments");
   if (!offsets_ok(msg_offsets, n)) return arg_err("bad message offsets");
-  const uint64_t msg_total = msg_offsets[n];
-  if (msg_total && !msgs) return arg_err("null messages");
-  ENTER();
-  Context& c = g_ctx;
+  if (msg_offsets[n] && !msgs) return arg_err("null messages");
+  ENSURE_INIT();
+  uint64_t T = 0;
+  {
+    std::lock_guard<std::mutex> lk(ctx(0).mu);
+    T = ctx(0).t_size;
+  }
   for (uint64_t i = 0; i < n; ++i)
-    if (key_idx[i] >= c.t_size) return arg_err("key index outside the pubshare table");
-  HIP_TRY(c.b_kidx.ensure(n * 4));
-  HIP_TRY(c.b_sig.ensure(n * 96));
-  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
-  HIP_TRY(c.b_off.ensure((n + 1) * 8));
-  HIP_TRY(c.b_st.ensure(n * 4));
-  HIP_TRY(hipMemcpyAsync(c.b_kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n * 96, hipMemcpyHostToDevice, c.stream));
-  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_off.p, msg_offsets, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  int rc = timed("verify_keys", c.stream, [&] {
-    hipLaunchKernelGGL(k_verify_keys, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream,
-                       (const uint32_t*)c.b_kidx.p, c.t_size, (const int32_t*)c.t_code.p, (const uint32_t*)c.t_tab.p,
-                       (const uint8_t*)c.b_msg.p, (const uint64_t*)c.b_off.p, (const uint8_t*)c.b_sig.p, n,
-                       (int32_t*)c.b_st.p);
+    if (key_idx[i] >= T) return arg_err("key index outside the pubshare table");
+  return run_ranges(plan_ranges(n, parts_for(n, kSplitVerify), nullptr), [&](Context& c, uint64_t lo, uint64_t hi) {
+    std::vector<uint64_t> tmp;
+    return verify_keys_host(c, key_idx + lo, msgs ? msgs + msg_offsets[lo] : msgs, rebase(msg_offsets, lo, hi, tmp),
+                            sigs + 96 * lo, hi - lo, status + lo);
   });
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(status, c.b_st.p, n * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return HIPBLS_OK;
 }
 
 int hipbls_verify_batch_keys_device(const uint32_t* d_key_idx, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
                                     const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream) {
   if (n == 0) return HIPBLS_OK;
-  ENTER();
-  Context& c = g_ctx;
-  hipStream_t s = pick(stream);
-  return timed("verify_keys", s, [&] {
+  ENSURE_INIT();
+  Context& c = ctx_of(d_status);
+  ENTER_CTX(c);
+  hipStream_t s = pick(c, stream);
+  return timed(c, "verify_keys", s, [&] {
     hipLaunchKernelGGL(k_verify_keys, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_key_idx, c.t_size,
                        (const int32_t*)c.t_code.p, (const uint32_t*)c.t_tab.p, d_msgs, d_msg_offsets, d_sigs, n,
                        d_status);
@@ -1569,10 +2148,15 @@ int hipbls_batch_verify_rlc_keys(const uint32_t* key_idx, const uint8_t* sigs, c
     if (msg_idx[i] >= n_msgs) return arg_err("message index out of range");
   if (!offsets_ok(msg_offsets, n_msgs)) return arg_err("bad message offsets");
   if (msg_offsets[n_msgs] && !msgs) return arg_err("null messages");
-  ENTER();
+  ENSURE_INIT();
+  uint64_t T = 0;
+  {
+    std::lock_guard<std::mutex> lk(ctx(0).mu);
+    T = ctx(0).t_size;
+  }
   for (uint64_t i = 0; i < n; ++i)
-    if (key_idx[i] >= g_ctx.t_size) return arg_err("key index outside the pubshare table");
-  return rlc_host(nullptr, key_idx, sigs, msg_idx, n, msgs, msg_offsets, n_msgs, seed32, status);
+    if (key_idx[i] >= T) return arg_err("key index outside the pubshare table");
+  return rlc_entry(nullptr, key_idx, sigs, msg_idx, n, msgs, msg_offsets, n_msgs, seed32, status);
 }
 
 int hipbls_batch_verify_rlc_keys_device(const uint32_t* d_key_idx, const uint8_t* d_sigs, const uint32_t* d_msg_idx,
@@ -1580,27 +2164,38 @@ int hipbls_batch_verify_rlc_keys_device(const uint32_t* d_key_idx, const uint8_t
                                         uint64_t n_msgs, const uint8_t* seed32, int32_t* d_status, void* stream) {
   if (n == 0) return HIPBLS_OK;
   if (!seed32 || !d_key_idx || mul_overflows(n, 288)) return arg_err("bad RLC arguments");
-  ENTER();
-  return launch_rlc(nullptr, d_sigs, d_msg_idx, n, d_msgs, d_msg_offsets, n_msgs, seed32, d_status, pick(stream),
-                    d_key_idx);
+  ENSURE_INIT();
+  Context& c = ctx_of(d_status);
+  ENTER_CTX(c);
+  return launch_rlc(c, nullptr, d_sigs, d_msg_idx, n, d_msgs, d_msg_offsets, n_msgs, parse_seed(seed32), d_status,
+                    pick(c, stream), g_call_seq.fetch_add(1) + 1, d_key_idx);
 }
 
+// Windows, failed windows and re-verified items of the newest RLC call, summed over the devices it ran on.
 int hipbls_rlc_stats(uint64_t* windows, uint64_t* windows_failed, uint64_t* items_fallback) {
   if (!windows || !windows_failed || !items_fallback) return arg_err("null output");
-  ENTER();
-  Context& c = g_ctx;
-  *windows = c.r_windows;
-  *windows_failed = 0;
-  *items_fallback = 0;
-  if (c.r_windows == 0) return HIPBLS_OK;
-  std::vector<int32_t> v(c.r_windows);
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(v.data(), c.r_win.p, v.size() * 4, hipMemcpyDeviceToHost));
-  for (int32_t x : v)
-    if (x > 0) {
-      *windows_failed += 1;
-      *items_fallback += (uint64_t)x;
-    }
+  ENSURE_INIT();
+  *windows = *windows_failed = *items_fallback = 0;
+  const int n = nctx();
+  uint64_t newest = 0;
+  for (int k = 0; k < n; ++k) {
+    std::lock_guard<std::mutex> lk(ctx(k).mu);
+    if (ctx(k).r_call > newest) newest = ctx(k).r_call;
+  }
+  for (int k = 0; k < n; ++k) {
+    Context& c = ctx(k);
+    ENTER_CTX(c);
+    if (c.r_call != newest || c.r_windows == 0) continue;
+    std::vector<int32_t> v(c.r_windows);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(v.data(), c.r_win.p, v.size() * 4, hipMemcpyDeviceToHost));
+    *windows += c.r_windows;
+    for (int32_t x : v)
+      if (x > 0) {
+        *windows_failed += 1;
+        *items_fallback += (uint64_t)x;
+      }
+  }
   return HIPBLS_OK;
 }
 

@@ -63,6 +63,10 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
     vp = ctypes.c_void_p
     sig = {
         "hipbls_current_device": ([], ctypes.c_int),
+        "hipbls_init_devices": ([ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32], ctypes.c_int),
+        "hipbls_device_slots": ([ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32], ctypes.c_int),
+        "hipbls_plan_ranges": ([u64, ctypes.c_uint32, u32p, u64p], ctypes.c_int),
+        "hipbls_queue_keyed_batches": ([u64p], ctypes.c_int),
         "hipbls_set_timing": ([ctypes.c_int], ctypes.c_int),
         "hipbls_set_pair_mode": ([ctypes.c_int], ctypes.c_int),
         "hipbls_rlc_set_mode": ([ctypes.c_int], ctypes.c_int),
@@ -134,8 +138,19 @@ def exported_symbols() -> List[str]:
         "hipbls_queue_config", "hipbls_queue_stats", "hipbls_verify_signed_data_batch", "hipbls_aggregate_device",
         "hipbls_hcache_config", "hipbls_hcache_stats", "hipbls_set_pair_mode",
         "hipbls_rlc_set_mode", "hipbls_rlc_batch_stats", "hipbls_threshold_aggregate_verify_batch",
-        "hipbls_threshold_aggregate_verify_batch_device",
+        "hipbls_threshold_aggregate_verify_batch_device", "hipbls_init_devices", "hipbls_device_slots",
+        "hipbls_plan_ranges", "hipbls_queue_keyed_batches",
     ]
+
+
+def plan_ranges(n: int, parts: int, run_keys: Optional[Sequence[int]] = None) -> List[int]:
+    """The library's batch split (hipbls_plan_ranges; host code, no GPU): bounds of `parts` contiguous ranges of n
+    items, inner bounds moved to the next change of run key (a validator's partials stay on one device)."""
+    lib = load_library()
+    b = (ctypes.c_uint64 * (parts + 1))()
+    keys = (ctypes.c_uint32 * max(n, 1))(*run_keys) if run_keys is not None else None
+    _check(lib.hipbls_plan_ranges(n, parts, keys, b), lib)
+    return list(b)
 
 
 def _check(rc: int, lib) -> None:
@@ -178,11 +193,23 @@ def _check_lengths(name: str, items: Sequence[bytes], size: int) -> None:
 class HipBLS:
     """tbls.Implementation on MI355X.  Method names follow tbls.go:28-69 (snake_case)."""
 
-    def __init__(self, device: Optional[int] = None):
+    def __init__(self, device: Optional[int] = None, devices: Optional[Sequence[int]] = None):
+        """device: the one GPU of this process (default LOCAL_RANK, or 0).  devices: every GPU this process drives
+        (charon's one process per node); batches are split across them (hipbls_init_devices)."""
         self.lib = load_library()
+        if devices is not None:
+            arr = (ctypes.c_int32 * len(devices))(*devices)
+            _check(self.lib.hipbls_init_devices(arr, len(devices)), self.lib)
+            return
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         _check(self.lib.hipbls_init(device), self.lib)
+
+    def device_slots(self) -> List[int]:
+        """The device of each context the library drives (hipbls_device_slots)."""
+        arr = (ctypes.c_int32 * 64)()
+        n = self.lib.hipbls_device_slots(arr, 64)
+        return list(arr)[:n]
 
     # ---------------------------------------------------------------- key tooling
     def generate_secret_key(self) -> bytes:
@@ -524,6 +551,12 @@ class HipBLS:
 
     def queue_config(self, max_batch: int = 65536, gather_us: int = 200) -> None:
         _check(self.lib.hipbls_queue_config(max_batch, gather_us), self.lib)
+
+    def queue_keyed_batches(self) -> int:
+        """Queue batches that ran keyed (resident pubshare table + distinct messages through the H(m) cache)."""
+        b = ctypes.c_uint64()
+        _check(self.lib.hipbls_queue_keyed_batches(ctypes.byref(b)), self.lib)
+        return b.value
 
     def queue_stats(self) -> Tuple[int, int]:
         b, i = ctypes.c_uint64(), ctypes.c_uint64()

@@ -3,10 +3,13 @@
  *
  * C-ABI only: plain pointers and sizes, no HIP or torch types.  All buffers are owned by the
  * caller; the library never keeps a caller pointer after a call returns (cgo pointer rules).
- * Every entry point is thread-safe and binds the library's device on the calling thread (cgo goroutines move
- * between OS threads).  Calls that share a device workspace are ordered on the device even when they are issued
- * on different streams.  A HIP failure is reported as HIPBLS_ERR_DEVICE for the whole call and NEVER as a
- * per-item "verified".
+ * One process drives every GPU of the node (charon is one process per node: app/app.go:127 wires all components
+ * through the one global tbls implementation, tbls/tbls.go:11-14): the library keeps a context per device it was
+ * given (hipbls_init_devices) and splits every host-buffer batch into contiguous ranges -- whole validators /
+ * message runs -- across them, writing each range's results straight into the caller's arrays.  Every entry point
+ * is thread-safe and binds the right device on the calling thread (cgo goroutines move between OS threads).  Calls
+ * that share a device workspace are ordered on the device even when they are issued on different streams.  A HIP
+ * failure is reported as HIPBLS_ERR_DEVICE for the whole call and NEVER as a per-item "verified".
  *
  * Reference interface each entry point replaces (paths relative to the charon repository):
  *   hipbls_verify                      tbls.Implementation.Verify (one item, coalesced by the submission queue)
@@ -58,12 +61,23 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 8
+#define HIPBLS_ABI_VERSION 9
 int hipbls_abi_version(void);
 
-/* Select the HIP device used by the calling process (one process per GPU); idempotent.
- * Returns HIPBLS_OK or HIPBLS_ERR_DEVICE. */
+/* Bind the library to the n devices ids[0..n) (n <= 64; a device may repeat: each entry is one context, e.g. to
+ * test the range split on one GPU).  Host-buffer batches are split across them; each device holds its own copy of
+ * the pubshare table and its own H(m) cache and submission queue.  Idempotent for the same list; a different list
+ * after the first bind is HIPBLS_ERR_ARG.  Without any init call the first entry point binds the devices named by
+ * the environment variable HIPBLS_DEVICES ("all" or "0,1,2") or else the calling thread's current device. */
+int hipbls_init_devices(const int32_t* ids, uint32_t n);
+/* hipbls_init_devices(&device, 1); device < 0: device 0, or the existing binding. */
 int hipbls_init(int device);
+/* Number of device contexts (0 before the first bind); their device ids in ids[0..min(n, cap)). */
+int hipbls_device_slots(int32_t* ids, uint32_t cap);
+/* The split planner the batch entry points use (no GPU needed): bounds[0] = 0 <= ... <= bounds[parts] = n, equal
+ * shares; with run_keys (e.g. each item's message index) an inner bound moves forward to the next change of key, by
+ * at most half a share, so a validator's partials stay on one device. */
+int hipbls_plan_ranges(uint64_t n, uint32_t parts, const uint32_t* run_keys, uint64_t* bounds);
 /* Number of visible HIP devices (0 when none). */
 int hipbls_device_count(void);
 /* Thread-local text of the last HIPBLS_ERR_DEVICE / HIPBLS_ERR_ARG. */
@@ -91,9 +105,14 @@ int hipbls_verify(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, con
 int hipbls_verify_submit(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, const uint8_t* sig96,
                          uint64_t* ticket);
 int hipbls_verify_wait(uint64_t ticket, int32_t* status);
-/* Queue policy (defaults 65,536 items, 200 us) and counters (batches launched, items verified). */
+/* Queue policy (defaults 65,536 items, 200 us) and counters (batches launched, items verified), summed over the
+ * devices.  An item goes to the device its message hashes to, so the partials of one signing root meet in one
+ * batch.  A batch of >= 8 items whose keys are all in the resident pubshare table runs as an RLC BatchVerify with
+ * keys by index over its distinct messages, through the H(m) cache (statuses unchanged); the number of batches
+ * that took this keyed path is hipbls_queue_keyed_batches. */
 int hipbls_queue_config(uint64_t max_batch, uint32_t gather_us);
 int hipbls_queue_stats(uint64_t* batches, uint64_t* items);
+int hipbls_queue_keyed_batches(uint64_t* batches);
 
 /* ---------------------------------------------------------------- batched, host buffers ---- */
 
@@ -199,7 +218,8 @@ int hipbls_hcache_stats(uint64_t* hits, uint64_t* misses, uint64_t* entries);
 
 /* ------------------------------------------- device-resident variants (inputs already in HBM) ---- */
 /* Same semantics; every pointer is a device pointer; work is enqueued on `stream` (a hipStream_t,
- * NULL = the library's stream) and the call returns without synchronizing. */
+ * NULL = the library's stream of that device) and the call returns without synchronizing.  The call runs on the
+ * device that owns the status array. */
 int hipbls_verify_batch_device(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
                                const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream);
 /* n_parts = group_offsets[n_groups], passed explicitly so the call never reads device memory. */

@@ -37,7 +37,7 @@ def test_ctypes_mirror_declares_header_set():
     from charon_amd import tbls
     assert sorted(tbls.exported_symbols()) == header_functions()
     lib = tbls.load_library()
-    assert lib.hipbls_abi_version() == 8
+    assert lib.hipbls_abi_version() == 9
 
 
 def test_no_cpu_fallback_without_library(tmp_path):
@@ -58,3 +58,44 @@ def test_product_never_imports_oracle():
             if f.endswith((".py", ".h", ".hip", ".cpp")):
                 src = open(os.path.join(dirpath, f), errors="replace").read()
                 assert "oracle" not in re.findall(r"(?:import|from|#include)\s+[\"<]?([a-z_./]+)", src), f
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libhipbls.so not built (run __graft_entry__.build())")
+def test_plan_ranges_tiles_exactly():
+    """hipbls_plan_ranges (the batch split across devices, host code): ranges tile [0, n) in order, are balanced,
+    and with run keys (a validator's message index) no run straddles two ranges unless it is longer than half a
+    share (then the bound stays at the equal split)."""
+    import random
+    from charon_amd.tbls import plan_ranges
+    rng = random.Random(3)
+    for n in (0, 1, 7, 64, 1000, 1048576, 262144 * 4 + 128):
+        for parts in (1, 2, 3, 8):
+            b = plan_ranges(n, parts)
+            assert b[0] == 0 and b[-1] == n and all(b[i] <= b[i + 1] for i in range(parts))
+            if n >= parts:
+                sizes = [b[i + 1] - b[i] for i in range(parts)]
+                assert max(sizes) - min(sizes) <= 1
+    for trial in range(40):
+        n = rng.randrange(1, 5000)
+        runs = []
+        while sum(runs) < n:
+            runs.append(rng.choice([1, 4, 4, 7, 10, 600]))
+        keys = []
+        for k, r in enumerate(runs):
+            keys += [k] * r
+        keys = keys[:n]
+        parts = rng.choice([2, 3, 4, 8])
+        b = plan_ranges(n, parts, keys)
+        assert b[0] == 0 and b[-1] == n and all(b[i] <= b[i + 1] for i in range(parts))
+        share = n // parts
+        for k in range(1, parts):
+            x = n * k // parts
+            y = b[k]
+            if y in (0, n) or keys[y] != keys[y - 1]:
+                assert x <= y <= x + share // 2 or y == n or y == x, (x, y)
+            else:  # the run is longer than the window: the bound stays at the equal split
+                assert y == max(x, b[k - 1])
+        # C4 shape: 4 partials per validator -> every inner bound starts a validator
+        keys4 = [i // 4 for i in range(4 * 1000)]
+        b4 = plan_ranges(4000, 8, keys4)
+        assert all(x % 4 == 0 for x in b4)

@@ -1,0 +1,177 @@
+"""GPU tests added in round 3 (VERDICT r02 "Next round" 6 and 8).
+
+* The submission queue serves the drop-in tbls.Verify from the resident tables: n = 1 calls from
+  64 threads over committee-shaped items (t partials per signing root) return the batch call's statuses, the keys
+  are looked up in the pubshare table instead of being decoded and subgroup-checked per call
+  (/root/reference/tbls/herumi.go:286-289), and every distinct root is hashed to G2 exactly once across all batches
+  (the H(m) cache).
+* The reference's own cross-implementation harness (/root/reference/tbls/tbls_test.go:210-346, `randomizedImpl`,
+  `TestRandomized`, `FuzzRandomImplementations`): each call of the TestSuite (tbls_test.go:33-168) goes to an
+  implementation picked at random -- here the GPU engine or the oracle restatement -- so keys, shares, partial and
+  aggregate signatures made by one are consumed by the other.
+"""
+import random
+import threading
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+@pytest.fixture(scope="module")
+def impl():
+    from charon_amd.tbls import HipBLS
+    return HipBLS()
+
+
+# ---------------------------------------------------------------- queue from the resident tables (§8f.2)
+def test_queue_keyed_committee_one_hash_per_root(impl):
+    rng = random.Random(0x51)
+    nkeys, t, n_roots = 96, 4, 128
+    sks = [rng.randrange(1, R_ORDER).to_bytes(32, "big") for _ in range(nkeys)]
+    pks, _ = impl.secret_to_public_key_batch(sks)
+    roots = [rng.randbytes(32) for _ in range(n_roots)]
+    owner = [rng.randrange(nkeys) for _ in range(n_roots * t)]
+    msgs = [roots[i // t] for i in range(n_roots * t)]
+    sigs, _ = impl.sign_batch([sks[o] for o in owner], msgs)
+    sigs, pk_list = list(sigs), [pks[o] for o in owner]
+    for i in range(0, len(sigs), 37):  # corrupted partials: wrong root, other key, broken encoding
+        if i % 3 == 0:
+            msgs[i] = rng.randbytes(32)
+        elif i % 3 == 1:
+            pk_list[i] = pks[(owner[i] + 1) % nkeys]
+        else:
+            b = bytearray(sigs[i])
+            b[0] &= 0x7F
+            sigs[i] = bytes(b)
+    want = impl.batch_verify_status(pk_list, msgs, sigs)
+    assert want.count(0) < len(want) and want.count(0) > len(want) // 2
+    assert set(impl.load_pubshares(pks)) == {0}
+    impl.hcache_config(4096)
+    impl.queue_config(65536, 1000)
+    try:
+        h0, m0, _ = impl.hcache_stats()
+        k0 = impl.queue_keyed_batches()
+        b0, _ = impl.queue_stats()
+        got = [None] * len(msgs)
+
+        def worker(th):
+            for i in range(th, len(msgs), 64):
+                got[i] = impl.verify_queued(pk_list[i], msgs[i], sigs[i])
+
+        ths = [threading.Thread(target=worker, args=(k,)) for k in range(64)]
+        for x in ths:
+            x.start()
+        for x in ths:
+            x.join()
+        assert got == want
+        h1, m1, _ = impl.hcache_stats()
+        k1 = impl.queue_keyed_batches()
+        b1, _ = impl.queue_stats()
+        assert k1 - k0 == b1 - b0 > 0  # every batch ran keyed (all keys are in the table, the cache is on)
+        assert m1 - m0 == len(set(msgs))  # one hash per distinct root across all batches
+        assert h1 - h0 >= 0
+        # a second pass over the same roots hashes nothing
+        got2 = [impl.verify_queued(pk_list[i], msgs[i], sigs[i]) for i in range(0, len(msgs), 17)]
+        assert got2 == want[::17]
+        assert impl.hcache_stats()[1] == m1
+    finally:
+        impl.hcache_config(0)
+        impl.queue_config(65536, 200)
+
+
+# ---------------------------------------------------------------- randomizedImpl (tbls_test.go:210-346)
+class TBLSErr(Exception):
+    """The error of either implementation, by message (the callers only see the text)."""
+
+
+class OracleImpl:
+    """The oracle (oracle/bls12381.py) behind the same method names as charon_amd.tbls.HipBLS."""
+
+    def __init__(self, rng):
+        from oracle import bls12381 as bls
+        self.bls, self.rng = bls, rng
+
+    def generate_secret_key(self):
+        return self.rng.randrange(1, R_ORDER).to_bytes(32, "big")
+
+    def secret_to_public_key(self, sk):
+        return self.bls.secret_to_public_key(sk)
+
+    def threshold_split(self, secret, total, threshold):
+        tail = [self.rng.randrange(R_ORDER) for _ in range(threshold - 1)]
+        return self.bls.threshold_split_poly(int.from_bytes(secret, "big"), tail, total)
+
+    def recover_secret(self, shares, total, threshold):
+        return self.bls.recover_secret(dict(shares))
+
+    def threshold_aggregate(self, parts):
+        return self.bls.threshold_aggregate(dict(parts))
+
+    def verify(self, pk, data, sig):
+        self.bls.verify(pk, data, sig)
+
+    def sign(self, sk, data):
+        return self.bls.sign(sk, data)
+
+    def verify_aggregate(self, shares, sig, data):
+        self.bls.verify_aggregate(list(shares), sig, data)
+
+    def aggregate(self, sigs):
+        return self.bls.aggregate(list(sigs))
+
+
+class RandomizedImpl:
+    """randomizedImpl: every method call picks one of the implementations at random (seeded here)."""
+
+    def __init__(self, impls, rng):
+        self.impls, self.rng, self.picks = impls, rng, []
+
+    def __getattr__(self, name):
+        def call(*a):
+            from charon_amd.tbls import TBLSError
+            k = self.rng.randrange(len(self.impls))
+            self.picks.append((name, k))
+            try:
+                return getattr(self.impls[k], name)(*a)
+            except (TBLSError, self.impls[1].bls.BLSError) as e:
+                raise TBLSErr(str(e)) from e
+        return call
+
+
+def _suite(ts):
+    """TestSuite (tbls_test.go:33-168), one pass."""
+    data = b"hello obol!"
+    secret = ts.generate_secret_key()
+    assert len(secret) == 32
+    pub = ts.secret_to_public_key(secret)
+    assert len(pub) == 48
+    shares = ts.threshold_split(secret, 5, 3)
+    assert sorted(shares) == [1, 2, 3, 4, 5]
+    assert ts.recover_secret(shares, 5, 3) == secret
+    total_og = ts.sign(secret, data)
+    sigs = {idx: ts.sign(key, data) for idx, key in shares.items()}
+    assert ts.threshold_aggregate(sigs) == total_og
+    three = dict(list(sigs.items())[:3])
+    assert ts.threshold_aggregate(three) == total_og  # any t of the n partials
+    ts.verify(pub, data, total_og)
+    with pytest.raises(TBLSErr, match="^signature not verified$"):
+        ts.verify(pub, data + b"?", total_og)
+    keys = [ts.generate_secret_key() for _ in range(10)]
+    pubs = [ts.secret_to_public_key(k) for k in keys]
+    signs = [ts.sign(k, data) for k in keys]
+    agg = ts.aggregate(signs)
+    ts.verify_aggregate(pubs, agg, data)
+    with pytest.raises(TBLSErr, match="^signature verification failed$"):
+        ts.verify_aggregate(pubs[:9], agg, data)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_randomized_engine_and_oracle(impl, seed):
+    rng = random.Random(seed)
+    r = RandomizedImpl([impl, OracleImpl(rng)], rng)
+    _suite(r)
+    used = {k for _, k in r.picks}
+    assert used == {0, 1}, r.picks  # both implementations took part
