@@ -133,7 +133,7 @@ struct Context {
   uint64_t r_windows = 0;        // window count of this context's last RLC call (hipbls_rlc_stats)
   uint64_t r_call = 0;           // entry-point call that call belonged to
   // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
-  DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_FS, m_flag;
+  DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_flag;
   // Verdicts come back through a ring of pinned slots, one per batch check in flight, so a launch only waits
   // on the host when kRlcbSlots checks are still unread (never in the enqueue-only *_device paths otherwise).
   static constexpr int kRlcbSlots = 8;
@@ -681,18 +681,19 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   HIP_TRY(c.m_B.ensure((uint64_t)MSM_WINDOWS * MSM_NB * 72 * 4));
   HIP_TRY(c.m_Sg.ensure((uint64_t)MSM_WINDOWS * MSM_NSEG * 72 * 4));
   HIP_TRY(c.m_W.ensure((uint64_t)MSM_WINDOWS * 72 * 4));
-  HIP_TRY(c.m_F.ensure(nch * 144 * 4));
-  HIP_TRY(c.m_F2.ensure(((nch + 15) / 16) * 144 * 4));
-  HIP_TRY(c.m_FS.ensure(144 * 4));
+  HIP_TRY(c.m_F.ensure((nch + 1) * 144 * 4));
+  HIP_TRY(c.m_F2.ensure(((nch + RLCB_FAN) / RLCB_FAN) * 144 * 4));
   HIP_TRY(c.m_flag.ensure(4));
   uint32_t* rpk = (uint32_t*)c.r_pk.p;
   uint32_t* rsig = (uint32_t*)c.r_sig.p;
   uint32_t* pts = (uint32_t*)c.m_pts.p;
   uint32_t* sc = (uint32_t*)c.m_sc.p;
   int32_t* flag = (int32_t*)c.m_flag.p;
-  // Streams: the caller's stream s hashes the messages; sub[0] runs items -> MSM -> the (-g1, S) Miller value;
-  // sub[1] runs the chunk Miller loops and their product once the items and the hash are done; s joins both for
-  // the verdict and the window stages.
+  // Streams: the caller's stream s hashes the messages while sub[0] runs the items and then the MSM's short
+  // kernels; sub[1] runs the chunk Miller loops (plus the (-g1, S) lane) and their product once the MSM and the
+  // hash are done -- after the MSM, because the chunk kernel holds every SIMD for its whole run and a short kernel
+  // queued behind it waits that long (round 2: k_msm_scan 33 ms beside k_rlcb_chunks 37.7 ms).  s joins for the
+  // verdict and the window stages.
   hipStream_t s0 = c.sub[0], s1 = c.sub[1];
   rc = ws_begin(c, s);
   if (rc) return rc;
@@ -731,26 +732,23 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
                        (uint32_t*)c.m_W.p);
   });
   if (rc) return rc;
-  rc = timed(c, "rlcb_sfactor", s0, [&] {
-    hipLaunchKernelGGL(k_rlcb_sfactor, dim3(1), dim3(kBlock), 0, s0, (const uint32_t*)c.m_W.p, (uint32_t*)c.m_FS.p);
-  });
-  if (rc) return rc;
   HIP_TRY(hipEventRecord(c.rlcb_ev_msm, s0));
-  HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_items, 0));
+  HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_msm, 0));
   HIP_TRY(hipStreamWaitEvent(s1, c.ev_hash, 0));
   rc = timed(c, "rlcb_chunks", s1, [&] {
-    hipLaunchKernelGGL(k_rlcb_chunks, dim3((unsigned)grid_for(nch)), dim3(kBlock), 0, s1, n, (const int32_t*)d_status,
-                       d_midx, (const uint32_t*)rpk, (const uint32_t*)d_H, hstride, d_hslot, (uint32_t*)c.m_F.p, nch);
+    hipLaunchKernelGGL(k_rlcb_chunks, dim3((unsigned)grid_for(nch + 1)), dim3(kBlock), 0, s1, n,
+                       (const int32_t*)d_status, d_midx, (const uint32_t*)rpk, (const uint32_t*)d_H, hstride, d_hslot,
+                       (uint32_t*)c.m_F.p, nch, (const uint32_t*)c.m_W.p);
   });
   if (rc) return rc;
   uint32_t* src = (uint32_t*)c.m_F.p;
   uint32_t* dst = (uint32_t*)c.m_F2.p;
-  uint64_t cur = nch;
+  uint64_t cur = nch + 1;
   rc = timed(c, "rlcb_product", s1, [&] {
     while (cur > 1) {
-      const uint64_t nxt = (cur + 15) / 16;
+      const uint64_t nxt = (cur + RLCB_FAN - 1) / RLCB_FAN;
       hipLaunchKernelGGL(k_fp12_prod, dim3((unsigned)grid_for(nxt)), dim3(kBlock), 0, s1, (const uint32_t*)src, cur,
-                         dst, nxt, 16);
+                         dst, nxt, RLCB_FAN);
       uint32_t* t = src;
       src = dst;
       dst = t;
@@ -759,10 +757,9 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));
-  HIP_TRY(hipStreamWaitEvent(s, c.rlcb_ev_msm, 0));
   HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
   rc = timed(c, "rlcb_final", s, [&] {
-    hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, (const uint32_t*)c.m_FS.p, flag);
+    hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, flag);
   });
   if (rc) return rc;
   rc = timed(c, "rlcb_mark", s, [&] {
@@ -1200,8 +1197,16 @@ int run_batch(Context& c, VBatch& b) {
     std::lock_guard<std::mutex> lk(c.mu);
     // small batches take the lower-latency lane-pair Verify, unless the caller enabled the H(m) cache
     bool keyed = c.t_size > 0 && (n >= kQueueKeyedMin || c.hcache.cap > 0);
-    for (uint64_t i = 0; keyed && i < n; ++i)
+    uint64_t miss_at = n;
+    for (uint64_t i = 0; keyed && i < n; ++i) {
       keyed = c.t_index.count(std::string((const char*)b.pk.data() + 48 * i, 48)) != 0;
+      if (!keyed) miss_at = i;
+    }
+    static const bool dbg = getenv("HIPBLS_DEBUG_QUEUE") != nullptr;
+    if (dbg)
+      fprintf(stderr, "[hipbls queue] ctx %d batch n=%llu keyed=%d t_size=%llu cap=%llu miss_at=%llu\n", c.slot,
+              (unsigned long long)n, (int)keyed, (unsigned long long)c.t_size, (unsigned long long)c.hcache.cap,
+              (unsigned long long)miss_at);
     if (keyed) {
       c.q.keyed += 1;
       return run_batch_keyed(c, b);
@@ -1539,6 +1544,32 @@ int table_load_host(Context& c, const uint8_t* pks, uint64_t n, int32_t* status)
   return HIPBLS_OK;
 }
 
+// herumi's Deserialize of n points (kind 1: 48-byte G1 public keys, kind 2: 96-byte G2 signatures): decode, on-curve
+// and subgroup checks; status[i] = OK, or ERR_PUBKEY / ERR_SIGNATURE.
+int deserialize_host(Context& c, const uint8_t* data, uint64_t n, int kind, int32_t* status) {
+  const uint64_t w = kind == 1 ? 48 : 96;
+  HIP_TRY(c.b_sig.ensure(n * w));
+  HIP_TRY(c.b_pts.ensure(n * (w / 2) * 4));
+  HIP_TRY(c.b_pst.ensure(n * 4));
+  HIP_TRY(hipMemcpyAsync(c.b_sig.p, data, n * w, hipMemcpyHostToDevice, c.stream));
+  int rc = ws_begin(c, c.stream);
+  if (rc) return rc;
+  if (kind == 1)
+    hipLaunchKernelGGL(k_g1_decode, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_sig.p,
+                       n, (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);
+  else
+    hipLaunchKernelGGL(k_g2_decode, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, c.stream, (const uint8_t*)c.b_sig.p,
+                       n, (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);
+  HIP_TRY(hipGetLastError());
+  rc = ws_end(c, c.stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(status, c.b_pst.p, n * 4, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  const int32_t bad = kind == 1 ? HIPBLS_ERR_PUBKEY : HIPBLS_ERR_SIGNATURE;
+  for (uint64_t i = 0; i < n; ++i) status[i] = status[i] == DEC_BAD ? bad : HIPBLS_OK;
+  return HIPBLS_OK;
+}
+
 // Minimum units per range before a batch is split across devices (each range must still fill a GPU's SIMDs for a
 // while; below this the call stays on one device and concurrent calls spread round robin).
 constexpr uint64_t kSplitVerify = 4096;   // Verify items
@@ -1709,6 +1740,16 @@ int hipbls_queue_stats(uint64_t* batches, uint64_t* items) {
     *items += q.items;
   }
   return HIPBLS_OK;
+}
+
+int hipbls_deserialize_status(const uint8_t* data, uint64_t n, int32_t kind, int32_t* status) {
+  if (n == 0) return HIPBLS_OK;
+  if (!data || !status || (kind != 1 && kind != 2) || mul_overflows(n, 192)) return arg_err("bad deserialize arguments");
+  ENSURE_INIT();
+  const uint64_t w = kind == 1 ? 48 : 96;
+  return run_ranges(plan_ranges(n, parts_for(n, kSplitSign), nullptr), [&](Context& c, uint64_t lo, uint64_t hi) {
+    return deserialize_host(c, data + w * lo, hi - lo, kind, status + lo);
+  });
 }
 
 int hipbls_queue_keyed_batches(uint64_t* batches) {

@@ -824,14 +824,21 @@ __global__ void __launch_bounds__(kSumBlock) k_msm_window(const uint32_t* __rest
     for (int k = 0; k < 72; ++k) W[72 * w + k] = (&acc.x.c0.v[0])[k];
 }
 
+// Stage 3: lanes [0, n_chunks) are the chunks; lane n_chunks (the last workgroup's first free lane) forms S from the
+// MSM window sums and stores the Miller value of (-g1, S) as column n_chunks, so the product tree multiplies it in
+// and the verdict kernel only exponentiates.  F has n_chunks + 1 columns.  Launched after the MSM, so the MSM's
+// small kernels never wait for SIMDs this kernel holds (profiles/r02_kernel_stats.csv: k_msm_scan 33 ms).
 __global__ void __launch_bounds__(kBlock) k_rlcb_chunks(uint64_t n, const int32_t* __restrict__ status,
                                                         const uint32_t* __restrict__ msg_idx,
                                                         const uint32_t* __restrict__ rpk,
                                                         const uint32_t* __restrict__ H, uint64_t hstride,
                                                         const uint32_t* __restrict__ hslot, uint32_t* __restrict__ F,
-                                                        uint64_t n_chunks) {
+                                                        uint64_t n_chunks, const uint32_t* __restrict__ W) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (c < n_chunks) rlcb_chunk_lane(c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks);
+  if (c < n_chunks)
+    rlcb_chunk_lane(c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks + 1);
+  else if (c == n_chunks)
+    rlcb_sfactor_lane(W, F, n_chunks + 1, n_chunks);
 }
 
 __global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict__ Fin, uint64_t nin,
@@ -840,38 +847,17 @@ __global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict
   if (g < nout) fp12_prod_lane(g, Fin, nin, Fout, nout, fan);
 }
 
-// The Miller value of (-g1, S), S = W0 + [2^16] W1 (one lane; runs beside the chunk stage on its own stream).
-__global__ void __launch_bounds__(kBlock) k_rlcb_sfactor(const uint32_t* __restrict__ W, uint32_t* __restrict__ FS) {
-  if (threadIdx.x != 0) return;
-  g2j W0, W1, S;
-  for (int k = 0; k < 72; ++k) {
-    (&W0.x.c0.v[0])[k] = W[k];
-    (&W1.x.c0.v[0])[k] = W[72 + k];
-  }
-  msm_combine(S, W0, W1);
-  fp12 f;
-  if (jac_is_inf(S)) {
-    fp12_set_one(f);
-  } else {
-    g1a P[1];
-    g2a Q[1];
-    P[0].x = G1_GEN_X;
-    P[0].y = G1_NEG_GEN_Y;
-    jac_to_aff(Q[0], S);
-    miller_loop_multi<1>(f, P, Q, 1);
-  }
-  soa_store<144>(FS, 1, 0, &f.c0.c0.c0.v[0]);
-}
-
-// The verdict, on lanes 0 and 1 as a pair (lg2.h): lane 0 holds the Miller value of (-g1, S), lane 1 the product of
-// the chunks' Miller values; split final exponentiation; flag[0] = 1 when the product is 1.
-__global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restrict__ Ftot,
-                                                       const uint32_t* __restrict__ FS, int32_t* __restrict__ flag) {
+// The verdict, on lanes 0 and 1 as a pair (lg2.h): lane 1 holds the product of all Miller values (the chunks' and
+// (-g1, S)'s), lane 0 the identity; split final exponentiation; flag[0] = 1 when the product is 1.
+__global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restrict__ Ftot, int32_t* __restrict__ flag) {
   const int t = threadIdx.x;
   if (t >= 2) return;
   const uint32_t m = t ? ~0u : 0u;
   fp12 f;
-  soa_load<144>(&f.c0.c0.c0.v[0], t ? Ftot : FS, 1, 0);
+  if (t)
+    soa_load<144>(&f.c0.c0.c0.v[0], Ftot, 1, 0);
+  else
+    fp12_set_one(f);
   const bool ok = lg2_finish(f, m);
   if (t == 0) flag[0] = ok ? 1 : 0;
 }

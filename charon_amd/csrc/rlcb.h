@@ -16,10 +16,11 @@
 //                 per 16-bucket segment folds sum_j j B_j by running sums, two workgroups tree-sum the
 //                 segments in LDS, and S = W0 + [2^16] W1;
 //   3. chunks   : one lane per 16 consecutive items: runs of equal message among pending items are summed in G1
-//                 and paired with H(m) in one multi-Miller loop (no final exponentiation) -> f_chunk;
-//   4. product  : the chunks' Miller values multiplied together (fan-in 16 per level);
-//   5. final    : a lane pair multiplies in the Miller value of (-g1, S) and runs the split final
-//                 exponentiation (lg2.h); the verdict goes to a device flag;
+//                 and paired with H(m) in one multi-Miller loop (no final exponentiation) -> f_chunk; one more
+//                 lane forms S from the window sums and computes the Miller value of (-g1, S) as the last column;
+//   4. product  : the chunks' Miller values multiplied together (fan-in RLCB_FAN per level);
+//   5. final    : a lane pair runs the split final exponentiation of the product (lg2.h); the verdict goes to
+//                 a device flag;
 //   6. mark     : pass -> every pending item is valid; fail -> each pending item gets [r_i] sig_i for the window
 //                 stages of rlc.h, which then decide item by item.
 // Soundness is the windows' argument over the whole batch: a batch with an invalid item passes with
@@ -35,6 +36,9 @@ constexpr int MSM_WINDOWS = 2;                 // 32-bit scalars
 constexpr uint32_t MSM_NB = 1u << MSM_BITS;    // buckets per window (bucket 0 unused)
 constexpr int MSM_SEG = 16;                    // buckets folded per segment lane
 constexpr uint32_t MSM_NSEG = MSM_NB / MSM_SEG;
+// Fan-in of the Miller-value product tree: a level costs `fan` serial Fp12 products, so f * log_f(chunks) products
+// of latency in all -- 32 at fan 4 for 65,536 chunks, 64 at fan 16.
+constexpr int RLCB_FAN = 4;
 
 #if defined(__HIP_DEVICE_COMPILE__)
 #define BLS_ATOMIC_ADD_U32(p, v) atomicAdd((p), (v))
@@ -221,6 +225,29 @@ BLS_HD BLS_INLINE void rlcb_chunk_lane(uint64_t c, uint64_t n, const int32_t* st
   else
     fp12_set_one(f);
   soa_store<144>(F, n_chunks, c, &f.c0.c0.c0.v[0]);
+}
+
+// The S lane of stage 3: S = W0 + [2^16] W1 from the window sums (W: 2 x 72 words, contiguous), then the Miller
+// value of (-g1, S) (1 when S is the point at infinity) into column `col` of F.
+BLS_HD BLS_INLINE void rlcb_sfactor_lane(const uint32_t* W, uint32_t* F, uint64_t stride, uint64_t col) {
+  g2j W0, W1, S;
+  for (int k = 0; k < 72; ++k) {
+    (&W0.x.c0.v[0])[k] = W[k];
+    (&W1.x.c0.v[0])[k] = W[72 + k];
+  }
+  msm_combine(S, W0, W1);
+  fp12 f;
+  if (jac_is_inf(S)) {
+    fp12_set_one(f);
+  } else {
+    g1a P[1];
+    g2a Q[1];
+    P[0].x = G1_GEN_X;
+    P[0].y = G1_NEG_GEN_Y;
+    jac_to_aff(Q[0], S);
+    miller_loop_multi<1>(f, P, Q, 1);
+  }
+  soa_store<144>(F, stride, col, &f.c0.c0.c0.v[0]);
 }
 
 // ---- stage 4: product of Miller values, fan-in `fan` ----------------------------------------------------

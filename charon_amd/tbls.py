@@ -67,6 +67,7 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_device_slots": ([ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32], ctypes.c_int),
         "hipbls_plan_ranges": ([u64, ctypes.c_uint32, u32p, u64p], ctypes.c_int),
         "hipbls_queue_keyed_batches": ([u64p], ctypes.c_int),
+        "hipbls_deserialize_status": ([u8p, u64, ctypes.c_int32, i32p], ctypes.c_int),
         "hipbls_set_timing": ([ctypes.c_int], ctypes.c_int),
         "hipbls_set_pair_mode": ([ctypes.c_int], ctypes.c_int),
         "hipbls_rlc_set_mode": ([ctypes.c_int], ctypes.c_int),
@@ -139,7 +140,7 @@ def exported_symbols() -> List[str]:
         "hipbls_hcache_config", "hipbls_hcache_stats", "hipbls_set_pair_mode",
         "hipbls_rlc_set_mode", "hipbls_rlc_batch_stats", "hipbls_threshold_aggregate_verify_batch",
         "hipbls_threshold_aggregate_verify_batch_device", "hipbls_init_devices", "hipbls_device_slots",
-        "hipbls_plan_ranges", "hipbls_queue_keyed_batches",
+        "hipbls_plan_ranges", "hipbls_queue_keyed_batches", "hipbls_deserialize_status",
     ]
 
 
@@ -525,6 +526,14 @@ class HipBLS:
         if st[0] != OK:
             raise DeviceError("unexpected aggregate status %d" % st[0])
         return out.raw
+
+    def deserialize_status(self, points: Sequence[bytes], kind: int) -> List[int]:
+        """herumi Deserialize per point: kind 1 = public keys (OK / ERR_PUBKEY), 2 = signatures (OK / ERR_SIGNATURE)."""
+        size = 48 if kind == 1 else 96
+        _check_lengths("points", points, size)
+        st = _status_array(len(points))
+        _check(self.lib.hipbls_deserialize_status(b"".join(points), len(points), kind, st), self.lib)
+        return list(st)[:len(points)]
 
     # ---------------------------------------------------------------- submission queue (coalesced Verify)
     def verify_queued(self, compressed_public_key: bytes, data: bytes, signature: bytes) -> int:

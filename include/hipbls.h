@@ -156,6 +156,12 @@ int hipbls_verify_aggregate_batch(const uint8_t* pks, const uint64_t* key_offset
                                   const uint8_t* sigs, const uint8_t* msgs, const uint64_t* msg_offsets,
                                   int32_t* status);
 
+/* herumi's Deserialize of n points, one status each: kind 1 = 48-byte public keys (OK | ERR_PUBKEY), kind 2 = 96-byte
+ * signatures (OK | ERR_SIGNATURE); flags, x < p, on the curve, in the subgroup (the point at infinity deserializes).
+ * The Go binding uses it to name the failing item in Aggregate / ThresholdAggregate errors, the
+ * z.Int("signature_number", idx) field of tbls/herumi.go:229-233, 255-258. */
+int hipbls_deserialize_status(const uint8_t* data, uint64_t n, int32_t kind, int32_t* status);
+
 /* Plain G2 sum of n signatures (decoded in parallel, tree-summed).  *status = OK | ERR_SIGNATURE.  As herumi
  * (tbls/herumi.go:220-242), n == 0 is not an error: the sum is the point at infinity, 0xc0 || 0^95. */
 int hipbls_aggregate(const uint8_t* sigs, uint64_t n, uint8_t* out_sig, int32_t* status);

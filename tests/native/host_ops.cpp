@@ -345,8 +345,8 @@ extern "C" int ht_verify_key(const uint8_t* pk48, const uint8_t* msg, uint32_t l
 #include "../../charon_amd/csrc/rlcb.h"
 
 namespace {
-// Pippenger over npts affine SoA points with 32-bit scalars: the device stages run serially.
-void host_msm(g2j& S, const uint32_t* pts, const uint32_t* sc, uint64_t npts) {
+// Pippenger over npts affine SoA points with 32-bit scalars: the device stages run serially; W = the window sums.
+void host_msm(g2j* W, const uint32_t* pts, const uint32_t* sc, uint64_t npts) {
   std::vector<uint32_t> cnt(MSM_WINDOWS * MSM_NB, 0), off(MSM_WINDOWS * (MSM_NB + 1)), cur(MSM_WINDOWS * MSM_NB);
   std::vector<uint32_t> list(MSM_WINDOWS * (npts ? npts : 1));
   for (uint64_t p = 0; p < npts; ++p) msm_hist_lane(p, sc, cnt.data());
@@ -365,7 +365,6 @@ void host_msm(g2j& S, const uint32_t* pts, const uint32_t* sc, uint64_t npts) {
     for (uint32_t j = 0; j < MSM_NB; ++j) msm_bucket_lane(w, j, off.data(), list.data(), npts, pts, B.data());
   for (int w = 0; w < MSM_WINDOWS; ++w)
     for (uint32_t s = 0; s < MSM_NSEG; ++s) msm_segment_lane(w, s, B.data(), Sg.data());
-  g2j W[MSM_WINDOWS];
   for (int w = 0; w < MSM_WINDOWS; ++w) {
     jac_set_inf(W[w]);
     for (uint32_t s = 0; s < MSM_NSEG; ++s) {
@@ -374,7 +373,6 @@ void host_msm(g2j& S, const uint32_t* pts, const uint32_t* sc, uint64_t npts) {
       jac_add(W[w], W[w], t);
     }
   }
-  msm_combine(S, W[0], W[1]);
 }
 }  // namespace
 
@@ -389,8 +387,9 @@ extern "C" void ht_msm_g2(const uint8_t* pts192, const uint32_t* sc, uint64_t n,
     fp_in(a.y.c1, pts192 + 192 * i + 144);
     soa_store<48>(pts.data(), n, i, &a.x.c0.v[0]);
   }
-  g2j S;
-  host_msm(S, pts.data(), sc, n);
+  g2j W[MSM_WINDOWS], S;
+  host_msm(W, pts.data(), sc, n);
+  msm_combine(S, W[0], W[1]);
   g2_compress(out96, S);
 }
 
@@ -416,19 +415,26 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
   mark(0);
   for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, H.data(), n_msgs, nullptr);
   mark(1);
-  g2j S;
-  host_msm(S, pts.data(), sc.data(), 2 * n);
+  g2j W[MSM_WINDOWS];
+  host_msm(W, pts.data(), sc.data(), 2 * n);
+  std::vector<uint32_t> Wc(2 * 72);
+  for (int k = 0; k < 72; ++k) {
+    Wc[k] = (&W[0].x.c0.v[0])[k];
+    Wc[72 + k] = (&W[1].x.c0.v[0])[k];
+  }
   mark(2);
+  // stage 3 as the device runs it: the chunks, then the (-g1, S) lane as the last column
   const uint64_t nch = (n + RLCB_C - 1) / RLCB_C;
-  std::vector<uint32_t> F(144 * (nch ? nch : 1));
+  std::vector<uint32_t> F(144 * (nch + 1));
   for (uint64_t c = 0; c < nch; ++c)
-    rlcb_chunk_lane(c, n, status, msg_idx, rpk.data(), H.data(), n_msgs, nullptr, F.data(), nch);
-  mark(3);
-  uint64_t cur = nch;
+    rlcb_chunk_lane(c, n, status, msg_idx, rpk.data(), H.data(), n_msgs, nullptr, F.data(), nch + 1);
+  mark(3);  // the (-g1, S) lane is counted with the product and the verdict (stage 4 of counts6)
+  rlcb_sfactor_lane(Wc.data(), F.data(), nch + 1, nch);
+  uint64_t cur = nch + 1;
   while (cur > 1) {
-    const uint64_t nxt = (cur + 15) / 16;
+    const uint64_t nxt = (cur + RLCB_FAN - 1) / RLCB_FAN;
     std::vector<uint32_t> G(144 * nxt);
-    for (uint64_t g = 0; g < nxt; ++g) fp12_prod_lane(g, F.data(), cur, G.data(), nxt, 16);
+    for (uint64_t g = 0; g < nxt; ++g) fp12_prod_lane(g, F.data(), cur, G.data(), nxt, RLCB_FAN);
     F.swap(G);
     cur = nxt;
   }
@@ -437,21 +443,7 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
   bool pass = true;
   if (any) {
     fp12 f;
-    if (nch)
-      soa_load<144>(&f.c0.c0.c0.v[0], F.data(), 1, 0);
-    else
-      fp12_set_one(f);
-    if (!jac_is_inf(S)) {
-      g1a P[1];
-      g2a Q[1];
-      P[0].x = G1_GEN_X;
-      P[0].y = G1_NEG_GEN_Y;
-      jac_to_aff(Q[0], S);
-      fp12 g;
-      miller_loop_multi<1>(g, P, Q, 1);
-      fp12 x = f;
-      fp12_mul(f, x, g);
-    }
+    soa_load<144>(&f.c0.c0.c0.v[0], F.data(), 1, 0);
     fp12 e;
     final_exponentiation(e, f);
     pass = fp12_is_one(e);

@@ -175,3 +175,29 @@ def test_randomized_engine_and_oracle(impl, seed):
     _suite(r)
     used = {k for _, k in r.picks}
     assert used == {0, 1}, r.picks  # both implementations took part
+
+
+# ---------------------------------------------------------------- Deserialize statuses (herumi's error fields)
+def test_deserialize_status_vs_oracle(impl):
+    """hipbls_deserialize_status (herumi PublicKey/Sign.Deserialize per item: flags, x < p, on curve, subgroup)
+    equals the oracle's decompression on every fixture key and signature, the small-order ones included.  The Go
+    binding uses it for the signature_number field of Aggregate / ThresholdAggregate errors (herumi.go:229-233)."""
+    import json
+    import os
+    from oracle import bls12381 as bls
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fixtures.json")) as f:
+        fx = json.load(f)
+    cases = fx["verify"] + fx["small_order"]["verify"]
+    pks = list(dict.fromkeys(bytes.fromhex(c["pk"]) for c in cases))
+    sigs = list(dict.fromkeys(bytes.fromhex(c["sig"]) for c in cases))
+
+    def ok(fn, b):
+        try:
+            fn(b)
+            return True
+        except bls.BLSError:
+            return False
+
+    assert impl.deserialize_status(pks, 1) == [0 if ok(bls.g1_decompress, p) else 1 for p in pks]
+    assert impl.deserialize_status(sigs, 2) == [0 if ok(bls.g2_decompress, s) else 2 for s in sigs]
+    assert 1 in impl.deserialize_status(pks, 1) and 2 in impl.deserialize_status(sigs, 2)
