@@ -425,6 +425,7 @@ def main():
     # ---- C3: threshold aggregation + Verify of each aggregate; node batch = groups x world validators, this rank's
     # slice; the 96-byte aggregates and the verify bitmap are all-gathered inside the timed step
     tagg = None
+    tagg_kms = {}
     if args.tagg_groups > 0:
         t0 = time.time()
         G_node = args.tagg_groups * world
@@ -452,7 +453,10 @@ def main():
                 node_aggs[1] = gather_node_bitmap(d_vst, G_node)
 
         tstep()
+        torch.cuda.synchronize(dev)
+        lib.hipbls_kernel_timing_reset()
         tel = timed_loop(tstep, args.tagg_steps, dev, barrier, world)
+        tagg_kms = kernel_ms(lib, ("tagg_scale", "tagg_sum", "tv_prep_pk", "verify_pair_lg2", "verify_pair_single"))
         assert set(d_gst.cpu().tolist()) == {0} and set(d_vst.cpu().tolist()) == {0}, "aggregate mismatch"
         if world > 1:
             assert torch.equal(node_aggs[0][96 * g_lo:96 * g_hi], d_agg), "gathered aggregates differ from local"
@@ -647,6 +651,7 @@ def main():
             "pairings_per_s": round(2 * value, 1),
             "verified_partial_sigs_per_s_pubshare_table": round(keys_rate, 1) if keys_rate else None,
             "threshold_aggregates_per_s": round(tagg, 1) if tagg else None,
+            "threshold_aggregate_kernel_avg_ms": tagg_kms or None,
             "threshold_aggregate_workload": "C3: %d validators per GPU x 7-of-10 Lagrange in G2 + Verify of each "
                                             "aggregate (hipbls_threshold_aggregate_verify_batch_device, sigagg in one "
                                             "call); aggregates and bitmap all-gathered" % args.tagg_groups

@@ -22,17 +22,19 @@ def stale(lib=LIB):
     return any(os.path.getmtime(s) > t for s in _sources())
 
 
-def build(force=False, verbose=True, extra=()):
-    if not force and not stale():
+def build(force=False, verbose=True, extra=(), out=LIB):
+    """Build the library; `extra` adds compiler flags (e.g. -D variants) and `out` names another file for A/B
+    measurements (loaded with HIPBLS_LIB=<path>); the product is the default in-tree build."""
+    if not force and out == LIB and not stale():
         return LIB
     cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-I" + CSRC, "-I" + os.path.join(ROOT, "include"),
-           "-o", LIB + ".tmp", os.path.join(CSRC, "hipbls.hip")] + list(extra)
+           "-o", out + ".tmp", os.path.join(CSRC, "hipbls.hip")] + list(extra)
     if verbose:
         print("[hipbls] " + " ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -823,7 +823,7 @@ int launch_tagg(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, const u
   }
   rc = timed(c, "tagg_sum", s, [&] {
     hipLaunchKernelGGL(k_tagg_sum, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s, (const uint32_t*)c.b_pts.p,
-                       (const int32_t*)c.b_pst.p, d_goffs, n_groups, n_parts, d_out, d_status);
+                       (const int32_t*)c.b_pst.p, d_ids, d_goffs, n_groups, n_parts, d_out, d_status);
   });
   if (rc) return rc;
   return ws_end(c, s);
@@ -858,14 +858,21 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
   }
   rc = timed(c, "tagg_sum", s0, [&] {
     hipLaunchKernelGGL(k_tagg_sum_v, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s0,
-                       (const uint32_t*)c.b_pts.p, (const int32_t*)c.b_pst.p, d_goffs, n_groups, n_parts, d_out,
-                       d_astatus, ws, agg_inf);
+                       (const uint32_t*)c.b_pts.p, (const int32_t*)c.b_pst.p, d_ids, d_goffs, n_groups, n_parts,
+                       d_out, d_astatus, ws, agg_inf);
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_join[0], s0));
+#ifndef BLS_TV_PAIR_HASH
+#define BLS_TV_PAIR_HASH 0
+#endif
   rc = timed(c, "tv_prep_pk", s1, [&] {
-    hipLaunchKernelGGL(k_tv_prep_pk, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s1, d_dvpks, d_msgs, d_moffs,
-                       n_groups, ws, d_vstatus);
+    if (BLS_TV_PAIR_HASH && n_groups <= kPairHashMaxVerify)
+      hipLaunchKernelGGL(k_tv_prep_pk2, dim3((unsigned)(3 * grid_for(n_groups))), dim3(kBlock), 0, s1, d_dvpks, d_msgs,
+                         d_moffs, n_groups, ws, d_vstatus);
+    else
+      hipLaunchKernelGGL(k_tv_prep_pk, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s1, d_dvpks, d_msgs,
+                         d_moffs, n_groups, ws, d_vstatus);
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));

@@ -143,7 +143,11 @@ __global__ void __launch_bounds__(kBlock) k_sk_to_pk(const uint8_t* __restrict__
 // ThresholdAggregate, stage 1: one lane per partial signature k.  Finds its group by binary search
 // over group_offsets, decodes + subgroup-checks sig_k, computes lambda_k(0) from the group's ids and
 // writes lambda_k * sig_k (Jacobian, limb-major SoA: 36 words x n_partials) plus a per-partial code.
-__global__ void __launch_bounds__(kBlock) k_tagg_scale(const uint8_t* __restrict__ sigs,
+#ifndef BLS_TAGG_WAVES
+#define BLS_TAGG_WAVES 1
+#endif
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BLS_TAGG_WAVES, BLS_TAGG_WAVES)))
+k_tagg_scale(const uint8_t* __restrict__ sigs,
                                                        const int64_t* __restrict__ ids,
                                                        const uint64_t* __restrict__ goffs, uint64_t n_groups,
                                                        uint64_t n_parts, uint32_t* __restrict__ pts,
@@ -175,20 +179,20 @@ __global__ void __launch_bounds__(kBlock) k_tagg_scale(const uint8_t* __restrict
   const int ds = g2_decompress(s, sigs + 96 * k, true);
   if (ds == DEC_BAD) st = HIPBLS_ERR_SIGNATURE;
   if (st == HIPBLS_OK && ds == DEC_OK) {
-    fr lam;
-    lagrange_at_zero(lam, ids + g0, t, me);
     g2j sj;
     jac_from_aff(sj, s);
-    g2_mul_glv4(acc, sj, lam.v);
+    tagg_scale_point(acc, sj, ids + g0, t, me);  // c_k sig_k (small ids) or lambda_k sig_k
   }
   const uint32_t* src = &acc.x.c0.v[0];
   for (int w = 0; w < 72; ++w) pts[(uint64_t)w * n_parts + k] = src[w];
   pstat[k] = st;
 }
 
-// ThresholdAggregate, stage 2: one lane per group sums its scaled partials and compresses.
+// ThresholdAggregate, stage 2: one lane per group sums its scaled partials, multiplies the sum by L^-1 on the
+// small-integer path (ops.h lagrange_small), and compresses.
 __global__ void __launch_bounds__(kBlock) k_tagg_sum(const uint32_t* __restrict__ pts,
                                                      const int32_t* __restrict__ pstat,
+                                                     const int64_t* __restrict__ ids,
                                                      const uint64_t* __restrict__ goffs, uint64_t n_groups,
                                                      uint64_t n_parts, uint8_t* __restrict__ out,
                                                      int32_t* __restrict__ status) {
@@ -211,6 +215,7 @@ __global__ void __launch_bounds__(kBlock) k_tagg_sum(const uint32_t* __restrict_
       for (int w = 0; w < 72; ++w) dst[w] = pts[(uint64_t)w * n_parts + k];
       jac_add(acc, acc, p);
     }
+    tagg_unscale(acc, ids + g0, (int)(g1 - g0));
   }
   uint8_t sig[96];
   g2_compress(sig, acc);
@@ -230,6 +235,7 @@ __global__ void __launch_bounds__(kBlock) k_tagg_sum(const uint32_t* __restrict_
 // agg_inf[g] = 1 when it is the point at infinity.
 __global__ void __launch_bounds__(kBlock) k_tagg_sum_v(const uint32_t* __restrict__ pts,
                                                        const int32_t* __restrict__ pstat,
+                                                       const int64_t* __restrict__ ids,
                                                        const uint64_t* __restrict__ goffs, uint64_t n_groups,
                                                        uint64_t n_parts, uint8_t* __restrict__ out,
                                                        int32_t* __restrict__ status, uint32_t* __restrict__ ws,
@@ -253,6 +259,7 @@ __global__ void __launch_bounds__(kBlock) k_tagg_sum_v(const uint32_t* __restric
       jac_add(y, x, p);
       acc = y;
     }
+    tagg_unscale(acc, ids + g0, (int)(g1 - g0));
   }
   uint8_t sig[96];
   g2_compress(sig, acc);
@@ -293,6 +300,42 @@ __global__ void __launch_bounds__(kBlock) k_tv_prep_pk(const uint8_t* __restrict
     soa_store<24>(ws, n, i, &pk.x.v[0]);
     soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);
   }
+  vstatus[i] = st;
+}
+
+// k_tv_prep_pk with the roles split per workgroup, as k_verify_prep: the first grid_for(n) blocks decode the keys
+// (status, pk), the next 2 grid_for(n) blocks hash the messages on lane pairs (lg2.h hash_to_g2_pair), so the key
+// decode runs beside the hash and each hash takes about half the latency.  Every message is hashed.
+__global__ void __launch_bounds__(kBlock) k_tv_prep_pk2(const uint8_t* __restrict__ pks,
+                                                        const uint8_t* __restrict__ msgs,
+                                                        const uint64_t* __restrict__ offs, uint64_t n,
+                                                        uint32_t* __restrict__ ws, int32_t* __restrict__ vstatus) {
+  const uint64_t nb = (n + kBlock - 1) / kBlock;
+  if (blockIdx.x >= nb) {  // uniform per workgroup
+    const uint64_t t = (blockIdx.x - nb) * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t i = t >> 1;
+    if (i >= n) return;  // same on both lanes of the pair
+    const uint32_t m = (t & 1) ? ~0u : 0u;
+    const uint64_t o0 = offs[i], o1 = offs[i + 1];
+    g2j hj;
+    hash_to_g2_pair(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43, m);
+    if (!m) {
+      g2a hm;
+      jac_to_aff(hm, hj);
+      soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);
+    }
+    return;
+  }
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g1a pk;
+  const int dp = g1_decompress(pk, pks + 48 * i, true);
+  int st = RLC_PENDING;
+  if (dp == DEC_BAD)
+    st = HIPBLS_ERR_PUBKEY;
+  else if (dp == DEC_INF)
+    st = HIPBLS_ERR_VERIFY;
+  if (st == RLC_PENDING) soa_store<24>(ws, n, i, &pk.x.v[0]);
   vstatus[i] = st;
 }
 

@@ -83,6 +83,116 @@ BLS_HD BLS_CALL void lagrange_at_zero(fr& out_plain, const int64_t* ids, int n, 
   fr_to_plain(out_plain, t);
 }
 
+// ThresholdAggregate with small share indices (charon's are 1..n, n the cluster size; app/app.go:344-381).
+// lambda_k = N_k / D_k with the integers N_k = prod_{j != k} x_j and D_k = prod_{j != k} (x_j - x_k).  With
+// L = lcm_k |D_k|, every c_k = N_k (L / D_k) is an integer and
+//     sum_k lambda_k sig_k = [L^-1 mod r] sum_k c_k sig_k,
+// so each partial needs a multiplication by a short integer (36 bits for 7-of-10 over ids 1..10) instead of a 255-bit
+// lambda_k, and the group one 255-bit multiplication of the sum.  Returns false -- the caller takes the field path,
+// lagrange_at_zero -- unless the whole group fits: t <= 16, |x_j| <= 2^20 and L and every c_k below 2^63.  The
+// decision is the group's (every c_k is checked), so all lanes of a group and the group's sum agree on the path.
+BLS_HD BLS_INLINE uint64_t gcd_u64(uint64_t a, uint64_t b) {
+  while (b) {
+    const uint64_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+BLS_HD BLS_CALL bool lagrange_small(const int64_t* ids, int t, int me, int64_t& c_me, uint64_t& L) {
+  if (t < 1 || t > 16) return false;
+  for (int a = 0; a < t; ++a)
+    if (ids[a] > (1 << 20) || ids[a] < -(1 << 20) || ids[a] == 0) return false;
+  int64_t D[16];
+  uint64_t l = 1;
+  for (int k = 0; k < t; ++k) {
+    int64_t d = 1;
+    for (int j = 0; j < t; ++j) {
+      if (j == k) continue;
+      if (__builtin_mul_overflow(d, ids[j] - ids[k], &d)) return false;
+    }
+    if (d == 0 || d == INT64_MIN) return false;  // duplicate ids (the status already says "cannot combine")
+    D[k] = d;
+    const uint64_t ad = d < 0 ? (uint64_t)(-d) : (uint64_t)d;
+    if (__builtin_mul_overflow(l, ad / gcd_u64(l, ad), &l) || l > (uint64_t)INT64_MAX) return false;
+  }
+  for (int k = 0; k < t; ++k) {
+    int64_t n = 1;
+    for (int j = 0; j < t; ++j)
+      if (j != k && __builtin_mul_overflow(n, ids[j], &n)) return false;
+    const uint64_t ad = D[k] < 0 ? (uint64_t)(-D[k]) : (uint64_t)D[k];
+    const int64_t f = D[k] < 0 ? -(int64_t)(l / ad) : (int64_t)(l / ad);
+    int64_t c;
+    if (__builtin_mul_overflow(n, f, &c) || c == INT64_MIN) return false;
+    if (k == me) c_me = c;
+  }
+  L = l;
+  return true;
+}
+
+// [c] P for a signed 64-bit c (jac_mul_u64 of |c|, negated for c < 0)
+BLS_HD BLS_INLINE void g2_mul_i64(g2j& r, const g2j& p, int64_t c) {
+  jac_mul_u64(r, p, c < 0 ? (uint64_t)0 - (uint64_t)c : (uint64_t)c);
+  if (c < 0) {
+    g2j t = r;
+    jac_neg(r, t);
+  }
+}
+
+// Partial k of a group (ids[0..t), this partial's index me): lambda_k * sig (small-integer path: c_k * sig, the
+// group's sum is multiplied by L^-1 in tagg_unscale).
+BLS_HD BLS_CALL void tagg_scale_point(g2j& out, const g2j& sj, const int64_t* ids, int t, int me) {
+  int64_t c;
+  uint64_t L;
+  if (lagrange_small(ids, t, me, c, L)) {
+    g2_mul_i64(out, sj, c);
+  } else {
+    fr lam;
+    lagrange_at_zero(lam, ids, t, me);
+    g2_mul_glv4(out, sj, lam.v);
+  }
+}
+
+// The group's sum of scaled partials -> the aggregate: [L^-1 mod r] sum on the small-integer path, as is otherwise.
+BLS_HD BLS_CALL void tagg_unscale(g2j& acc, const int64_t* ids, int t) {
+  int64_t c;
+  uint64_t L;
+  if (!lagrange_small(ids, t, 0, c, L) || jac_is_inf(acc)) return;
+  fr lf, li, plain;
+  fr_from_i64(lf, (int64_t)L);
+  fr_inv(li, lf);
+  fr_to_plain(plain, li);
+  g2j x = acc;
+  g2_mul_glv4(acc, x, plain.v);
+}
+
+// One ThresholdAggregate group on one lane (host builds: tests/native): status as the kernels'.
+BLS_HD BLS_CALL int op_threshold_aggregate(uint8_t* out96, const uint8_t* sigs, const int64_t* ids, int t) {
+  int st = t > 0 ? HIPBLS_OK : HIPBLS_ERR_COMBINE;
+  for (int a = 0; a < t; ++a) {
+    if (ids[a] == 0) st = HIPBLS_ERR_COMBINE;
+    for (int b = a + 1; b < t; ++b)
+      if (ids[a] == ids[b]) st = HIPBLS_ERR_COMBINE;
+  }
+  g2j acc;
+  jac_set_inf(acc);
+  for (int k = 0; k < t; ++k) {  // every partial is deserialized first (herumi.go:250-262)
+    g2a s;
+    const int ds = g2_decompress(s, sigs + 96 * k, true);
+    if (ds == DEC_BAD) return HIPBLS_ERR_SIGNATURE;
+    if (st != HIPBLS_OK || ds == DEC_INF) continue;
+    g2j sj, p;
+    jac_from_aff(sj, s);
+    tagg_scale_point(p, sj, ids, t, k);
+    g2j x = acc;
+    jac_add(acc, x, p);
+  }
+  if (st != HIPBLS_OK) return st;
+  tagg_unscale(acc, ids, t);
+  g2_compress(out96, acc);
+  return HIPBLS_OK;
+}
+
 BLS_HD BLS_CALL int op_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96) {
   g1a pk;
   const int dp = g1_decompress(pk, pk48, true);

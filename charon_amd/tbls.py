@@ -42,7 +42,8 @@ class DeviceError(RuntimeError):
     """HIP runtime failure.  Never converted into a 'verified' result."""
 
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhipbls.so")
+# HIPBLS_LIB: another build of the same library (A/B measurements of compile-time variants); default in-tree
+_LIB_PATH = os.environ.get("HIPBLS_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhipbls.so")
 _lib = None
 
 

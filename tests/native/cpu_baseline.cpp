@@ -49,32 +49,8 @@ double cb_threshold_aggregate_batch(const uint8_t* sigs, const int64_t* ids, con
                                     uint8_t* out, int32_t* status, int threads) {
   return run_parallel(n_groups, threads, [&](uint64_t g) {
     const uint64_t g0 = goffs[g], g1 = goffs[g + 1];
-    const int t = (int)(g1 - g0);
-    int st = t > 0 ? HIPBLS_OK : HIPBLS_ERR_COMBINE;
-    for (int a = 0; a < t; ++a) {
-      if (ids[g0 + a] == 0) st = HIPBLS_ERR_COMBINE;
-      for (int b = a + 1; b < t; ++b)
-        if (ids[g0 + a] == ids[g0 + b]) st = HIPBLS_ERR_COMBINE;
-    }
-    g2j acc;
-    jac_set_inf(acc);
-    for (int k = 0; k < t && st == HIPBLS_OK; ++k) {
-      g2a s;
-      const int ds = g2_decompress(s, sigs + 96 * (g0 + k), true);
-      if (ds == DEC_BAD) {
-        st = HIPBLS_ERR_SIGNATURE;
-        break;
-      }
-      if (ds == DEC_INF) continue;
-      fr lam;
-      lagrange_at_zero(lam, ids + g0, t, k);
-      g2j sj, p;
-      jac_from_aff(sj, s);
-      g2_mul_glv4(p, sj, lam.v);
-      jac_add(acc, acc, p);
-    }
     uint8_t sig[96];
-    g2_compress(sig, acc);
+    const int st = op_threshold_aggregate(sig, sigs + 96 * g0, ids + g0, (int)(g1 - g0));
     for (int b = 0; b < 96; ++b) out[96 * g + b] = st == HIPBLS_OK ? sig[b] : 0;
     status[g] = st;
   });

@@ -189,30 +189,12 @@ void ht_fp12_op(int op, const uint8_t* a576, const uint8_t* b576, uint8_t* out57
 }
 
 int ht_threshold_aggregate(const uint8_t* sigs, const int64_t* ids, int n, uint8_t* out96) {
-  g2j acc;
-  jac_set_inf(acc);
-  for (int i = 0; i < n; ++i) {
-    for (int j = 0; j < n; ++j)
-      if (j != i && ids[j] == ids[i]) return HIPBLS_ERR_COMBINE;
-    if (ids[i] == 0) return HIPBLS_ERR_COMBINE;
-  }
-  for (int i = 0; i < n; ++i) {
-    g2a s;
-    int st = g2_decompress(s, sigs + 96 * i, true);
-    if (st == DEC_BAD) return HIPBLS_ERR_SIGNATURE;
-    g2j sj;
-    if (st == DEC_INF)
-      jac_set_inf(sj);
-    else
-      jac_from_aff(sj, s);
-    fr lam;
-    lagrange_at_zero(lam, ids, n, i);
-    g2j t;
-    g2_mul_glv4(t, sj, lam.v);
-    jac_add(acc, acc, t);
-  }
-  g2_compress(out96, acc);
-  return HIPBLS_OK;
+  return op_threshold_aggregate(out96, sigs, ids, n);  // ops.h: the kernels' two paths (small ids / field)
+}
+
+// ops.h lagrange_small: 1 and (c_me, L) when the group takes the small-integer path, else 0.
+int ht_lagrange_small(const int64_t* ids, int t, int me, int64_t* c, uint64_t* L) {
+  return lagrange_small(ids, t, me, *c, *L) ? 1 : 0;
 }
 
 // [k] P on G2 by the 4-dimensional GLS split (k: 8 plain little-endian limbs) or, with glv = 0,

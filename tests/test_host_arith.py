@@ -331,3 +331,48 @@ def test_verify_signature_membership_from_miller_loop(L):
         for p, m, want in ((pk, msg, 0 if k == 0 else 2), (pk, msg[::-1], 3 if k == 0 else 2),
                            (inf_pk, msg, 3 if k == 0 else 2)):
             assert L.ht_verify(p, m, 32, s) == want, (k, want)
+
+
+def test_lagrange_small_integers(L):
+    """ops.h lagrange_small: for small share ids, c_k = N_k (L / D_k) is an exact integer with c_k = lambda_k L mod r
+    (so sum lambda_k sig_k = [L^-1] sum c_k sig_k); large, zero or duplicate ids take the field path (0)."""
+    import ctypes
+    R = bls.R
+    rng = random.Random(9)
+    cases = [[1, 2, 3], list(range(1, 11))[:7], [3, 7, 1, 10, 2, 9, 5], [-3, 5, 2], list(range(1, 17)),
+             [1, 1 << 20], [5]]
+    for _ in range(20):
+        n = rng.randrange(2, 11)
+        cases.append(rng.sample(range(1, 40), n))
+    from math import gcd, prod
+
+    def expect(ids):  # the exact integers, and whether all of them fit the 63-bit path
+        t = len(ids)
+        D = [prod(ids[j] - ids[k] for j in range(t) if j != k) for k in range(t)]
+        Lx = 1
+        for d in D:
+            Lx = Lx * abs(d) // gcd(Lx, abs(d))
+        N = [prod(ids[j] for j in range(t) if j != k) for k in range(t)]
+        c = [N[k] * (Lx // abs(D[k])) * (1 if D[k] > 0 else -1) for k in range(t)]
+        fits = t <= 16 and all(abs(v) < 2 ** 63 for v in D + N + c + [Lx])
+        return fits, c, Lx
+
+    n_small = 0
+    for ids in cases:
+        t = len(ids)
+        arr = (ctypes.c_int64 * t)(*ids)
+        lam = bls.lagrange_coeffs_at_zero(ids)
+        fits, cx, Lx = expect(ids)
+        n_small += fits
+        for me in range(t):
+            c, Lv = ctypes.c_int64(), ctypes.c_uint64()
+            ok = L.ht_lagrange_small(arr, t, me, ctypes.byref(c), ctypes.byref(Lv))
+            assert ok == int(fits), ids
+            if ok:
+                assert c.value == cx[me] and Lv.value == Lx
+                assert (c.value - lam[me] * Lv.value) % R == 0, (ids, me)
+    assert n_small >= 20
+    for ids in ([1, 2, 1 << 21], [0, 1, 2], [4, 4, 1], [1 << 40, 3], list(range(1, 18))):
+        arr = (ctypes.c_int64 * len(ids))(*ids)
+        c, Lv = ctypes.c_int64(), ctypes.c_uint64()
+        assert L.ht_lagrange_small(arr, len(ids), 0, ctypes.byref(c), ctypes.byref(Lv)) == 0, ids
