@@ -829,8 +829,9 @@ int launch_tagg(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, const u
   return ws_end(c, s);
 }
 
-// sigagg in one call: ThresholdAggregate on sub[0] while sub[1] decodes the validators' root keys and hashes their
-// messages; the caller's stream joins both and runs the pairing checks on the aggregates (kernels.h, k_tagg_sum_v).
+// sigagg in one call: ThresholdAggregate on sub[0] while sub[1] decodes and scales the validators' root keys and
+// hashes their messages; the caller's stream joins both and runs the pairing checks on S (kernels.h, k_tagg_sum_s)
+// while sub[0] goes on to [L^-1] S and the 96-byte aggregates (k_tagg_unscale).
 int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, const uint64_t* d_goffs,
                        uint64_t n_groups, uint64_t n_parts, const uint8_t* d_dvpks, const uint8_t* d_msgs,
                        const uint64_t* d_moffs, uint8_t* d_out, int32_t* d_astatus, int32_t* d_vstatus, hipStream_t s) {
@@ -857,22 +858,28 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
     if (rc) return rc;
   }
   rc = timed(c, "tagg_sum", s0, [&] {
-    hipLaunchKernelGGL(k_tagg_sum_v, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s0,
-                       (const uint32_t*)c.b_pts.p, (const int32_t*)c.b_pst.p, d_ids, d_goffs, n_groups, n_parts,
-                       d_out, d_astatus, ws, agg_inf);
+    hipLaunchKernelGGL(k_tagg_sum_s, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s0,
+                       (const uint32_t*)c.b_pts.p, (const int32_t*)c.b_pst.p, d_goffs, n_groups, n_parts, d_astatus,
+                       ws, agg_inf);
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_join[0], s0));
+  rc = timed(c, "tagg_unscale", s0, [&] {
+    hipLaunchKernelGGL(k_tagg_unscale, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s0, d_ids, d_goffs,
+                       n_groups, (const uint32_t*)ws, (const int32_t*)agg_inf, (const int32_t*)d_astatus, d_out);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c.ev_hash, s0));
 #ifndef BLS_TV_PAIR_HASH
 #define BLS_TV_PAIR_HASH 0
 #endif
   rc = timed(c, "tv_prep_pk", s1, [&] {
     if (BLS_TV_PAIR_HASH && n_groups <= kPairHashMaxVerify)
       hipLaunchKernelGGL(k_tv_prep_pk2, dim3((unsigned)(3 * grid_for(n_groups))), dim3(kBlock), 0, s1, d_dvpks, d_msgs,
-                         d_moffs, n_groups, ws, d_vstatus);
+                         d_moffs, n_groups, d_ids, d_goffs, ws, d_vstatus);
     else
       hipLaunchKernelGGL(k_tv_prep_pk, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s1, d_dvpks, d_msgs,
-                         d_moffs, n_groups, ws, d_vstatus);
+                         d_moffs, n_groups, d_ids, d_goffs, ws, d_vstatus);
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));
@@ -892,6 +899,7 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
                          (const uint32_t*)ws, n_groups, d_vstatus);
     });
   if (rc) return rc;
+  HIP_TRY(hipStreamWaitEvent(s, c.ev_hash, 0));  // the aggregates are part of the call's result
   return ws_end(c, s);
 }
 

@@ -225,21 +225,23 @@ __global__ void __launch_bounds__(kBlock) k_tagg_sum(const uint32_t* __restrict_
 
 // ---------------------------------------------------------------- sigagg: aggregate + Verify in one call
 // core/sigagg/sigagg.go:138-159 threshold-aggregates each validator's partials and verifies the aggregate
-// against the validator's root pubkey.  hipbls_threshold_aggregate_verify_batch fuses the two: the key decode and
-// H(m) (k_tv_prep_pk) run beside the aggregation, the group sum hands its point straight to the pairing check
-// (k_tagg_sum_v: the 96-byte encoding is still written, and decompressing it would return the same point, which
-// is in G2 by construction), so the aggregate is never decompressed or subgroup-checked again.
+// against the validator's root pubkey.  hipbls_threshold_aggregate_verify_batch fuses the two:
+//   * the key side (k_tv_prep_pk) decodes the root key, scales it by the group's L (ops.h tagg_group_L) and hashes the
+//     message, beside the aggregation;
+//   * k_tagg_sum_s sums the scaled partials into S and hands S straight to the pairing check, which tests
+//     e([L] pk, H(m)) == e(g1, S) -- the same verdict as e(pk, H(m)) == e(g1, [L^-1] S);
+//   * k_tagg_unscale runs beside the pairing check: sigma = [L^-1] S, compressed into the 96-byte output.
+// The aggregate is never decompressed or subgroup-checked again (it is in G2 by construction).
 // ws: the lane-pair Verify layout (pk 24 words, H(m) 48, sig 48; SoA over the groups).
 
-// Stage 2 of ThresholdAggregate (k_tagg_sum) that also leaves the affine aggregate in ws (sig slot) and
-// agg_inf[g] = 1 when it is the point at infinity.
-__global__ void __launch_bounds__(kBlock) k_tagg_sum_v(const uint32_t* __restrict__ pts,
+// Stage 2 of ThresholdAggregate for the fused call: per group, the status (as k_tagg_sum) and S = the sum of the
+// scaled partials, left affine in ws (sig slot) with agg_inf[g] = 1 when it is the point at infinity (or the group
+// failed).
+__global__ void __launch_bounds__(kBlock) k_tagg_sum_s(const uint32_t* __restrict__ pts,
                                                        const int32_t* __restrict__ pstat,
-                                                       const int64_t* __restrict__ ids,
                                                        const uint64_t* __restrict__ goffs, uint64_t n_groups,
-                                                       uint64_t n_parts, uint8_t* __restrict__ out,
-                                                       int32_t* __restrict__ status, uint32_t* __restrict__ ws,
-                                                       int32_t* __restrict__ agg_inf) {
+                                                       uint64_t n_parts, int32_t* __restrict__ status,
+                                                       uint32_t* __restrict__ ws, int32_t* __restrict__ agg_inf) {
   const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (g >= n_groups) return;
   const uint64_t g0 = goffs[g], g1 = goffs[g + 1];
@@ -259,11 +261,7 @@ __global__ void __launch_bounds__(kBlock) k_tagg_sum_v(const uint32_t* __restric
       jac_add(y, x, p);
       acc = y;
     }
-    tagg_unscale(acc, ids + g0, (int)(g1 - g0));
   }
-  uint8_t sig[96];
-  g2_compress(sig, acc);
-  for (int b = 0; b < 96; ++b) out[96 * g + b] = st == HIPBLS_OK ? sig[b] : (uint8_t)0;
   status[g] = st;
   const bool inf = jac_is_inf(acc);
   g2a a;
@@ -277,10 +275,37 @@ __global__ void __launch_bounds__(kBlock) k_tagg_sum_v(const uint32_t* __restric
   agg_inf[g] = inf ? 1 : 0;
 }
 
+// Stage 3 (beside the pairing check): sigma = [L^-1] S on the small-integer path (S itself otherwise), compressed.
+// The output bytes equal k_tagg_sum's: the encoding of sigma for a group that combined, zeros otherwise.
+__global__ void __launch_bounds__(kBlock) k_tagg_unscale(const int64_t* __restrict__ ids,
+                                                         const uint64_t* __restrict__ goffs, uint64_t n_groups,
+                                                         const uint32_t* __restrict__ ws,
+                                                         const int32_t* __restrict__ agg_inf,
+                                                         const int32_t* __restrict__ status, uint8_t* __restrict__ out) {
+  const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (g >= n_groups) return;
+  const int st = status[g];
+  g2j acc;
+  jac_set_inf(acc);
+  if (st == HIPBLS_OK && !agg_inf[g]) {
+    g2a a;
+    soa_load<48>(&a.x.c0.v[0], ws + 72 * n_groups, n_groups, g);
+    jac_from_aff(acc, a);
+    const uint64_t g0 = goffs[g], g1 = goffs[g + 1];
+    tagg_unscale(acc, ids + g0, (int)(g1 - g0));
+  }
+  uint8_t sig[96];
+  g2_compress(sig, acc);
+  for (int b = 0; b < 96; ++b) out[96 * g + b] = st == HIPBLS_OK ? sig[b] : (uint8_t)0;
+}
+
 // Verify prep of the key side (one lane per group, beside the aggregation): decode + subgroup-check the
-// validator's root pubkey, hash its message; vstatus = ERR_PUBKEY / ERR_VERIFY (identity key) or pending.
+// validator's root pubkey, scale it by the group's L, hash its message; vstatus = ERR_PUBKEY / ERR_VERIFY (identity
+// key) or pending.
 __global__ void __launch_bounds__(kBlock) k_tv_prep_pk(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ msgs,
                                                        const uint64_t* __restrict__ offs, uint64_t n,
+                                                       const int64_t* __restrict__ ids,
+                                                       const uint64_t* __restrict__ goffs,
                                                        uint32_t* __restrict__ ws, int32_t* __restrict__ vstatus) {
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -292,6 +317,8 @@ __global__ void __launch_bounds__(kBlock) k_tv_prep_pk(const uint8_t* __restrict
   else if (dp == DEC_INF)
     st = HIPBLS_ERR_VERIFY;
   if (st == RLC_PENDING) {
+    const uint64_t g0 = goffs[i], g1 = goffs[i + 1];
+    g1_scale_affine(pk, tagg_group_L(ids + g0, (int)(g1 - g0)));
     const uint64_t o0 = offs[i], o1 = offs[i + 1];
     g2j hj;
     hash_to_g2(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43);
@@ -303,12 +330,14 @@ __global__ void __launch_bounds__(kBlock) k_tv_prep_pk(const uint8_t* __restrict
   vstatus[i] = st;
 }
 
-// k_tv_prep_pk with the roles split per workgroup, as k_verify_prep: the first grid_for(n) blocks decode the keys
-// (status, pk), the next 2 grid_for(n) blocks hash the messages on lane pairs (lg2.h hash_to_g2_pair), so the key
-// decode runs beside the hash and each hash takes about half the latency.  Every message is hashed.
+// k_tv_prep_pk with the roles split per workgroup, as k_verify_prep: the first grid_for(n) blocks decode and scale
+// the keys (status, pk), the next 2 grid_for(n) blocks hash the messages on lane pairs (lg2.h hash_to_g2_pair), so the
+// key decode runs beside the hash and each hash takes about half the latency.  Every message is hashed.
 __global__ void __launch_bounds__(kBlock) k_tv_prep_pk2(const uint8_t* __restrict__ pks,
                                                         const uint8_t* __restrict__ msgs,
                                                         const uint64_t* __restrict__ offs, uint64_t n,
+                                                        const int64_t* __restrict__ ids,
+                                                        const uint64_t* __restrict__ goffs,
                                                         uint32_t* __restrict__ ws, int32_t* __restrict__ vstatus) {
   const uint64_t nb = (n + kBlock - 1) / kBlock;
   if (blockIdx.x >= nb) {  // uniform per workgroup
@@ -335,7 +364,11 @@ __global__ void __launch_bounds__(kBlock) k_tv_prep_pk2(const uint8_t* __restric
     st = HIPBLS_ERR_PUBKEY;
   else if (dp == DEC_INF)
     st = HIPBLS_ERR_VERIFY;
-  if (st == RLC_PENDING) soa_store<24>(ws, n, i, &pk.x.v[0]);
+  if (st == RLC_PENDING) {
+    const uint64_t g0 = goffs[i], g1 = goffs[i + 1];
+    g1_scale_affine(pk, tagg_group_L(ids + g0, (int)(g1 - g0)));
+    soa_store<24>(ws, n, i, &pk.x.v[0]);
+  }
   vstatus[i] = st;
 }
 

@@ -166,6 +166,26 @@ BLS_HD BLS_CALL void tagg_unscale(g2j& acc, const int64_t* ids, int t) {
   g2_mul_glv4(acc, x, plain.v);
 }
 
+// Aggregate-and-verify without waiting for [L^-1]: on the small-integer path the aggregate is sigma = [L^-1] S with
+// S = sum_k c_k sig_k, and since L is invertible mod r,
+//     e(pk, H(m)) == e(g1, [L^-1] S)   <=>   e([L] pk, H(m)) == e(g1, S)
+// (raise both sides to L; G_T has order r).  So the pairing check runs on S and on [L] pk -- a G1 multiplication by
+// an integer below 2^63 -- while [L^-1] S, which only the 96-byte output needs, runs beside it.  Returns 1 off the
+// small-integer path (S is then sigma itself).
+BLS_HD BLS_INLINE uint64_t tagg_group_L(const int64_t* ids, int t) {
+  int64_t c;
+  uint64_t L;
+  return lagrange_small(ids, t, 0, c, L) ? L : 1;
+}
+// pk <- [L] pk for pk in G1, not infinity: [L] pk is not infinity either (0 < L < 2^63 < r).
+BLS_HD BLS_CALL void g1_scale_affine(g1a& pk, uint64_t L) {
+  if (L <= 1) return;
+  g1j pj, q;
+  jac_from_aff(pj, pk);
+  jac_mul_u64(q, pj, L);
+  jac_to_aff(pk, q);
+}
+
 // One ThresholdAggregate group on one lane (host builds: tests/native): status as the kernels'.
 BLS_HD BLS_CALL int op_threshold_aggregate(uint8_t* out96, const uint8_t* sigs, const int64_t* ids, int t) {
   int st = t > 0 ? HIPBLS_OK : HIPBLS_ERR_COMBINE;

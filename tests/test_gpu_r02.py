@@ -421,7 +421,7 @@ def test_threshold_aggregate_verify_fused_equals_two_calls(impl):
     """hipbls_threshold_aggregate_verify_batch == batch_threshold_aggregate + batch_verify_status of the
     aggregates, on honest groups, a failing aggregation (id 0, bad partial), a wrong root key, a wrong message,
     an identity root key and an all-infinity group (aggregate at infinity)."""
-    from charon_amd.tbls import TBLSError
+    from oracle import bls12381 as bls
     rng = random.Random(404)
     groups, dvpks, msgs = [], [], []
     secrets_ = []
@@ -429,6 +429,8 @@ def test_threshold_aggregate_verify_fused_equals_two_calls(impl):
         secret = rng.randrange(1, R_ORDER)
         tail = [rng.randrange(R_ORDER) for _ in range(2)]
         ids = rng.sample(range(1, 9), 3)
+        if g in (11, 12):  # ids off the small-integer Lagrange path (ops.h lagrange_small): L = 1, S = sigma
+            ids = [2 ** 40 + 3 + g, 5, 2 ** 21]
         sh = _shares_at(secret, tail, ids)
         root = rng.randbytes(32)
         sigs, _ = impl.sign_batch([sh[i] for i in ids], [root] * 3)
@@ -459,4 +461,6 @@ def test_threshold_aggregate_verify_fused_equals_two_calls(impl):
     assert [vst[g] for g in ok] == want_v
     assert vst[3] == 5 and vst[4] == 2  # aggregation statuses carried over
     assert vst[5] == 3 and vst[7] == 3 and vst[8] == 3 and vst[9] == 3 and vst[10] == 1
+    assert vst[11] == 0 and vst[12] == 0
+    assert res[11] == bls.threshold_aggregate(groups[11])
     assert sum(1 for v in vst if v == 0) == 40 - 7
