@@ -418,7 +418,9 @@ BLS_HD BLS_INLINE void fp_mul_small(fp& r, const fp& a, uint32_t k) {
 // 30 divsteps per outer iteration on 62-bit approximations (the low 30 bits and the top 32 bits of a and b at
 // the longer one's length), then one signed 2x2 update of the full a, b (30-bit limbs) and of u, v mod p with an
 // exact division by 2^30 (one Montgomery-style digit).  Invariant a = x u, b = x v (mod p); a reaches 0 and b = 1
-// within 2*381 - 1 = 761 divsteps, so 26 iterations of 30; an extra iteration is a no-op (a = 0 stays 0).
+// within len(a) + len(b) - 1 divsteps: 761 for a canonical input (< p, 381 bits), 763 for any input below 2^382
+// (callers pass canonical values: fp_inv's operands are product or fp_add outputs, never fp_add_lazy sums).  ITERS =
+// 27 runs 810 divsteps, covering both with a spare iteration; once a = 0 an iteration is a no-op (a stays 0).
 // Every decision is a select on lane data: all lanes run the same instruction stream.  ~33k VALU per inversion
 // against ~300k for the Fermat power x^(p-2) (455 products); inverse of 0 is 0, like the power.
 // Result: x^-1 for the plain integer x = a_mont = aR, then one product by R^3 gives (aR)^-1 R^2 = a^-1 R.

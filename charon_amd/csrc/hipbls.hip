@@ -91,8 +91,21 @@ struct VBatch {
   uint64_t n() const { return off.size() - 1; }
 };
 
-// Per-context submission queue (worker, stream and buffers of its own).
+// A wire-format batch in flight on the GPU: its own stream, buffers and pinned status copy, so a second batch can be
+// copied in and launched while the first one runs.
+struct QSlot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done_ev = nullptr;
+  DevBuf d_pk, d_sig, d_msg, d_off, d_st, d_ws;
+  int32_t* h_st = nullptr;  // pinned: the status copy is a real async D2H (a pageable one would block the worker)
+  uint64_t h_cap = 0;
+  std::shared_ptr<VBatch> b;
+  int rc = HIPBLS_OK;
+};
+
+// Per-context submission queue (worker, streams and buffers of its own).
 struct VerifyQueue {
+  static constexpr int kSlots = 2;  // wire batches in flight at once
   std::mutex mu;
   std::condition_variable cv_work, cv_done;
   std::deque<std::shared_ptr<VBatch>> open;  // accepting (back) / waiting for the worker (front)
@@ -100,11 +113,13 @@ struct VerifyQueue {
   uint64_t next_ticket = 1;
   std::thread worker;
   bool started = false, stop = false;
-  uint64_t batches = 0, items = 0, keyed = 0;
-  hipStream_t stream = nullptr;
-  DevBuf d_pk, d_sig, d_msg, d_off, d_st, d_ws, d_kidx, d_midx, d_slot, d_mlist, d_rlc_st;
+  uint64_t batches = 0, items = 0, keyed = 0, overlapped = 0;
+  hipStream_t stream = nullptr;  // the keyed path's stream
+  QSlot slot[kSlots];
+  std::deque<int> inflight;  // slots in launch order
+  DevBuf d_pk, d_sig, d_msg, d_off, d_kidx, d_midx, d_slot, d_mlist, d_rlc_st;
   // host staging of the keyed path (reused across batches)
-  std::vector<uint32_t> kidx, midx, order, slot, miss;
+  std::vector<uint32_t> kidx, midx, order, slotv, miss;
   std::vector<uint8_t> sig_sorted, umsg;
   std::vector<uint64_t> uoff;
   std::vector<int32_t> st_sorted;
@@ -871,7 +886,7 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_hash, s0));
 #ifndef BLS_TV_PAIR_HASH
-#define BLS_TV_PAIR_HASH 0
+#define BLS_TV_PAIR_HASH 1
 #endif
   rc = timed(c, "tv_prep_pk", s1, [&] {
     if (BLS_TV_PAIR_HASH && n_groups <= kPairHashMaxVerify)
@@ -1136,23 +1151,38 @@ std::atomic<uint64_t> g_q_max_batch{65536};
 std::atomic<uint32_t> g_q_gather_us{200};
 constexpr uint64_t kQueueKeyedMin = 8;  // without the H(m) cache, batches below this take the lane-pair Verify
 
-int run_batch_wire(Context& c, VBatch& b) {
-  VerifyQueue& q = c.q;
+// Copies a wire-format batch in and launches it on slot k; the status comes back into the slot's pinned buffer and
+// done_ev marks completion (wire_finish collects it).  Nothing here waits for the GPU.
+int wire_launch(Context& c, QSlot& k, VBatch& b) {
   const uint64_t n = b.n();
-  HIP_TRY(q.d_pk.ensure(n * 48));
-  HIP_TRY(q.d_sig.ensure(n * 96));
-  HIP_TRY(q.d_msg.ensure(b.msg.size() ? b.msg.size() : 1));
-  HIP_TRY(q.d_off.ensure((n + 1) * 8));
-  HIP_TRY(q.d_st.ensure(n * 4));
-  HIP_TRY(hipMemcpyAsync(q.d_pk.p, b.pk.data(), n * 48, hipMemcpyHostToDevice, q.stream));
-  HIP_TRY(hipMemcpyAsync(q.d_sig.p, b.sig.data(), n * 96, hipMemcpyHostToDevice, q.stream));
-  if (b.msg.size()) HIP_TRY(hipMemcpyAsync(q.d_msg.p, b.msg.data(), b.msg.size(), hipMemcpyHostToDevice, q.stream));
-  HIP_TRY(hipMemcpyAsync(q.d_off.p, b.off.data(), (n + 1) * 8, hipMemcpyHostToDevice, q.stream));
-  int rc = launch_verify(c, (const uint8_t*)q.d_pk.p, (const uint8_t*)q.d_msg.p, (const uint64_t*)q.d_off.p,
-                         (const uint8_t*)q.d_sig.p, n, (int32_t*)q.d_st.p, q.stream, q.d_ws);
+  HIP_TRY(k.d_pk.ensure(n * 48));
+  HIP_TRY(k.d_sig.ensure(n * 96));
+  HIP_TRY(k.d_msg.ensure(b.msg.size() ? b.msg.size() : 1));
+  HIP_TRY(k.d_off.ensure((n + 1) * 8));
+  HIP_TRY(k.d_st.ensure(n * 4));
+  if (k.h_cap < n) {
+    if (k.h_st) HIP_TRY(hipHostFree(k.h_st));
+    k.h_st = nullptr;
+    k.h_cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&k.h_st, n * 4, hipHostMallocDefault));
+    k.h_cap = n;
+  }
+  HIP_TRY(hipMemcpyAsync(k.d_pk.p, b.pk.data(), n * 48, hipMemcpyHostToDevice, k.stream));
+  HIP_TRY(hipMemcpyAsync(k.d_sig.p, b.sig.data(), n * 96, hipMemcpyHostToDevice, k.stream));
+  if (b.msg.size()) HIP_TRY(hipMemcpyAsync(k.d_msg.p, b.msg.data(), b.msg.size(), hipMemcpyHostToDevice, k.stream));
+  HIP_TRY(hipMemcpyAsync(k.d_off.p, b.off.data(), (n + 1) * 8, hipMemcpyHostToDevice, k.stream));
+  int rc = launch_verify(c, (const uint8_t*)k.d_pk.p, (const uint8_t*)k.d_msg.p, (const uint64_t*)k.d_off.p,
+                         (const uint8_t*)k.d_sig.p, n, (int32_t*)k.d_st.p, k.stream, k.d_ws);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(b.status.data(), q.d_st.p, n * 4, hipMemcpyDeviceToHost, q.stream));
-  HIP_TRY(hipStreamSynchronize(q.stream));
+  HIP_TRY(hipMemcpyAsync(k.h_st, k.d_st.p, n * 4, hipMemcpyDeviceToHost, k.stream));
+  HIP_TRY(hipEventRecord(k.done_ev, k.stream));
+  return HIPBLS_OK;
+}
+
+int wire_finish(QSlot& k) {
+  if (k.rc) return k.rc;
+  HIP_TRY(hipEventSynchronize(k.done_ev));
+  memcpy(k.b->status.data(), k.h_st, k.b->n() * 4);
   return HIPBLS_OK;
 }
 
@@ -1205,56 +1235,104 @@ int run_batch_keyed(Context& c, VBatch& b) {
   return HIPBLS_OK;
 }
 
-int run_batch(Context& c, VBatch& b) {
+// The keyed path when every key of the batch is in the table (run here, synchronously); otherwise false.
+bool try_keyed(Context& c, VBatch& b, int& rc) {
   const uint64_t n = b.n();
-  b.status.assign(n, HIPBLS_ERR_DEVICE);
-  {
-    std::lock_guard<std::mutex> lk(c.mu);
-    // small batches take the lower-latency lane-pair Verify, unless the caller enabled the H(m) cache
-    bool keyed = c.t_size > 0 && (n >= kQueueKeyedMin || c.hcache.cap > 0);
-    uint64_t miss_at = n;
-    for (uint64_t i = 0; keyed && i < n; ++i) {
-      keyed = c.t_index.count(std::string((const char*)b.pk.data() + 48 * i, 48)) != 0;
-      if (!keyed) miss_at = i;
-    }
-    static const bool dbg = getenv("HIPBLS_DEBUG_QUEUE") != nullptr;
-    if (dbg)
-      fprintf(stderr, "[hipbls queue] ctx %d batch n=%llu keyed=%d t_size=%llu cap=%llu miss_at=%llu\n", c.slot,
-              (unsigned long long)n, (int)keyed, (unsigned long long)c.t_size, (unsigned long long)c.hcache.cap,
-              (unsigned long long)miss_at);
-    if (keyed) {
-      c.q.keyed += 1;
-      return run_batch_keyed(c, b);
-    }
+  std::lock_guard<std::mutex> lk(c.mu);
+  // small batches take the lower-latency lane-pair Verify, unless the caller enabled the H(m) cache
+  bool keyed = c.t_size > 0 && (n >= kQueueKeyedMin || c.hcache.cap > 0);
+  uint64_t miss_at = n;
+  for (uint64_t i = 0; keyed && i < n; ++i) {
+    keyed = c.t_index.count(std::string((const char*)b.pk.data() + 48 * i, 48)) != 0;
+    if (!keyed) miss_at = i;
   }
-  return run_batch_wire(c, b);
+  static const bool dbg = getenv("HIPBLS_DEBUG_QUEUE") != nullptr;
+  if (dbg)
+    fprintf(stderr, "[hipbls queue] ctx %d batch n=%llu keyed=%d t_size=%llu cap=%llu miss_at=%llu\n", c.slot,
+            (unsigned long long)n, (int)keyed, (unsigned long long)c.t_size, (unsigned long long)c.hcache.cap,
+            (unsigned long long)miss_at);
+  if (!keyed) return false;
+  c.q.keyed += 1;
+  rc = run_batch_keyed(c, b);
+  return true;
 }
 
+// Marks a batch finished (under q.mu) and drops its inputs: a ticket that is never waited then holds only its
+// status word, not the batch's keys, signatures and messages.
+void batch_done(VerifyQueue& q, VBatch& b, int rc) {
+  b.rc = rc;
+  b.done = true;
+  std::vector<uint8_t>().swap(b.pk);
+  std::vector<uint8_t>().swap(b.sig);
+  std::vector<uint8_t>().swap(b.msg);
+  std::vector<uint64_t>(1, 0).swap(b.off);
+  q.batches += 1;
+  q.cv_done.notify_all();
+}
+
+// The worker: up to kSlots wire batches in flight (the next one is copied in and launched while the previous one
+// runs, on its own stream), keyed batches run synchronously on the queue's stream.  An idle worker (nothing in
+// flight) waits gather_us for company before launching a small batch.
 void queue_worker(Context* cp) {
   Context& c = *cp;
   VerifyQueue& q = c.q;
-  const bool dev_ok = hipSetDevice(c.device) == hipSuccess &&
-                      hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) == hipSuccess;
+  bool dev_ok = hipSetDevice(c.device) == hipSuccess &&
+                hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) == hipSuccess;
+  for (int k = 0; dev_ok && k < VerifyQueue::kSlots; ++k)
+    dev_ok = hipStreamCreateWithFlags(&q.slot[k].stream, hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&q.slot[k].done_ev, hipEventDisableTiming) == hipSuccess;
   std::unique_lock<std::mutex> lk(q.mu);
   for (;;) {
-    q.cv_work.wait(lk, [&] { return q.stop || (!q.open.empty() && q.open.front()->n() > 0); });
-    if (q.open.empty() || q.open.front()->n() == 0) break;  // stop requested and nothing pending
-    const uint64_t max_batch = g_q_max_batch.load();
-    const uint32_t gather_us = g_q_gather_us.load();
-    if (gather_us && q.open.front()->n() < max_batch && !q.stop) {
-      const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(gather_us);
-      q.cv_work.wait_until(lk, until, [&] { return q.stop || q.open.front()->n() >= max_batch; });
+    const bool pending = !q.open.empty() && q.open.front()->n() > 0;
+    if (pending && (int)q.inflight.size() < VerifyQueue::kSlots) {
+      const uint64_t max_batch = g_q_max_batch.load();
+      const uint32_t gather_us = g_q_gather_us.load();
+      if (q.inflight.empty() && gather_us && q.open.front()->n() < max_batch && !q.stop) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(gather_us);
+        q.cv_work.wait_until(lk, until, [&] { return q.stop || q.open.front()->n() >= max_batch; });
+      }
+      std::shared_ptr<VBatch> b = q.open.front();
+      q.open.pop_front();
+      q.items += b->n();
+      lk.unlock();
+      b->status.assign(b->n(), HIPBLS_ERR_DEVICE);
+      int rc = HIPBLS_ERR_DEVICE;
+      if (dev_ok && try_keyed(c, *b, rc)) {
+        lk.lock();
+        batch_done(q, *b, rc);
+        continue;
+      }
+      int k = 0;
+      while (q.slot[k].b) ++k;  // a free slot (inflight.size() < kSlots); only this thread touches slots
+      QSlot& sl = q.slot[k];
+      sl.b = b;
+      sl.rc = dev_ok ? wire_launch(c, sl, *b) : HIPBLS_ERR_DEVICE;
+      lk.lock();
+      if (!q.inflight.empty()) q.overlapped += 1;
+      q.inflight.push_back(k);
+      continue;
     }
-    std::shared_ptr<VBatch> b = q.open.front();
-    q.open.pop_front();
-    lk.unlock();
-    const int rc = dev_ok ? run_batch(c, *b) : HIPBLS_ERR_DEVICE;
-    lk.lock();
-    b->rc = rc;
-    b->done = true;
-    q.batches += 1;
-    q.items += b->n();
-    q.cv_done.notify_all();
+    if (!q.inflight.empty()) {  // collect the oldest batch in flight
+      const int k = q.inflight.front();
+      QSlot& sl = q.slot[k];
+      const bool ready = sl.rc != HIPBLS_OK || hipEventQuery(sl.done_ev) != hipErrorNotReady;
+      if (!ready && (int)q.inflight.size() < VerifyQueue::kSlots) {
+        // a slot is free: wait for new work or the batch, whichever comes first (arrivals launch at once)
+        q.cv_work.wait_for(lk, std::chrono::microseconds(100),
+                           [&] { return q.stop || (!q.open.empty() && q.open.front()->n() > 0); });
+        continue;
+      }
+      lk.unlock();
+      const int rc = wire_finish(sl);
+      lk.lock();
+      q.inflight.pop_front();
+      std::shared_ptr<VBatch> b = std::move(sl.b);
+      sl.b.reset();
+      batch_done(q, *b, rc);
+      continue;
+    }
+    if (q.stop) break;  // nothing pending, nothing in flight
+    q.cv_work.wait(lk, [&] { return q.stop || (!q.open.empty() && q.open.front()->n() > 0); });
   }
 }
 

@@ -256,6 +256,14 @@ def test_binary_gcd_inverse(L):
             outs.append(sum(v << (32 * i) for i, v in enumerate(o)))
         want = (pow(x, P - 2, P) * R) % P
         assert outs[0] == outs[1] == want, hex(x)
+    # the divstep bound also covers non-canonical operands below 2^382 (p + 1, 2p - 1: 763 divsteps <= 27 x 30)
+    for xm in (P, P + 1, 2 * P - 1, 2 * P - 2, (1 << 382) - 1):
+        inp = (ctypes.c_uint32 * 12)(*[(xm >> (32 * i)) & 0xFFFFFFFF for i in range(12)])
+        o = (ctypes.c_uint32 * 12)()
+        fn(inp, 1, o)
+        got = sum(v << (32 * i) for i, v in enumerate(o))
+        x = xm * pow(R, -1, P) % P
+        assert got == (pow(x, P - 2, P) * R) % P, hex(xm)
 
 
 def test_compressed_cyclotomic_exponentiation(L):
