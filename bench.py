@@ -320,6 +320,24 @@ def timed_loop(step, steps, dev, barrier, world):
     return float(t.item())
 
 
+def kernel_stats(lib, name):
+    a = ctypes.c_double()
+    c = ctypes.c_uint64()
+    lib.hipbls_kernel_timing(name.encode(), ctypes.byref(a), ctypes.byref(c))
+    return a.value, c.value
+
+
+def stage_fracs(lib, work, calls):
+    """Per-stage roofline fraction: algorithmic Fp products of the stage over `calls` calls x 300 MADs, over the
+    stage's summed kernel time (all its launches, from HIP events on the launch streams), against MAD_PEAK_T."""
+    out = {}
+    for k, fpmul in work.items():
+        avg, n = kernel_stats(lib, k)
+        if n and fpmul:
+            out[k] = round(fpmul * calls * MADS_PER_FPMUL / (avg * n * 1e-3) / 1e12 / MAD_PEAK_T, 4)
+    return out
+
+
 def kernel_ms(lib, names):
     out = {}
     for k in names:
@@ -534,7 +552,23 @@ def main():
                             "kernel_avg_ms": kernel_ms(lib, ("rlc_items", "rlc_hash", "rlc_window", "rlc_window_lg2",
                                                              "rlc_fallback", "rlc_fallback_lg2", "rlcb_items",
                                                              "rlcb_msm", "rlcb_chunks", "rlcb_product", "rlcb_final",
-                                                             "rlcb_mark"))}
+                                                             "rlcb_mark")),
+                            "stage_frac": stage_fracs(lib, {
+                                "rlc_items": RLC_FPMUL["item"] * n4, "rlc_hash": RLC_FPMUL["hash"] * len(roots4),
+                                "rlc_window": per_win * w.value, "rlc_window_lg2": per_win * w.value,
+                                "rlc_fallback": RLC_FPMUL["fallback"] * fb.value,
+                                "rlc_fallback_lg2": RLC_FPMUL["fallback"] * fb.value,
+                                "rlcb_items": RLCB_FPMUL["item"] * n4,
+                                "rlcb_chunks": RLCB_FPMUL["chunk_4runs"] * ((n4 + 15) // 16)}, args.rlc_steps)}
+            if corrupt and variant == "i_root_per_validator":
+                # the library's default policy (HIPBLS_RLC_AUTO) on the same stream: one failing batch-wide check,
+                # then windows while it backs off (rlc_mode comment above)
+                impl.set_rlc_mode(RLC_AUTO)
+                rstep()
+                torch.cuda.synchronize(dev)
+                tel_auto = timed_loop(rstep, args.rlc_steps, dev, barrier, world)
+                assert {i for i, x in enumerate(d_st4.cpu().tolist()) if x != 0} == bad4, "RLC bitmap mismatch (auto)"
+                rlc[variant]["auto_mode_ms_per_batch"] = round(1000 * tel_auto / args.rlc_steps, 3)
             if args.keys and variant in ("i_root_per_validator", "i_all_valid"):
                 table4 = list(dict.fromkeys(pks4))
                 pos4 = {k: j for j, k in enumerate(table4)}

@@ -130,33 +130,40 @@ BLS_HD BLS_INLINE void msm_scatter_lane(uint64_t p, const uint32_t* sc, uint32_t
 }
 
 // bucket (w, j): the sum of its points.  off: MSM_WINDOWS x (MSM_NB + 1) exclusive offsets.  B: Jacobian SoA,
-// 72 words x (MSM_WINDOWS * MSM_NB).
+// 72 words x (MSM_WINDOWS * MSM_NB).  Software-pipelined: the next point's gather is issued before the current
+// addition (a call the loads cannot move across), so its latency hides behind ~30 products of work.
 BLS_HD BLS_INLINE void msm_bucket_lane(uint32_t w, uint32_t j, const uint32_t* off, const uint32_t* list,
                                        uint64_t npts, const uint32_t* pts, uint32_t* B) {
   g2j acc;
   jac_set_inf(acc);
   const uint32_t k0 = off[w * (MSM_NB + 1) + j], k1 = off[w * (MSM_NB + 1) + j + 1];
+  g2a q;
+  if (k0 < k1) soa_load<48>(&q.x.c0.v[0], pts, npts, list[(uint64_t)w * npts + k0]);
   for (uint32_t k = k0; k < k1; ++k) {
-    g2a q;
-    soa_load<48>(&q.x.c0.v[0], pts, npts, list[(uint64_t)w * npts + k]);
+    const g2a cur = q;
+    if (k + 1 < k1) soa_load<48>(&q.x.c0.v[0], pts, npts, list[(uint64_t)w * npts + k + 1]);
     g2j x = acc, y;
-    jac_add_aff(y, x, q);
+    jac_add_aff(y, x, cur);
     acc = y;
   }
   soa_store<72>(B, (uint64_t)MSM_WINDOWS * MSM_NB, (uint64_t)w * MSM_NB + j, &acc.x.c0.v[0]);
 }
 
 // segment (w, s): sum_{j in [16 s, 16 s + 16)} j B_j = T + (16 s - 1) R with R = sum B_j and T = sum (j - 16 s + 1) B_j
-// from running sums (top bucket first).  Sg: Jacobian SoA, 72 words x (MSM_WINDOWS * MSM_NSEG).
+// from running sums (top bucket first).  Sg: Jacobian SoA, 72 words x (MSM_WINDOWS * MSM_NSEG).  The next bucket is
+// loaded before the current one's two additions (as msm_bucket_lane).
 BLS_HD BLS_INLINE void msm_segment_lane(uint32_t w, uint32_t s, const uint32_t* B, uint32_t* Sg) {
   g2j R, T;
   jac_set_inf(R);
   jac_set_inf(T);
+  const uint64_t nb = (uint64_t)MSM_WINDOWS * MSM_NB, base = (uint64_t)w * MSM_NB + s * MSM_SEG;
+  g2j b;
+  soa_load<72>(&b.x.c0.v[0], B, nb, base + MSM_SEG - 1);
   for (int k = MSM_SEG - 1; k >= 0; --k) {
-    g2j b;
-    soa_load<72>(&b.x.c0.v[0], B, (uint64_t)MSM_WINDOWS * MSM_NB, (uint64_t)w * MSM_NB + s * MSM_SEG + k);
+    const g2j cur = b;
+    if (k > 0) soa_load<72>(&b.x.c0.v[0], B, nb, base + k - 1);
     g2j x = R, y;
-    jac_add(y, x, b);
+    jac_add(y, x, cur);
     R = y;
     g2j u = T, v;
     jac_add(v, u, R);

@@ -26,3 +26,21 @@ def kat():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "kat_reference.json")) as f:
         return json.load(f)
+
+
+@pytest.hookimpl(trylast=True)  # after -m deselection
+def pytest_collection_modifyitems(session, config, items):
+    """GPU sessions: bring up torch's HIP runtime before the first test touches libhipbls.
+
+    torch ships its own libamdhip64/libhsa-runtime64 (no SONAME shared with /opt/rocm's, which libhipbls links), so a
+    process that uses both holds two HIP runtimes.  bench.py always initializes torch's first; a test session whose
+    first GPU user is libhipbls could leave torch's later device enumeration failing ("No HIP GPUs are available",
+    seen once after the RLC tests ran first).  Initializing torch up front gives every GPU session bench.py's order."""
+    if not any(item.get_closest_marker("gpu") for item in items):
+        return
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda")
+    except Exception:
+        pass
