@@ -475,7 +475,7 @@ def main():
         lib.hipbls_kernel_timing_reset()
         tel = timed_loop(tstep, args.tagg_steps, dev, barrier, world)
         tagg_kms = kernel_ms(lib, ("tagg_scale", "tagg_sum", "tagg_unscale", "tv_prep_pk",
-                                         "verify_pair_lg2", "verify_pair_single"))
+                                         "verify_pair_lq4", "verify_pair_lg2", "verify_pair_single"))
         assert set(d_gst.cpu().tolist()) == {0} and set(d_vst.cpu().tolist()) == {0}, "aggregate mismatch"
         if world > 1:
             assert torch.equal(node_aggs[0][96 * g_lo:96 * g_hi], d_agg), "gathered aggregates differ from local"

@@ -445,7 +445,7 @@ int timed(Context& c, const char* name, hipStream_t s, Launch launch) {
 // uses two lanes, so it wins while the batch leaves lanes idle: one wave per SIMD is 64 x 1024 lanes on MI355X.
 int initial_pair_mode() {
   const char* pm = getenv("HIPBLS_PAIR_MODE");
-  if (pm && pm[0] >= '0' && pm[0] <= '2' && pm[1] == 0) return pm[0] - '0';
+  if (pm && pm[0] >= '0' && pm[0] <= '3' && pm[1] == 0) return pm[0] - '0';
   return HIPBLS_PAIR_AUTO;
 }
 std::atomic<int> g_pair_mode{initial_pair_mode()};
@@ -454,11 +454,21 @@ std::atomic<int> g_pair_mode{initial_pair_mode()};
 constexpr uint64_t kLg2MaxVerify = 32768;    // auto: Verify batches up to this many items take lane pairs
 constexpr uint64_t kLg2MaxWindows = 32768;   // auto: RLC sub-batches up to this many windows take lane pairs
 
+#ifndef BLS_LQ4_MAX_VERIFY
+#define BLS_LQ4_MAX_VERIFY 16384  // profiles/r03_pair_sweep_quads.txt: quads win up to 16,384 items (one round of waves)
+#endif
+constexpr uint64_t kLq4MaxVerify = BLS_LQ4_MAX_VERIFY;  // auto: Verify-shaped batches up to this many take quads
+
 bool use_pairs(uint64_t units, uint64_t auto_max) {
   const int mode = g_pair_mode.load();
   if (mode == HIPBLS_PAIR_SINGLE) return false;
-  if (mode == HIPBLS_PAIR_LANES) return true;
+  if (mode == HIPBLS_PAIR_LANES || mode == HIPBLS_PAIR_QUADS) return true;
   return units <= auto_max;
+}
+bool use_quads(uint64_t n) {
+  const int mode = g_pair_mode.load();
+  if (mode == HIPBLS_PAIR_QUADS) return true;
+  return mode == HIPBLS_PAIR_AUTO && n <= kLq4MaxVerify;
 }
 
 // Verify: fused (one lane per item) or prep + lane-pair check; `ws` is the caller's SoA workspace for the latter
@@ -478,6 +488,11 @@ int launch_verify(Context& c, const uint8_t* d_pks, const uint8_t* d_msgs, const
                        d_msgs, d_offs, d_sigs, n, (uint32_t*)ws.p, d_status, pair_hash);
   });
   if (rc) return rc;
+  if (use_quads(n))
+    return timed(c, "verify_pair_lq4", s, [&] {
+      hipLaunchKernelGGL(k_verify_pair_lq4, dim3((unsigned)grid_for(4 * n)), dim3(kBlock), 0, s,
+                         (const uint32_t*)ws.p, n, d_status);
+    });
   return timed(c, "verify_pair_lg2", s, [&] {
     hipLaunchKernelGGL(k_verify_pair_lg2, dim3((unsigned)grid_for(2 * n)), dim3(kBlock), 0, s,
                        (const uint32_t*)ws.p, n, d_status);
@@ -903,7 +918,12 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
   hipLaunchKernelGGL(k_tv_join, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s, n_groups,
                      (const int32_t*)d_astatus, (const int32_t*)agg_inf, d_vstatus);
   HIP_TRY(hipGetLastError());
-  if (use_pairs(n_groups, kLg2MaxVerify))
+  if (use_quads(n_groups))
+    rc = timed(c, "verify_pair_lq4", s, [&] {
+      hipLaunchKernelGGL(k_verify_pair_lq4, dim3((unsigned)grid_for(4 * n_groups)), dim3(kBlock), 0, s,
+                         (const uint32_t*)ws, n_groups, d_vstatus);
+    });
+  else if (use_pairs(n_groups, kLg2MaxVerify))
     rc = timed(c, "verify_pair_lg2", s, [&] {
       hipLaunchKernelGGL(k_verify_pair_lg2, dim3((unsigned)grid_for(2 * n_groups)), dim3(kBlock), 0, s,
                          (const uint32_t*)ws, n_groups, d_vstatus);
@@ -1767,7 +1787,7 @@ int hipbls_rlc_batch_stats(uint64_t* attempted, uint64_t* passed, int32_t* last)
 }
 
 int hipbls_set_pair_mode(int mode) {
-  if (mode != HIPBLS_PAIR_AUTO && mode != HIPBLS_PAIR_SINGLE && mode != HIPBLS_PAIR_LANES)
+  if (mode != HIPBLS_PAIR_AUTO && mode != HIPBLS_PAIR_SINGLE && mode != HIPBLS_PAIR_LANES && mode != HIPBLS_PAIR_QUADS)
     return arg_err("unknown pair mode");
   return g_pair_mode.exchange(mode);
 }

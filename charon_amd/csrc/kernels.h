@@ -118,6 +118,23 @@ __global__ void __launch_bounds__(kBlock) k_verify_pair_lg2(const uint32_t* __re
   if (!m) status[i] = !sig_in_g2 ? HIPBLS_ERR_SIGNATURE : (ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY);
 }
 
+// Stage 2 on a lane quad per item (lg2.h lq4_verify): lanes 4i, 4i+1 split e(pk, H(m))'s Miller loop, lanes 4i+2,
+// 4i+3 e(-g1, sig)'s, then the split final exponentiation.  Same statuses as k_verify_pair_lg2.
+__global__ void __launch_bounds__(kBlock) k_verify_pair_lq4(const uint32_t* __restrict__ ws, uint64_t n,
+                                                            int32_t* __restrict__ status) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t i = t >> 2;
+  const int q = (int)(t & 3);
+  if (i >= n || status[i] != RLC_PENDING) return;  // same decision on all four lanes of the quad
+  g1a pk;
+  g2a hm, sig;
+  soa_load<24>(&pk.x.v[0], ws, n, i);
+  soa_load<48>(&hm.x.c0.v[0], ws + 24 * n, n, i);
+  soa_load<48>(&sig.x.c0.v[0], ws + 72 * n, n, i);
+  const int st = lq4_verify(pk, hm, sig, q);
+  if (q == 0) status[i] = st;
+}
+
 __global__ void __launch_bounds__(kBlock) k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restrict__ msgs,
                                                  const uint64_t* __restrict__ offs, uint64_t n,
                                                  uint8_t* __restrict__ out, int32_t* __restrict__ status) {

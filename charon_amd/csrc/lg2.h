@@ -9,8 +9,12 @@
 //     per dword, no LDS), which need both lanes of a pair active: every exchange sits in pair-uniform control flow.
 //   * The final exponentiation runs on the split value: each lane computes its own half of every product
 //     (Fp12 products: two Fp6 products per lane, schoolbook; the exponentiations by |x| as Karabina's compressed
-//     squarings with three Fp2 squarings per lane instead of six), so its latency is roughly halved.  The inversion of the easy part is computed redundantly
-//     on both lanes from the gathered value.
+//     squarings with three Fp2 squarings per lane instead of six), so its latency is roughly halved.  The
+//     inversion of the easy part is computed redundantly on both lanes from the gathered value.
+//   * Lane quads (miller_loop_split, lq4_verify): for batches that leave lanes idle, ONE Miller loop is split across
+//     a pair (the Fp12 squaring and line products halved, the point steps redundant), and a quad runs a Verify's
+//     two loops on its two pairs: n = 1 Verify 23.8 -> 20.7 ms, C3 359k -> 411k aggregates/s
+//     (profiles/r03_pair_sweep_quads.txt, r03_c3_quads.json).
 //
 // Semantics are those of pairing_check_verify / the RLC checks (ops.h, rlc.h): the same formulas, the same e^3
 // final exponentiation, so a split check and a single-lane check accept exactly the same inputs.  Device-only
@@ -371,6 +375,114 @@ static __device__ bool lg2_finish(const fp12& f, uint32_t m) {
   fp12h_mul_full(h, fe, fo, m);
   final_exponentiation_split(e, h, m);
   return fp12h_is_one(e, m);
+}
+
+// ---------------------------------------------------------------- one Miller loop split across a lane pair
+// f_{|x|, Q}(P) (miller_loop_multi<1>: the same steps, the same f) held split as above (even lane c0, odd lane c1).
+// Both lanes carry the same T and run the same doubling/addition steps (the point arithmetic and its lines are
+// computed redundantly); the Fp12 work, which is 3/4 of a step, is split:
+//   * squaring: f = a + b w, f^2 = ((a + b)(a + v b) - t - v t) + 2 t w with t = a b: the even lane forms the first
+//     product, the odd lane t, one exchange brings t to the even lane -- one Fp6 product per lane instead of two;
+//   * line: l = (g0 + g1 v) + (h1 v) w, f l = (a L0 + v b L1) + (a L1 + b L0) w: the even lane computes a L0 and
+//     b L1, the odd lane b L0 and a L1 (5 + 3 Fp2 products per lane instead of 13).
+// A step costs ~55 products of latency instead of 100.  Both lanes must call it together with the same P, Q.
+__device__ __forceinline__ void fp12h_sqr_split(fp6& h, uint32_t m) {
+  fp6 o;
+  pair_swap(o, h);
+  const fp6 a = sel(m, o, h), b = sel(m, h, o);
+  fp6 s0, vb, s1;
+  fp6_add(s0, a, b);
+  fp6_mul_v(vb, b);
+  fp6_add(s1, a, vb);
+  const fp6 x = sel(m, a, s0), y = sel(m, b, s1);  // odd: a b | even: (a + b)(a + v b)
+  fp6 p;
+  fp6_mul(p, x, y);
+  fp6 t;
+  pair_swap(t, p);  // even receives t = a b
+  fp6 vt, c0, c1;
+  fp6_mul_v(vt, t);
+  fp6_sub(c0, p, t);
+  fp6_sub(c0, c0, vt);
+  fp6_add(c1, p, p);
+  h = sel(m, c1, c0);
+}
+__device__ __forceinline__ void fp12h_mul_line_split(fp6& h, const fp2& g0, const fp2& g1, const fp2& h1, uint32_t m) {
+  fp6 o;
+  pair_swap(o, h);
+  const fp6 a = sel(m, o, h), b = sel(m, h, o);
+  const fp6 x = sel(m, b, a), y = sel(m, a, b);
+  fp6 t0, t1, vt1, r;
+  fp6_mul_01(t0, x, g0, g1);  // even a L0 | odd b L0
+  fp6_mul_1(t1, y, h1);       // even b h1 v | odd a h1 v
+  fp6_mul_v(vt1, t1);
+  fp6_add(r, t0, sel(m, t1, vt1));
+  h = r;
+}
+BLS_CALL __device__ void miller_loop_split(fp6& h_out, const g1a& P_in, const g2a& Q_in, uint32_t m,
+                                           g2j* T_out = nullptr) {
+  const g1a P = P_in;
+  const g2a Q = Q_in;
+  g2j T;
+  T.x = Q.x;
+  T.y = Q.y;
+  fp2_set_one(T.z);
+  fp6 one6, zero6, h;
+  fp6_set_one(one6);
+  fp6_set_zero(zero6);
+  h = sel(m, zero6, one6);
+  for (int bit = 62; bit >= 0; --bit) {
+    if (bit != 62) fp12h_sqr_split(h, m);
+    fp2 g0, g1, h1;
+    miller_dbl_step_inl(T, g0, g1, h1, P.x, P.y);
+    fp12h_mul_line_split(h, g0, g1, h1, m);
+    if ((X_ABS >> bit) & 1ull) {
+      miller_add_step_inl(T, g0, g1, h1, Q, P.x, P.y);
+      fp12h_mul_line_split(h, g0, g1, h1, m);
+    }
+  }
+  fp12h_conj(h_out, h, m);
+  if (T_out) *T_out = T;
+}
+
+// Partner lane across the two pairs of a quad (lane ^ 2).  All four lanes must be active.
+__device__ __forceinline__ uint32_t quad_swap(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E /* quad_perm [2,3,0,1] */, 0xF, 0xF, false);
+#else
+  return v;
+#endif
+}
+
+// Verify's pairing check on a lane quad: lanes 0, 1 run e(pk, H(m))'s Miller loop split, lanes 2, 3 e(-g1, sig)'s;
+// the quad forms the product's halves (each pair multiplies its split value by the other pair's, the same
+// product on both pairs) and both pairs run the split final exponentiation.  The signature's G2 membership comes
+// from the second pair's T (g2_subgroup_from_miller).  Returns HIPBLS_OK / _ERR_SIGNATURE / _ERR_VERIFY on every
+// lane of the quad.  q = lane index within the quad.
+__device__ int lq4_verify(const g1a& pk, const g2a& hm, const g2a& sig, int q) {
+  const uint32_t m = (q & 1) ? ~0u : 0u;
+  const bool second = q >= 2;
+  g1a P;
+  g2a Q;
+  if (second) {
+    P.x = G1_GEN_X;
+    P.y = G1_NEG_GEN_Y;
+    Q = sig;
+  } else {
+    P = pk;
+    Q = hm;
+  }
+  fp6 h;
+  g2j T;
+  miller_loop_split(h, P, Q, m, &T);
+  const uint32_t mine = g2_subgroup_from_miller(T, Q) ? 1u : 0u;  // meaningful on the second pair
+  const uint32_t other = quad_swap(mine);
+  const uint32_t sig_in_g2 = second ? mine : other;
+  fp6 ho, r, e;
+  for (int k = 0; k < 72; ++k) (&ho.c0.c0.v[0])[k] = quad_swap((&h.c0.c0.v[0])[k]);
+  fp12h_mul(r, h, ho, m);
+  final_exponentiation_split(e, r, m);
+  const bool ok = fp12h_is_one(e, m);
+  return !sig_in_g2 ? HIPBLS_ERR_SIGNATURE : (ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY);
 }
 
 template <int MAXN>

@@ -19,9 +19,9 @@ def main():
     import torch
 
     import bench
-    from charon_amd.tbls import PAIR_LANES, PAIR_SINGLE, HipBLS, load_library
+    from charon_amd.tbls import PAIR_LANES, PAIR_QUADS, PAIR_SINGLE, HipBLS, load_library
     sizes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else
-                              "1,64,1024,4096,10000,16384,24576,32768,49152,65536").split(",")]
+                              "1,64,1024,4096,10000,16384,24576,32768").split(",")]
     dev = torch.device("cuda", 0)
     impl = HipBLS(device=0)
     lib = load_library()
@@ -35,7 +35,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     rows = []
     for n in sizes:
-        for mode, name in ((PAIR_SINGLE, "single"), (PAIR_LANES, "lanes")):
+        for mode, name in ((PAIR_SINGLE, "single"), (PAIR_LANES, "lanes"), (PAIR_QUADS, "quads")):
             impl.set_pair_mode(mode)
             reps = 3 if n >= 4096 else 10
 

@@ -61,7 +61,7 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 9
+#define HIPBLS_ABI_VERSION 10
 int hipbls_abi_version(void);
 
 /* Bind the library to the n devices ids[0..n) (n <= 64; a device may repeat: each entry is one context, e.g. to
@@ -88,11 +88,13 @@ int hipbls_current_device(void);
 int hipbls_set_timing(int enabled);
 /* Pairing-check layout.  HIPBLS_PAIR_SINGLE: one lane per check.  HIPBLS_PAIR_LANES: a lane pair per check (the
  * two Miller loops side by side, the final exponentiation split across the pair; about half the latency, twice
- * the lanes).  HIPBLS_PAIR_AUTO (default): lane pairs for batches that leave lanes idle (Verify up to 32,768
- * items, RLC sub-batches up to 32,768 windows, every RLC fallback list and FastAggregateVerify).  Results are
- * identical in every mode.  Returns the previous mode, or HIPBLS_ERR_ARG for an unknown one.  The environment
- * variable HIPBLS_PAIR_MODE (0/1/2) sets the initial mode. */
-enum { HIPBLS_PAIR_AUTO = 0, HIPBLS_PAIR_SINGLE = 1, HIPBLS_PAIR_LANES = 2 };
+ * the lanes).  HIPBLS_PAIR_QUADS: four lanes per Verify-shaped check (each Miller loop split across a lane pair,
+ * the two pairs side by side; RLC windows keep lane pairs).  HIPBLS_PAIR_AUTO (default): the widest layout the
+ * batch leaves lanes for (Verify: quads up to the quad limit, then pairs up to 32,768 items; RLC sub-batches up to
+ * 32,768 windows, every RLC fallback list and FastAggregateVerify on pairs).  Results are identical in every mode.
+ * Returns the previous mode, or HIPBLS_ERR_ARG for an unknown one.  The environment variable HIPBLS_PAIR_MODE
+ * (0/1/2/3) sets the initial mode. */
+enum { HIPBLS_PAIR_AUTO = 0, HIPBLS_PAIR_SINGLE = 1, HIPBLS_PAIR_LANES = 2, HIPBLS_PAIR_QUADS = 3 };
 int hipbls_set_pair_mode(int mode);
 
 /* ------------------------------------------------ single-item Verify through the submission queue ---- */

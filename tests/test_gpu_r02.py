@@ -417,7 +417,8 @@ def test_cluster_locks_bulk_verify(impl, kat):
 
 
 # ---------------------------------------------------------------- sigagg in one call (sigagg.go:138-159)
-def test_threshold_aggregate_verify_fused_equals_two_calls(impl):
+@pytest.mark.parametrize("layout", ["auto", "quads"])
+def test_threshold_aggregate_verify_fused_equals_two_calls(impl, layout):
     """hipbls_threshold_aggregate_verify_batch == batch_threshold_aggregate + batch_verify_status of the
     aggregates, on honest groups, a failing aggregation (id 0, bad partial), a wrong root key, a wrong message,
     an identity root key and an all-infinity group (aggregate at infinity)."""
@@ -452,7 +453,12 @@ def test_threshold_aggregate_verify_fused_equals_two_calls(impl):
     bad_pk = bytearray(dvpks[10])
     bad_pk[0] &= 0x7F
     dvpks[10] = bytes(bad_pk)                                                           # undecodable root key
-    res, vst = impl.batch_threshold_aggregate_verify(groups, dvpks, msgs)
+    from charon_amd.tbls import PAIR_AUTO, PAIR_QUADS
+    prev = impl.set_pair_mode(PAIR_QUADS if layout == "quads" else PAIR_AUTO)
+    try:
+        res, vst = impl.batch_threshold_aggregate_verify(groups, dvpks, msgs)
+    finally:
+        impl.set_pair_mode(prev)
     want_res = impl.batch_threshold_aggregate(groups)
     assert [r if isinstance(r, bytes) else str(r) for r in res] == \
         [r if isinstance(r, bytes) else str(r) for r in want_res]

@@ -62,10 +62,10 @@ def _padded(impl, so, n_honest, seed):
     return [list(x) for x in zip(*items)]
 
 
-@pytest.mark.parametrize("mode", ["auto", "single", "lanes"])
+@pytest.mark.parametrize("mode", ["auto", "single", "lanes", "quads"])
 def test_small_order_batch_verify_every_layout(impl, so, mode):
-    from charon_amd.tbls import PAIR_AUTO, PAIR_LANES, PAIR_SINGLE
-    m = {"auto": PAIR_AUTO, "single": PAIR_SINGLE, "lanes": PAIR_LANES}[mode]
+    from charon_amd.tbls import PAIR_AUTO, PAIR_LANES, PAIR_QUADS, PAIR_SINGLE
+    m = {"auto": PAIR_AUTO, "single": PAIR_SINGLE, "lanes": PAIR_LANES, "quads": PAIR_QUADS}[mode]
     pks, msgs, sigs, want = _cases(so)
     prev = impl.set_pair_mode(m)
     try:
