@@ -555,7 +555,9 @@ def main():
                                                              "rlcb_mark")),
                             "stage_frac": stage_fracs(lib, {
                                 "rlc_items": RLC_FPMUL["item"] * n4, "rlc_hash": RLC_FPMUL["hash"] * len(roots4),
-                                "rlc_window": per_win * w.value, "rlc_window_lg2": per_win * w.value,
+                                # windows and fallback do nothing once the batch-wide check has passed
+                                "rlc_window": 0 if b_pass1 > b_pass0 else per_win * w.value,
+                                "rlc_window_lg2": 0 if b_pass1 > b_pass0 else per_win * w.value,
                                 "rlc_fallback": RLC_FPMUL["fallback"] * fb.value,
                                 "rlc_fallback_lg2": RLC_FPMUL["fallback"] * fb.value,
                                 "rlcb_items": RLCB_FPMUL["item"] * n4,

@@ -522,6 +522,36 @@ rlc_seed parse_seed(const uint8_t* seed32) {
   return seed;
 }
 
+// RLC stage 4 over a device-side list of at most `cap` items (its length is only known on the device): AUTO launches
+// both layouts and each kernel takes the lists on its side of the crossover -- lane pairs while the `concurrent`
+// lists running side by side fit one round of waves (1024 waves x 64 lanes / 2 per item), one lane per item above.
+// The pair kernel's grid covers only the lists it can take, so when it stands aside it costs a few hundred
+// workgroups that exit at once.
+constexpr uint64_t kLg2FallbackLanes = 32768;
+int launch_fallback(Context& c, hipStream_t s, const uint32_t* list, const uint32_t* cnt, uint64_t cap,
+                    uint64_t concurrent, const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx,
+                    const uint32_t* d_H, uint64_t hstride, const uint32_t* d_hslot, int32_t* d_status,
+                    const uint32_t* d_kidx, uint64_t T, const uint32_t* tab) {
+  const int mode = g_pair_mode.load();
+  const uint64_t pair_upto = mode == HIPBLS_PAIR_SINGLE ? 0
+                             : (mode == HIPBLS_PAIR_AUTO ? kLg2FallbackLanes / (concurrent ? concurrent : 1)
+                                                         : ~(uint64_t)0);
+  const uint64_t pairs = cap < pair_upto ? cap : pair_upto;
+  int rc = HIPBLS_OK;
+  if (pairs > 0)
+    rc = timed(c, "rlc_fallback_lg2", s, [&] {
+      hipLaunchKernelGGL(k_rlc_fallback_lg2, dim3((unsigned)grid_for(2 * pairs)), dim3(kBlock), 0, s, list, cnt, cap,
+                         d_pks, d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab, pair_upto);
+    });
+  if (rc) return rc;
+  if (pair_upto < cap)
+    rc = timed(c, "rlc_fallback", s, [&] {
+      hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(cap)), dim3(kBlock), 0, s, list, cnt, cap, d_pks,
+                         d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab, pair_upto);
+    });
+  return rc;
+}
+
 // RLC BatchVerify: the batch is cut into up to kSub window-aligned sub-batches, each running items -> window ->
 // fallback on its own stream, while the distinct messages are hashed on the caller's stream; windows wait only
 // for the hash.  Every stage is latency-bound on its own (one lane per item at one wave per SIMD), so overlapping
@@ -612,18 +642,8 @@ int launch_rlc(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const ui
     if (rc) return rc;
     // The list length is only known on the device: launch for the worst case, idle lanes exit.  The list is short
     // (failed windows only) and latency-bound, so lane pairs unless the caller forced single lanes.
-    if (g_pair_mode.load() != HIPBLS_PAIR_SINGLE)
-      rc = timed(c, "rlc_fallback_lg2", ss, [&] {
-        hipLaunchKernelGGL(k_rlc_fallback_lg2, dim3((unsigned)grid_for(2 * (i1 - i0))), dim3(kBlock), 0, ss,
-                           (const uint32_t*)(list + i0), (const uint32_t*)(cnt + k), i1 - i0, d_pks, d_sigs, d_midx,
-                           (const uint32_t*)d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
-      });
-    else
-      rc = timed(c, "rlc_fallback", ss, [&] {
-        hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(i1 - i0)), dim3(kBlock), 0, ss,
-                           (const uint32_t*)(list + i0), (const uint32_t*)(cnt + k), i1 - i0, d_pks, d_sigs, d_midx,
-                           (const uint32_t*)d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
-      });
+    rc = launch_fallback(c, ss, list + i0, cnt + k, i1 - i0, nsub, d_pks, d_sigs, d_midx, d_H, hstride, d_hslot,
+                         d_status, d_kidx, T, tab);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c.ev_join[k], ss));
     HIP_TRY(hipStreamWaitEvent(s, c.ev_join[k], 0));
@@ -820,18 +840,7 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
                          d_status, win, list, cnt);
     });
   if (rc) return rc;
-  if (g_pair_mode.load() != HIPBLS_PAIR_SINGLE)
-    rc = timed(c, "rlc_fallback_lg2", s, [&] {
-      hipLaunchKernelGGL(k_rlc_fallback_lg2, dim3((unsigned)grid_for(2 * n)), dim3(kBlock), 0, s,
-                         (const uint32_t*)list, (const uint32_t*)cnt, n, d_pks, d_sigs, d_midx, (const uint32_t*)d_H,
-                         hstride, d_hslot, d_status, d_kidx, T, tab);
-    });
-  else
-    rc = timed(c, "rlc_fallback", s, [&] {
-      hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, (const uint32_t*)list,
-                         (const uint32_t*)cnt, n, d_pks, d_sigs, d_midx, (const uint32_t*)d_H, hstride, d_hslot,
-                         d_status, d_kidx, T, tab);
-    });
+  rc = launch_fallback(c, s, list, cnt, n, 1, d_pks, d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
   if (rc) return rc;
   c.r_windows = n_win;
   return ws_end(c, s);

@@ -775,6 +775,10 @@ __global__ void __launch_bounds__(kBlock) k_rlc_window_lg2(uint64_t w0, uint64_t
 }
 
 // Stage 4: items of failed windows (dense list) are checked one by one (rlc_fallback_lane).
+// Stage 4 over the list of failed-window items: the bare 2-pair check per item.  The list length is known only on
+// the device, so the host launches both layouts (one lane per item here, a lane pair per item below) and each kernel
+// takes the lists on its side of pair_upto: pairs halve a check's latency while the list leaves lanes idle, one lane
+// per item wins once pairs would need a second round of waves.  Same verdicts either way.
 __global__ void __launch_bounds__(kBlock) k_rlc_fallback(const uint32_t* __restrict__ list,
                                                          const uint32_t* __restrict__ list_len, uint64_t cap,
                                                          const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
@@ -783,15 +787,16 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback(const uint32_t* __restr
                                                          const uint32_t* __restrict__ hslot,
                                                          int32_t* __restrict__ status,
                                                          const uint32_t* __restrict__ key_idx, uint64_t T,
-                                                         const uint32_t* __restrict__ tab) {
+                                                         const uint32_t* __restrict__ tab, uint64_t pair_upto) {
   const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t len = *list_len;
+  if (len <= pair_upto) return;  // k_rlc_fallback_lg2 takes short lists
   if (j >= len || j >= cap) return;
   rlc_fallback_lane(list[j], pks, sigs, msg_idx, H, hstride, hslot, status, key_idx, T, tab);
 }
 
-// Stage 4 on lane pairs (lg2.h): the even lane decodes the key and takes e(pk, H(m)), the odd lane decodes the
-// signature and takes e(-g1, sig); the final exponentiation is split.  Same verdicts as k_rlc_fallback.
+// The lane-pair layout (lg2.h): the even lane decodes the key and takes e(pk, H(m)), the odd lane decodes the
+// signature and takes e(-g1, sig); the final exponentiation is split.
 __global__ void __launch_bounds__(kBlock) k_rlc_fallback_lg2(const uint32_t* __restrict__ list,
                                                              const uint32_t* __restrict__ list_len, uint64_t cap,
                                                              const uint8_t* __restrict__ pks,
@@ -801,11 +806,12 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback_lg2(const uint32_t* __r
                                                              const uint32_t* __restrict__ hslot,
                                                              int32_t* __restrict__ status,
                                                              const uint32_t* __restrict__ key_idx, uint64_t T,
-                                                             const uint32_t* __restrict__ tab) {
+                                                             const uint32_t* __restrict__ tab, uint64_t pair_upto) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t j = t >> 1;
   const uint32_t m = (t & 1) ? ~0u : 0u;
   const uint64_t len = *list_len;
+  if (len > pair_upto) return;  // a long list fills the GPU one lane per item (k_rlc_fallback)
   if (j >= len || j >= cap) return;
   const uint64_t i = list[j];
   if (status[i] != RLC_PENDING) return;
