@@ -198,7 +198,7 @@ def c4_node_bad(tag, v_node, nk, shares=4, corrupt=True):
     return {v * shares + j for v in range(v_node) for j in range(shares) if c4_item(tag, v, j, nk, corrupt)[1]}
 
 
-def pmc_summary(path=os.path.join(ROOT, "profiles", "r02_pmc_verify.json")):
+def pmc_summary(path=os.path.join(ROOT, "profiles", "r03_pmc_verify.json")):
     """k_verify_fused counters from the committed rocprofv3 --pmc passes over this build's bench (scripts/gpu_pmc.sh,
     scripts/pmc_summary.py): HBM bytes per launch (FETCH_SIZE + WRITE_SIZE), their ratio to the 188 B/verify of
     algorithmic input, VALU utilisation (SQ_ACTIVE_INST_VALU / SQ_BUSY_CYCLES per SIMD) and the fraction of wave
