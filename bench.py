@@ -632,11 +632,15 @@ def main():
                    + 4 * (shard_range(32, r, world)[1] - shard_range(32, r, world)[0]) for r in range(world)]
         c5_max = max(c5_rows)
 
+        c5_fav = os.environ.get("BENCH_C5_FAV", "1") == "1"  # 0: the RLC part alone (A/B of the overlap)
+        s_fav = torch.cuda.Stream(device=dev)  # a stream of its own: on the RLC's stream it would run before it
+        sp_fav = ctypes.c_void_p(s_fav.cuda_stream)
+
         def c5step():
-            if rank == 0:  # on the library's own stream (NULL), overlapping the RLC
+            if rank == 0 and c5_fav:  # on its own stream, overlapping the RLC
                 rc = lib.hipbls_verify_aggregate_batch_device(d_spk.data_ptr(), 512, d_skoff.data_ptr(), 1,
                                                               d_ssig.data_ptr(), d_smsg.data_ptr(), d_smoff.data_ptr(),
-                                                              d_sst.data_ptr(), None)
+                                                              d_sst.data_ptr(), sp_fav)
                 assert rc == 0
             rc = lib.hipbls_batch_verify_rlc_device(d_pk5.data_ptr(), d_sig5.data_ptr(), d_midx5.data_ptr(), n5,
                                                     d_msg5.data_ptr(), d_off5.data_ptr(), len(roots5), seed5,
@@ -650,7 +654,7 @@ def main():
         t5 = timed_loop(c5step, args.rlc_steps, dev, barrier, world)
         torch.cuda.synchronize()
         assert {i for i, x in enumerate(d_st5.cpu().tolist()) if x != 0} == bad5, "C5 bitmap mismatch"
-        if rank == 0:
+        if rank == 0 and c5_fav:
             assert d_sst.cpu().tolist() == [0], "sync-committee FastAggregateVerify failed"
         if world > 1:  # node-wide failure count == construction
             rows = node5[0]

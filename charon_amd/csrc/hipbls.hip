@@ -144,7 +144,10 @@ struct Context {
   static constexpr int kSub = 2;
   hipStream_t sub[kSub] = {};
   hipEvent_t ev_fork = nullptr, ev_hash = nullptr, ev_join[kSub] = {};
-  hipEvent_t ws_done = nullptr;  // last workspace user's completion (cross-stream ordering)
+  // Last workspace user's completion (cross-stream ordering), per workspace group: the general buffers (b_*, v_ws) and
+  // the RLC ones (r_*, m_*, the H(m) cache), so an RLC batch and, say, a FastAggregateVerify on another stream (the C5
+  // slot mix) overlap instead of queueing behind each other.
+  hipEvent_t ws_done = nullptr, ws_done_rlc = nullptr;
   uint64_t r_windows = 0;        // window count of this context's last RLC call (hipbls_rlc_stats)
   uint64_t r_call = 0;           // entry-point call that call belonged to
   // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
@@ -211,6 +214,7 @@ int init_locked(const std::vector<int>& ids) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ws_done_rlc, hipEventDisableTiming));
     made.push_back(c);
   }
   const char* t = getenv("HIPBLS_TIMING");
@@ -292,12 +296,13 @@ Context& ctx_of(const void* p) {
 hipStream_t pick(Context& c, void* stream) { return stream ? (hipStream_t)stream : c.stream; }
 
 // Workspace ordering: the call's stream waits for the previous workspace user, and publishes its own end.
-int ws_begin(Context& c, hipStream_t s) {
-  HIP_TRY(hipStreamWaitEvent(s, c.ws_done, 0));
+enum { WS_GEN = 0, WS_RLC = 1 };
+int ws_begin(Context& c, hipStream_t s, int group = WS_GEN) {
+  HIP_TRY(hipStreamWaitEvent(s, group == WS_RLC ? c.ws_done_rlc : c.ws_done, 0));
   return HIPBLS_OK;
 }
-int ws_end(Context& c, hipStream_t s) {
-  HIP_TRY(hipEventRecord(c.ws_done, s));
+int ws_end(Context& c, hipStream_t s, int group = WS_GEN) {
+  HIP_TRY(hipEventRecord(group == WS_RLC ? c.ws_done_rlc : c.ws_done, s));
   return HIPBLS_OK;
 }
 
@@ -603,7 +608,7 @@ int launch_rlc(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const ui
   if (nsub < 1) nsub = 1;
   const uint64_t win_per = (n_win + nsub - 1) / nsub;
 
-  rc = ws_begin(c, s);
+  rc = ws_begin(c, s, WS_RLC);
   if (rc) return rc;
   HIP_TRY(hipMemsetAsync(cnt, 0, Context::kSub * 4, s));
   HIP_TRY(hipEventRecord(c.ev_fork, s));
@@ -649,7 +654,7 @@ int launch_rlc(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const ui
     HIP_TRY(hipStreamWaitEvent(s, c.ev_join[k], 0));
   }
   c.r_windows = n_win;
-  return ws_end(c, s);
+  return ws_end(c, s, WS_RLC);
 }
 
 // ============================================================================ batch-wide RLC check (rlcb.h)
@@ -745,7 +750,7 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   // queued behind it waits that long (round 2: k_msm_scan 33 ms beside k_rlcb_chunks 37.7 ms).  s joins for the
   // verdict and the window stages.
   hipStream_t s0 = c.sub[0], s1 = c.sub[1];
-  rc = ws_begin(c, s);
+  rc = ws_begin(c, s, WS_RLC);
   if (rc) return rc;
   HIP_TRY(hipMemsetAsync(c.m_cnt.p, 0, (size_t)MSM_WINDOWS * MSM_NB * 4, s));
   HIP_TRY(hipMemsetAsync(c.r_cnt.p, 0, 4, s));
@@ -843,7 +848,7 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   rc = launch_fallback(c, s, list, cnt, n, 1, d_pks, d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
   if (rc) return rc;
   c.r_windows = n_win;
-  return ws_end(c, s);
+  return ws_end(c, s, WS_RLC);
 }
 
 int launch_tagg(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, const uint64_t* d_goffs, uint64_t n_groups,
@@ -1085,7 +1090,7 @@ int rlc_host_on(Context& c, RlcBufs B, hipStream_t s, const uint8_t* pks, const 
     HIP_TRY(B.slot->ensure((n_msgs ? n_msgs : 1) * 4));
     HIP_TRY(B.mlist->ensure((miss.size() ? miss.size() : 1) * 4));
     // the copies run on s behind every earlier workspace user (ws_done): the slot table is per call
-    int rc = ws_begin(c, s);
+    int rc = ws_begin(c, s, WS_RLC);
     if (rc) return rc;
     if (n_msgs) HIP_TRY(hipMemcpyAsync(B.slot->p, slot.data(), n_msgs * 4, hipMemcpyHostToDevice, s));
     if (miss.size()) HIP_TRY(hipMemcpyAsync(B.mlist->p, miss.data(), miss.size() * 4, hipMemcpyHostToDevice, s));
