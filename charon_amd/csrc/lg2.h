@@ -453,6 +453,186 @@ __device__ __forceinline__ uint32_t quad_swap(uint32_t v) {
 #endif
 }
 
+// ---------------------------------------------------------------- the final exponentiation on a lane quad
+// The value is held in full on all four lanes (bit-identical), and the work of each step is dealt out:
+//   * Fp12 product: lane q computes one of the four Fp6 products of the schoolbook form (a0 b0, a1 b1, a0 b1, a1 b0),
+//     the pairs combine theirs into c0 = a0 b0 + v a1 b1 (lanes 0, 1) and c1 = a0 b1 + a1 b0 (lanes 2, 3), and one
+//     exchange across the pairs gives every lane both halves: one Fp6 product per lane instead of two on a pair;
+//   * Karabina's compressed squaring: its six Fp2 squarings as two rounds of four (z2 | z3 | z4 | z5, then
+//     z2 + z3 | z4 + z5 on lanes 0, 1), each result broadcast to the quad: two squarings of latency instead of three.
+// Everything else (decompression, the easy part's inversion, Frobenius maps) runs redundantly on all lanes on the
+// same data, so every branch is quad-uniform (DPP needs all four lanes).
+template <int SRC>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, SRC * 0x55 /* quad_perm [SRC,SRC,SRC,SRC] */, 0xF, 0xF, false);
+#else
+  return v;
+#endif
+}
+template <int SRC>
+__device__ __forceinline__ fp2 quad_bcast(const fp2& s) {
+  fp2 d;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) (&d.c0.v[0])[i] = quad_bcast<SRC>((&s.c0.v[0])[i]);
+  return d;
+}
+__device__ __forceinline__ void quad_swap(fp6& d, const fp6& s) {
+#pragma unroll
+  for (int i = 0; i < 72; ++i) (&d.c0.c0.v[0])[i] = quad_swap((&s.c0.c0.v[0])[i]);
+}
+struct quad_m {  // lane masks within the quad (q = lane & 3)
+  uint32_t odd, hi, cross;  // q & 1, q >= 2, q in {1, 2}
+  __device__ explicit quad_m(int q)
+      : odd((q & 1) ? ~0u : 0u), hi((q & 2) ? ~0u : 0u), cross(((q ^ (q >> 1)) & 1) ? ~0u : 0u) {}
+};
+
+BLS_CALL __device__ void fp12q_mul(fp12& r, const fp12& a_in, const fp12& b_in, const quad_m& qm) {
+  const fp12 a = a_in, b = b_in;
+  const fp6 x = sel(qm.odd, a.c1, a.c0);    // a0 | a1 | a0 | a1
+  const fp6 y = sel(qm.cross, b.c1, b.c0);  // b0 | b1 | b1 | b0
+  fp6 p, o, vp, vo, t0, t1, t2;
+  fp6_mul(p, x, y);
+  pair_swap(o, p);
+  fp6_mul_v(vp, p);
+  fp6_mul_v(vo, o);
+  fp6_add(t0, p, vo);  // lane 0: a0 b0 + v a1 b1
+  fp6_add(t1, o, vp);  // lane 1: the same sum
+  fp6_add(t2, p, o);   // lanes 2, 3: a0 b1 + a1 b0
+  const fp6 mine = sel(qm.hi, t2, sel(qm.odd, t1, t0));
+  fp6 other;
+  quad_swap(other, mine);
+  r.c0 = sel(qm.hi, other, mine);
+  r.c1 = sel(qm.hi, mine, other);
+}
+
+__device__ __forceinline__ void cyc_sqr_compressed_quad(cyc_c& c, const quad_m& qm) {
+  // round 1: z2 | z3 | z4 | z5
+  const fp2 xa = sel(qm.hi, sel(qm.odd, c.z5, c.z4), sel(qm.odd, c.z3, c.z2));
+  // round 2: z2 + z3 | z4 + z5 (lanes 2, 3 repeat lanes 0, 1)
+  fp2 s23, s45;  // canonical: the squaring routine forms a0 + p - a1
+  fp2_add(s23, c.z2, c.z3);
+  fp2_add(s45, c.z4, c.z5);
+  const fp2 xb = sel(qm.odd, s45, s23);
+  fp2 ra, rb;
+  BLS_KAR_FP2_SQR(ra, xa);
+  BLS_KAR_FP2_SQR(rb, xb);
+  const fp2 s2 = quad_bcast<0>(ra), s3 = quad_bcast<1>(ra), s4 = quad_bcast<2>(ra), s5 = quad_bcast<3>(ra);
+  fp2 u = quad_bcast<0>(rb), t = quad_bcast<1>(rb);
+  fp2 v;
+  fp2_sub(t, t, s4);
+  fp2_sub(t, t, s5);  // 2 z4 z5
+  fp2_sub(u, u, s2);
+  fp2_sub(u, u, s3);  // 2 z2 z3
+  // the new state as cyc_sqr_compressed (pairing.h)
+  fp2 q45, q23;
+  fp2_mul_xi(t, t);
+  fp2_add(v, c.z2, t);
+  fp2_add(v, v, v);
+  fp2_add(c.z2, v, t);
+  fp2_mul_xi(q45, s5);
+  fp2_add(q45, q45, s4);
+  fp2_sub(v, q45, c.z3);
+  fp2_add(v, v, v);
+  fp2_add(c.z3, v, q45);
+  fp2_mul_xi(q23, s3);
+  fp2_add(q23, q23, s2);
+  fp2_sub(v, q23, c.z4);
+  fp2_add(v, v, v);
+  fp2_add(c.z4, v, q23);
+  fp2_add(v, c.z5, u);
+  fp2_add(v, v, v);
+  fp2_add(c.z5, v, u);
+}
+
+// r = a^|x| on a quad (a in the cyclotomic subgroup, in full on every lane), pairing.h fp12_cyc_exp_xabs_karabina's
+// steps; the degenerate case (a saved power with z2 = z3 = 0) takes the one-lane Granger-Scott exponentiation on
+// every lane.
+BLS_CALL __device__ void fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, const quad_m& qm) {
+  static_assert(X_ABS == 0xd201000000010000ull, "the squaring counts below are |x|'s set bits");
+  cyc_c c;
+  c.z2 = a_in.c1.c0;
+  c.z3 = a_in.c0.c2;
+  c.z4 = a_in.c0.c1;
+  c.z5 = a_in.c1.c2;
+  cyc_c st[6];
+  int s = 0;
+#pragma unroll 1
+  for (int k = 1; k <= 63; ++k) {
+    cyc_sqr_compressed_quad(c, qm);
+    if (k == 16 || k == 48 || k == 57 || k == 60 || k == 62 || k == 63) st[s++] = c;
+  }
+  fp2 num[6], den[6], pre[6];
+#pragma unroll 1
+  for (s = 0; s < 6; ++s) cyc_z1_parts(num[s], den[s], st[s]);
+  pre[0] = den[0];
+#pragma unroll 1
+  for (s = 1; s < 6; ++s) fp2_mul(pre[s], pre[s - 1], den[s]);
+  if (fp2_is_zero(pre[5])) {  // the same on all four lanes
+    fp12_cyc_exp_xabs_gs(r, a_in);
+    return;
+  }
+  fp2 inv;
+  fp2_inv(inv, pre[5]);
+  fp12 acc;
+#pragma unroll 1
+  for (s = 5; s >= 0; --s) {
+    fp2 is, z1;
+    if (s > 0) {
+      fp2_mul(is, inv, pre[s - 1]);  // 1 / den[s]
+      fp2_mul(inv, inv, den[s]);
+    } else {
+      is = inv;
+    }
+    fp2_mul(z1, num[s], is);
+    fp12 d;
+    cyc_decompress(d, st[s], z1);
+    if (s == 5) {
+      acc = d;
+    } else {
+      fp12 x = acc, y;
+      fp12q_mul(y, x, d, qm);
+      acc = y;
+    }
+  }
+  r = acc;
+}
+
+// final_exponentiation (pairing.h) on a quad: the same formula and the same result on every lane.
+BLS_CALL __device__ void final_exponentiation_quad(fp12& r, const fp12& f_in, const quad_m& qm) {
+  const fp12 f = f_in;
+  fp12 t, fi, m;
+  fp12_conj(t, f);
+  fp12_inv(fi, f);
+  fp12q_mul(m, t, fi, qm);
+  fp12_frobenius(t, m, 2);
+  fp12q_mul(m, t, m, qm);
+  fp12 t0, t1, t2, u;
+  fp12q_exp_xabs_karabina(t0, m, qm);
+  fp12q_mul(t0, t0, m, qm);
+  fp12_conj(t0, t0);
+  fp12q_exp_xabs_karabina(u, t0, qm);
+  fp12q_mul(u, u, t0, qm);
+  fp12_conj(t0, u);
+  fp12q_exp_xabs_karabina(u, t0, qm);
+  fp12_conj(u, u);
+  fp12_frobenius(t1, t0, 1);
+  fp12q_mul(t1, t1, u, qm);
+  fp12q_exp_xabs_karabina(u, t1, qm);
+  fp12q_exp_xabs_karabina(u, u, qm);
+  fp12_frobenius(t2, t1, 2);
+  fp12q_mul(t2, t2, u, qm);
+  fp12_conj(u, t1);
+  fp12q_mul(t2, t2, u, qm);
+  fp12_cyclotomic_sqr(u, m);
+  fp12q_mul(u, u, m, qm);
+  fp12q_mul(r, t2, u, qm);
+}
+
+#ifndef BLS_LQ4_FE_QUAD
+#define BLS_LQ4_FE_QUAD 1
+#endif
+
 // Verify's pairing check on a lane quad: lanes 0, 1 run e(pk, H(m))'s Miller loop split, lanes 2, 3 e(-g1, sig)'s;
 // the quad forms the product's halves (each pair multiplies its split value by the other pair's, the same
 // product on both pairs) and both pairs run the split final exponentiation.  The signature's G2 membership comes
@@ -477,11 +657,27 @@ __device__ int lq4_verify(const g1a& pk, const g2a& hm, const g2a& sig, int q) {
   const uint32_t mine = g2_subgroup_from_miller(T, Q) ? 1u : 0u;  // meaningful on the second pair
   const uint32_t other = quad_swap(mine);
   const uint32_t sig_in_g2 = second ? mine : other;
+#if BLS_LQ4_FE_QUAD
+  // full values: this pair's loop (gathered over the pair), the other pair's (one exchange across the pairs)
+  fp12 fm, fo, f0, f1, r, e;
+  fp12h_gather(fm, h, m);
+  quad_swap(fo.c0, fm.c0);
+  quad_swap(fo.c1, fm.c1);
+  const quad_m qm(q);
+  f0.c0 = sel(qm.hi, fo.c0, fm.c0);
+  f0.c1 = sel(qm.hi, fo.c1, fm.c1);
+  f1.c0 = sel(qm.hi, fm.c0, fo.c0);
+  f1.c1 = sel(qm.hi, fm.c1, fo.c1);
+  fp12q_mul(r, f0, f1, qm);
+  final_exponentiation_quad(e, r, qm);
+  const bool ok = fp12_is_one(e);
+#else
   fp6 ho, r, e;
   for (int k = 0; k < 72; ++k) (&ho.c0.c0.v[0])[k] = quad_swap((&h.c0.c0.v[0])[k]);
   fp12h_mul(r, h, ho, m);
   final_exponentiation_split(e, r, m);
   const bool ok = fp12h_is_one(e, m);
+#endif
   return !sig_in_g2 ? HIPBLS_ERR_SIGNATURE : (ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY);
 }
 

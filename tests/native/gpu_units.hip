@@ -8,6 +8,9 @@
 //                       fp12h_exp_xabs with DPP exchanges), reached when a saved compressed power has z2 = z3 = 0,
 //                       e.g. for the identity and for Fp2 elements (ADVICE r02, lg2.h:263).
 //   gu_exp_xabs_split   fp12h_exp_xabs_karabina on a split value (no easy part): the raw a^|x| of the pair.
+//   gu_quad             final_exponentiation_quad / fp12q_exp_xabs_karabina (lg2.h), a lane quad per element, the
+//                       value in full on all four lanes; each lane's result is returned, so the test sees that the four
+//                       agree.  Fp2 elements and the identity take the quad's degenerate branch (Granger-Scott).
 // Elements cross the ABI as 12 big-endian 48-byte Fp coefficients (c0.c0.c0 .. c1.c2.c1), canonical, not Montgomery.
 #include <hip/hip_runtime.h>
 
@@ -66,7 +69,36 @@ __global__ void __launch_bounds__(64) k_gu_split(const uint8_t* in, uint8_t* out
   if (!m) f12_out(out + 576 * i, full);
 }
 
+// op 0: final_exponentiation_quad; op 1: fp12q_exp_xabs_karabina.  out holds 4 results per element (lanes 0..3).
+__global__ void __launch_bounds__(64) k_gu_quad(const uint8_t* in, uint8_t* out, uint64_t n, int op) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t i = t >> 2;
+  if (i >= n) return;  // quad-uniform
+  const quad_m qm((int)(t & 3));
+  fp12 f, r;
+  f12_in(f, in + 576 * i);
+  if (op == 0)
+    final_exponentiation_quad(r, f, qm);
+  else
+    fp12q_exp_xabs_karabina(r, f, qm);
+  f12_out(out + 576 * t, r);
+}
+
 int check(hipError_t e) { return e == hipSuccess ? 0 : 1; }
+
+int run_quad(const uint8_t* in, uint8_t* out, uint64_t n, int op) {
+  uint8_t *din = nullptr, *dout = nullptr;
+  if (check(hipMalloc(&din, 576 * n)) || check(hipMalloc(&dout, 4 * 576 * n))) return 1;
+  int rc = check(hipMemcpy(din, in, 576 * n, hipMemcpyHostToDevice));
+  if (!rc) {
+    hipLaunchKernelGGL(k_gu_quad, dim3((unsigned)((4 * n + 63) / 64)), dim3(64), 0, 0, din, dout, n, op);
+    rc = check(hipGetLastError()) || check(hipDeviceSynchronize()) ||
+         check(hipMemcpy(out, dout, 4 * 576 * n, hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  return rc;
+}
 
 int run(unsigned lanes, const uint8_t* in, uint8_t* out, uint64_t n, int extra_op, bool split) {
   uint8_t *din = nullptr, *dout = nullptr;
@@ -98,4 +130,5 @@ int gu_final_exp_split(const uint8_t* in, uint8_t* out, uint64_t n) {
 int gu_exp_xabs_split(const uint8_t* in, uint8_t* out, uint64_t n, int karabina) {
   return n ? run((unsigned)(2 * n), in, out, n, karabina ? 1 : 2, true) : 0;
 }
+int gu_quad(const uint8_t* in, uint8_t* out, uint64_t n, int op) { return n ? run_quad(in, out, n, op) : 0; }
 }

@@ -71,3 +71,27 @@ def test_exp_xabs_split_vs_oracle(G, karabina):
     got = _run(G.gu_exp_xabs_split, elems, ctypes.c_int(karabina))
     for e, g in zip(elems, got):
         assert g == bls.f12_pow(e, X_ABS)
+
+
+@pytest.mark.parametrize("op", [0, 1])
+def test_quad_final_exp_and_exp_xabs(G, op):
+    """lg2.h final_exponentiation_quad (op 0) and fp12q_exp_xabs_karabina (op 1) on a lane quad: all four lanes agree,
+    and equal the one-lane final exponentiation / the oracle's a^|x|; the identity and Fp2 elements take the
+    quad's degenerate branch."""
+    rng = random.Random(47 + op)
+    z = (0, 0)
+    fp2s = [(((rng.randrange(bls.P), rng.randrange(bls.P)), z, z), (z, z, z)) for _ in range(2)]
+    if op == 0:
+        elems = [bls.F12_ONE] + fp2s + [rand_f12(rng) for _ in range(4)]
+        want = _run(G.gu_final_exp, elems)
+    else:
+        elems = [bls.F12_ONE] + [_cyclotomic(rng) for _ in range(4)]
+        want = [bls.f12_pow(e, X_ABS) for e in elems]
+    n = len(elems)
+    inp = b"".join(f12_bytes(e) for e in elems)
+    out = ctypes.create_string_buffer(4 * 576 * n)
+    assert G.gu_quad(inp, out, ctypes.c_uint64(n), ctypes.c_int(op)) == 0
+    raw = out.raw
+    for i in range(n):
+        lanes = [f12_from(raw[576 * (4 * i + q):576 * (4 * i + q) + 576]) for q in range(4)]
+        assert lanes[0] == lanes[1] == lanes[2] == lanes[3] == want[i], i
