@@ -12,9 +12,9 @@
 //     squarings with three Fp2 squarings per lane instead of six), so its latency is roughly halved.  The
 //     inversion of the easy part is computed redundantly on both lanes from the gathered value.
 //   * Lane quads (miller_loop_split, lq4_verify): for batches that leave lanes idle, ONE Miller loop is split across
-//     a pair (the Fp12 squaring and line products halved, the point steps redundant), and a quad runs a Verify's
-//     two loops on its two pairs: n = 1 Verify 23.8 -> 20.7 ms, C3 359k -> 411k aggregates/s
-//     (profiles/r03_pair_sweep_quads.txt, r03_c3_quads.json).
+//     a pair (the Fp12 squaring and line products halved, the doubling step's products dealt out), a quad runs a
+//     Verify's two loops on its two pairs, and the final exponentiation is dealt out over the quad: n = 1 Verify
+//     23.8 -> 18.6 ms, C3 359k -> 439k aggregates/s (profiles/r03_pair_sweep_dblsplit.txt).
 //
 // Semantics are those of pairing_check_verify / the RLC checks (ops.h, rlc.h): the same formulas, the same e^3
 // final exponentiation, so a split check and a single-lane check accept exactly the same inputs.  Device-only
@@ -418,6 +418,65 @@ __device__ __forceinline__ void fp12h_mul_line_split(fp6& h, const fp2& g0, cons
   fp6_add(r, t0, sel(m, t1, vt1));
   h = r;
 }
+// pairing.h miller_dbl_step_inl split across the pair: the same formulas and the same (canonical) outputs on both
+// lanes, with the Fp2 products dealt out in three uniform slots per phase (even | odd):
+//   phase 1: Y^2 | X^2,  Z Z | X Y,  (Y + Z)^2 on both                -> swap (B, C) for (J, XY)
+//   phase 2: G G | A (B - F),  E E | B H,  H y_P | 3J x_P            -> swap (Y3, h1) for (X3, Z3, g1)
+// 15 products of latency instead of 25.
+__device__ __forceinline__ fp sel(uint32_t m, const fp& if_odd, const fp& if_even) {
+  fp r;
+  sel_words<12>(&r.v[0], m, &if_odd.v[0], &if_even.v[0]);
+  return r;
+}
+__device__ __forceinline__ void miller_dbl_step_split(g2j& T, fp2& g0, fp2& g1, fp2& h1, const fp& xp, const fp& yp,
+                                                      uint32_t m) {
+  fp2 r1, r2, r3, s;
+  fp2_sqr(r1, sel(m, T.x, T.y));                     // even B = Y^2 | odd J = X^2
+  fp2_mul(r2, sel(m, T.x, T.z), sel(m, T.y, T.z));   // even C = Z^2 | odd X Y
+  fp2_add(s, T.y, T.z);
+  fp2_sqr(r3, s);                                    // D = (Y + Z)^2 on both lanes
+  fp2 o1, o2;
+  pair_swap(o1, r1);
+  pair_swap(o2, r2);
+  const fp2 B = sel(m, o1, r1), J = sel(m, r1, o1), C = sel(m, o2, r2), XY = sel(m, r2, o2), D = r3;
+  fp2 A, E, F, G, H, t;
+  fp2_half(A, XY);
+  fp2_mul_3b2(E, C);
+  fp2_add(F, E, E);
+  fp2_add(F, F, E);
+  fp2_add(G, B, F);
+  fp2_half(G, G);
+  fp2_sub(H, D, B);
+  fp2_sub(H, H, C);
+  fp2_sub(g0, E, B);
+  fp2 J3, BF;
+  fp2_add(J3, J, J);
+  fp2_add(J3, J3, J);
+  fp2_sub(BF, B, F);
+  fp2 p1, p2, p3;
+  fp2_mul(p1, sel(m, A, G), sel(m, BF, G));          // even G^2 | odd X3 = A (B - F)
+  fp2_mul(p2, sel(m, B, E), sel(m, H, E));           // even E^2 | odd Z3 = B H
+  fp2_mul_fp(p3, sel(m, J3, H), sel(m, xp, yp));     // even H y_P | odd g1 = 3J x_P
+  fp2 Y3, E3, hneg;
+  fp2_add(E3, p2, p2);
+  fp2_add(E3, E3, p2);
+  fp2_sub(Y3, p1, E3);                               // even: G^2 - 3 E^2
+  fp2_neg(hneg, p3);                                 // even: h1 = -H y_P
+  const fp2 s1 = sel(m, p1, Y3), s2 = sel(m, p2, hneg), s3 = sel(m, p3, hneg);
+  fp2 q1, q2, q3;
+  pair_swap(q1, s1);  // even receives X3 | odd receives Y3
+  pair_swap(q2, s2);  // even receives Z3 | odd receives h1
+  pair_swap(q3, s3);  // even receives g1
+  T.x = sel(m, p1, q1);
+  T.y = sel(m, q1, Y3);
+  T.z = sel(m, p2, q2);
+  g1 = sel(m, p3, q3);
+  h1 = sel(m, q2, hneg);
+}
+
+#ifndef BLS_LQ4_DBL_SPLIT
+#define BLS_LQ4_DBL_SPLIT 1
+#endif
 BLS_CALL __device__ void miller_loop_split(fp6& h_out, const g1a& P_in, const g2a& Q_in, uint32_t m,
                                            g2j* T_out = nullptr) {
   const g1a P = P_in;
@@ -433,7 +492,11 @@ BLS_CALL __device__ void miller_loop_split(fp6& h_out, const g1a& P_in, const g2
   for (int bit = 62; bit >= 0; --bit) {
     if (bit != 62) fp12h_sqr_split(h, m);
     fp2 g0, g1, h1;
+#if BLS_LQ4_DBL_SPLIT
+    miller_dbl_step_split(T, g0, g1, h1, P.x, P.y, m);
+#else
     miller_dbl_step_inl(T, g0, g1, h1, P.x, P.y);
+#endif
     fp12h_mul_line_split(h, g0, g1, h1, m);
     if ((X_ABS >> bit) & 1ull) {
       miller_add_step_inl(T, g0, g1, h1, Q, P.x, P.y);
