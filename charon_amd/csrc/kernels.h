@@ -193,12 +193,24 @@ k_tagg_scale(const uint8_t* __restrict__ sigs,
       if (ids[g0 + a] == ids[g0 + b]) st = HIPBLS_ERR_COMBINE;
   }
   g2a s;
-  const int ds = g2_decompress(s, sigs + 96 * k, true);
-  if (ds == DEC_BAD) st = HIPBLS_ERR_SIGNATURE;
-  if (st == HIPBLS_OK && ds == DEC_OK) {
+  int64_t c;
+  uint64_t L;
+  // small ids: the subgroup test and c_k sig_k share one doubling chain (ops.h g2_subgroup_and_mul_i64)
+  const bool small = st == HIPBLS_OK && lagrange_small(ids + g0, t, me, c, L);
+  int ds = g2_decompress(s, sigs + 96 * k, !small);
+  if (small && ds == DEC_OK) {
     g2j sj;
     jac_from_aff(sj, s);
-    tagg_scale_point(acc, sj, ids + g0, t, me);  // c_k sig_k (small ids) or lambda_k sig_k
+    if (!g2_subgroup_and_mul_i64(acc, sj, c)) {
+      ds = DEC_BAD;
+      jac_set_inf(acc);
+    }
+  }
+  if (ds == DEC_BAD) st = HIPBLS_ERR_SIGNATURE;
+  if (st == HIPBLS_OK && ds == DEC_OK && !small) {
+    g2j sj;
+    jac_from_aff(sj, s);
+    tagg_scale_point(acc, sj, ids + g0, t, me);  // lambda_k sig_k (field path)
   }
   const uint32_t* src = &acc.x.c0.v[0];
   for (int w = 0; w < 72; ++w) pts[(uint64_t)w * n_parts + k] = src[w];

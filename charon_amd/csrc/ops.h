@@ -153,6 +153,44 @@ BLS_HD BLS_CALL void tagg_scale_point(g2j& out, const g2j& sj, const int64_t* id
   }
 }
 
+// A partial's G2 membership test and its small-integer multiple from ONE chain of doublings.  herumi deserializes
+// every partial with a subgroup check (tbls/herumi.go:250-262), here psi(sig) == [x] sig (Scott 2021, as
+// g2_in_subgroup), and the small-integer path then needs [c] sig.  Right to left, the points 2^i sig (i < 64) serve
+// both: [|x|] sig = sum over |x|'s six set bits, [|c|] sig = sum over c's bits -- 63 doublings and ~23 additions
+// instead of 63 + 35 doublings and the same additions.  The sums are the same group elements as the left-to-right
+// chains compute (the additions handle the exceptional cases), so the aggregate's bytes do not change.  Returns
+// whether sig is in G2 (sig affine, not infinity).
+BLS_HD BLS_CALL bool g2_subgroup_and_mul_i64(g2j& out, const g2j& sj, int64_t c) {
+  const uint64_t k = c < 0 ? (uint64_t)0 - (uint64_t)c : (uint64_t)c;
+  g2j pw = sj, ax, ac;
+  jac_set_inf(ax);
+  jac_set_inf(ac);
+  for (int i = 0; i < 64; ++i) {
+    if ((X_ABS >> i) & 1ull) {
+      g2j t = ax;
+      jac_add(ax, t, pw);
+    }
+    if ((k >> i) & 1ull) {
+      g2j t = ac;
+      jac_add(ac, t, pw);
+    }
+    if (i < 63 && ((X_ABS | k) >> (i + 1)) != 0) {
+      g2j t;
+      jac_dbl_body(t, pw);
+      pw = t;
+    }
+  }
+  if (c < 0) {
+    g2j t = ac;
+    jac_neg(ac, t);
+  }
+  out = ac;
+  g2j q, ps;
+  jac_neg(q, ax);  // [x] sig, x < 0
+  g2_psi(ps, sj);
+  return jac_eq(q, ps);
+}
+
 // The group's sum of scaled partials -> the aggregate: [L^-1 mod r] sum on the small-integer path, as is otherwise.
 BLS_HD BLS_CALL void tagg_unscale(g2j& acc, const int64_t* ids, int t) {
   int64_t c;

@@ -101,6 +101,26 @@ int ht_g2_in_subgroup(const uint8_t* xy192) {
   fp2_set_one(p.z);
   return g2_in_subgroup(p) ? 1 : 0;
 }
+// ops.h g2_subgroup_and_mul_i64: membership and [c] P from one doubling chain (k_tagg_scale's small-integer path)
+int ht_g2_subgroup_and_mul_i64(const uint8_t* xy192, int64_t c, uint8_t* out192, int* out_inf) {
+  g2j p, q;
+  fp_in(p.x.c0, xy192);
+  fp_in(p.x.c1, xy192 + 48);
+  fp_in(p.y.c0, xy192 + 96);
+  fp_in(p.y.c1, xy192 + 144);
+  fp2_set_one(p.z);
+  const int in = g2_subgroup_and_mul_i64(q, p, c) ? 1 : 0;
+  *out_inf = jac_is_inf(q) ? 1 : 0;
+  if (!*out_inf) {
+    g2a a;
+    jac_to_aff(a, q);
+    fp_out(out192, a.x.c0);
+    fp_out(out192 + 48, a.x.c1);
+    fp_out(out192 + 96, a.y.c0);
+    fp_out(out192 + 144, a.y.c1);
+  }
+  return in;
+}
 void ht_g2_clear_cofactor(const uint8_t* xy192, uint8_t* out192) {
   g2j p, q;
   fp_in(p.x.c0, xy192);

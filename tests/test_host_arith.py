@@ -141,6 +141,27 @@ def test_g2_subgroup_check_vs_order(L):
         assert L.ht_g2_in_subgroup(g2_bytes(pt_in)) == 1
 
 
+def test_g2_subgroup_and_small_multiple_one_chain(L):
+    """ops.h g2_subgroup_and_mul_i64 (k_tagg_scale, small Lagrange integers): the membership answer equals the
+    order test's and [c] P equals the oracle's, for points in and out of G2, signed c, c = +-1 and c past |x|'s
+    top bit."""
+    import ctypes
+    rng = random.Random(21)
+    out, inf = buf(192), ctypes.c_int(0)
+    fn = L.ht_g2_subgroup_and_mul_i64
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+    for trial in range(3):
+        pt = _random_g2_point(rng)
+        pt_in = bls.g2_mul(pt, bls.H_EFF_G2)
+        for p, member in [(pt, 0), (pt_in, 1)]:
+            for c in [1, -1, 5, -36, rng.randrange(1, 1 << 40), -rng.randrange(1, 1 << 62), (1 << 63) - 1]:
+                assert fn(g2_bytes(p), c, out, ctypes.byref(inf)) == member
+                want = bls.g2_mul(p, c) if c > 0 else bls.g2_neg(bls.g2_mul(p, -c))
+                assert inf.value == int(want is None)
+                if want is not None:
+                    assert g2_from(out.raw) == want, (trial, member, c)
+
+
 def test_decompress_roundtrip(L):
     rng = random.Random(5)
     out1, out2 = buf(96), buf(192)
