@@ -13,6 +13,9 @@ using namespace bls;
 // ============================================================================ kernels
 namespace {
 
+#ifndef BLS_VERIFY_LDS
+#define BLS_VERIFY_LDS 1
+#endif
 constexpr int kBlock = 64;  // one wave per workgroup: these kernels are register-bound, not LDS-bound
 
 __global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restrict__ pks,
@@ -23,7 +26,13 @@ __global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restri
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t o0 = offs[i], o1 = offs[i + 1];
+#if BLS_VERIFY_LDS
+  __shared__ u32x4 s_f[36 * kBlock];  // each lane's Miller-loop f (pairing_lds.h): 36 KiB per one-wave workgroup
+  const f12l<kBlock> F{(BLS_LDS u32x4*)&s_f[threadIdx.x]};
+  status[i] = op_verify_l(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i, F);
+#else
   status[i] = op_verify(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i);
+#endif
 }
 
 // ---------------------------------------------------------------- lane-pair Verify (lg2.h)

@@ -9,6 +9,7 @@
 #include "fr.h"
 #include "h2c.h"
 #include "pairing.h"
+#include "pairing_lds.h"
 
 namespace bls {
 
@@ -40,6 +41,21 @@ BLS_HD BLS_CALL int pairing_check_verify_sig(const g1a& pk, const g2a& hm, const
   fp12 f, e;
   g2j T1;
   miller_loop_2(f, pk, hm, P1, sig, &T1);
+  const bool in_g2 = g2_subgroup_from_miller(T1, sig);
+  final_exponentiation(e, f);
+  if (!in_g2) return HIPBLS_ERR_SIGNATURE;
+  return fp12_is_one(e) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+}
+
+// pairing_check_verify_sig with the Miller loop's f in LDS (pairing_lds.h): the C2 kernel k_verify_fused.
+template <int S>
+BLS_HD BLS_CALL int pairing_check_verify_sig_l(const g1a& pk, const g2a& hm, const g2a& sig, const f12l<S> F) {
+  g1a P1;
+  P1.x = G1_GEN_X;
+  P1.y = G1_NEG_GEN_Y;
+  fp12 f, e;
+  g2j T1;
+  miller_loop_2_l(f, F, pk, hm, P1, sig, &T1);
   const bool in_g2 = g2_subgroup_from_miller(T1, sig);
   final_exponentiation(e, f);
   if (!in_g2) return HIPBLS_ERR_SIGNATURE;
@@ -264,6 +280,24 @@ BLS_HD BLS_CALL int op_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t 
   g2a hm;
   jac_to_aff(hm, hj);
   return pairing_check_verify_sig(pk, hm, sig);
+}
+
+// op_verify with the Miller loop's f in LDS (F: this lane's slot; pairing_lds.h).
+template <int S>
+BLS_HD BLS_CALL int op_verify_l(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96,
+                                const f12l<S> F) {
+  g1a pk;
+  const int dp = g1_decompress(pk, pk48, true);
+  if (dp == DEC_BAD) return HIPBLS_ERR_PUBKEY;
+  g2a sig;
+  const int ds = g2_decompress(sig, sig96, false);
+  if (ds == DEC_BAD) return HIPBLS_ERR_SIGNATURE;
+  if (dp == DEC_INF || ds == DEC_INF) return verify_inf_status(ds, sig);
+  g2j hj;
+  hash_to_g2(hj, msg, msg_len, DST_POP, 43);
+  g2a hm;
+  jac_to_aff(hm, hj);
+  return pairing_check_verify_sig_l(pk, hm, sig, F);
 }
 
 BLS_HD BLS_CALL int op_sign(uint8_t* out96, const uint8_t* sk32, const uint8_t* msg, uint32_t msg_len) {

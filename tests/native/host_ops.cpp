@@ -29,6 +29,13 @@ int ht_sk_to_pk(const uint8_t* sk, uint8_t* out) { return op_sk_to_pk(out, sk); 
 int ht_verify(const uint8_t* pk, const uint8_t* msg, uint32_t len, const uint8_t* sig) {
   return op_verify(pk, msg, len, sig);
 }
+// op_verify_l (k_verify_fused's path: the Miller loop's f in LDS, pairing_lds.h) over a host array standing in for
+// the lane's LDS slot (one lane: S = 1)
+int ht_verify_l(const uint8_t* pk, const uint8_t* msg, uint32_t len, const uint8_t* sig) {
+  u32x4 slot[36];
+  const f12l<1> F{slot};
+  return op_verify_l(pk, msg, len, sig, F);
+}
 
 void ht_hash_to_g2(const uint8_t* msg, uint32_t len, const uint8_t* dst, uint32_t dst_len, uint8_t* out_aff192) {
   g2j h;
@@ -171,6 +178,39 @@ void ht_miller(const uint8_t* p96, const uint8_t* q192, uint8_t* out576) {
   miller_loop_n(f, P, Q, skip, 1);
   const fp* c = &f.c0.c0.c0;
   for (int i = 0; i < 12; ++i) fp_out(out576 + 48 * i, c[i]);
+}
+
+// The two-pair Miller loop (Verify's shape) with f in registers (lds = 0, pairing.h miller_loop_2) or in the LDS
+// layout (lds = 1, pairing_lds.h miller_loop_2_l); out576 = f, outT = the second pair's final T (X, Y, Z: 288 bytes)
+void ht_miller2(const uint8_t* p0, const uint8_t* q0, const uint8_t* p1, const uint8_t* q1, int lds,
+                uint8_t* out576, uint8_t* outT) {
+  g1a P0, P1;
+  g2a Q0, Q1;
+  fp_in(P0.x, p0);
+  fp_in(P0.y, p0 + 48);
+  fp_in(P1.x, p1);
+  fp_in(P1.y, p1 + 48);
+  const uint8_t* qs[2] = {q0, q1};
+  g2a* Qs[2] = {&Q0, &Q1};
+  for (int k = 0; k < 2; ++k) {
+    fp_in(Qs[k]->x.c0, qs[k]);
+    fp_in(Qs[k]->x.c1, qs[k] + 48);
+    fp_in(Qs[k]->y.c0, qs[k] + 96);
+    fp_in(Qs[k]->y.c1, qs[k] + 144);
+  }
+  fp12 f;
+  g2j T;
+  if (lds) {
+    u32x4 slot[36];
+    const f12l<1> F{slot};
+    miller_loop_2_l(f, F, P0, Q0, P1, Q1, &T);
+  } else {
+    miller_loop_2(f, P0, Q0, P1, Q1, &T);
+  }
+  const fp* c = &f.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) fp_out(out576 + 48 * i, c[i]);
+  const fp* t = &T.x.c0;
+  for (int i = 0; i < 6; ++i) fp_out(outT + 48 * i, t[i]);
 }
 
 // Fp12 product / final exponentiation on raw coefficient arrays (plain, tower order)

@@ -360,6 +360,24 @@ def test_verify_signature_membership_from_miller_loop(L):
         for p, m, want in ((pk, msg, 0 if k == 0 else 2), (pk, msg[::-1], 3 if k == 0 else 2),
                            (inf_pk, msg, 3 if k == 0 else 2)):
             assert L.ht_verify(p, m, 32, s) == want, (k, want)
+            assert L.ht_verify_l(p, m, 32, s) == want, (k, want)  # k_verify_fused's LDS-resident Miller loop
+
+
+def test_miller_loop_lds_resident_f_matches_registers(L):
+    """pairing_lds.h miller_loop_2_l (k_verify_fused: f in LDS, squaring and line products reordered in place) returns
+    the same f and the same final T as pairing.h miller_loop_2 (pinned to the oracle through ht_verify and the fixture
+    tests), limb for limb, for Verify-shaped operands: a G1 key, H(m), -g1 and a signature in or outside G2."""
+    rng = random.Random(29)
+    f_reg, f_lds, t_reg, t_lds = buf(576), buf(576), buf(288), buf(288)
+    neg_g1 = (bls.G1_GEN[0], (-bls.G1_GEN[1]) % P)
+    for trial in range(3):
+        p0 = bls.g1_mul(bls.G1_GEN, rng.randrange(1, bls.R))
+        q0 = bls.hash_to_g2(rng.randbytes(32), bls.DST_POP)
+        q1 = bls.g2_mul(q0, rng.randrange(1, bls.R)) if trial else _random_g2_point(rng)
+        args = (g1_bytes(p0), g2_bytes(q0), g1_bytes(neg_g1), g2_bytes(q1))
+        L.ht_miller2(*args, 0, f_reg, t_reg)
+        L.ht_miller2(*args, 1, f_lds, t_lds)
+        assert f_lds.raw == f_reg.raw and t_lds.raw == t_reg.raw, trial
 
 
 def test_lagrange_small_integers(L):
