@@ -16,7 +16,12 @@ namespace {
 #ifndef BLS_VERIFY_LDS
 #define BLS_VERIFY_LDS 1
 #endif
-constexpr int kBlock = 64;  // one wave per workgroup: these kernels are register-bound, not LDS-bound
+constexpr int kBlock = 64;
+// This lane's Miller-loop accumulator in LDS (pairing_lds.h): 36 KiB per one-wave workgroup, so the four one-wave
+// workgroups a CU holds at this register count use 144 of its 160 KiB.  Every single-lane pairing check declares it.
+#define BLS_LANE_F12(F)                      \
+  __shared__ u32x4 s_f12_[36 * kBlock];      \
+  const f12l<kBlock> F { (BLS_LDS u32x4*)&s_f12_[threadIdx.x] }  // one wave per workgroup: these kernels are register-bound, not LDS-bound
 
 __global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restrict__ pks,
                                                          const uint8_t* __restrict__ msgs,
@@ -27,8 +32,7 @@ __global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restri
   if (i >= n) return;
   const uint64_t o0 = offs[i], o1 = offs[i + 1];
 #if BLS_VERIFY_LDS
-  __shared__ u32x4 s_f[36 * kBlock];  // each lane's Miller-loop f (pairing_lds.h): 36 KiB per one-wave workgroup
-  const f12l<kBlock> F{(BLS_LDS u32x4*)&s_f[threadIdx.x]};
+  BLS_LANE_F12(F);
   status[i] = op_verify_l(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i, F);
 #else
   status[i] = op_verify(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i);
@@ -432,7 +436,8 @@ __global__ void __launch_bounds__(kBlock) k_verify_pair_single(const uint32_t* _
   soa_load<24>(&pk.x.v[0], ws, n, i);
   soa_load<48>(&hm.x.c0.v[0], ws + 24 * n, n, i);
   soa_load<48>(&sig.x.c0.v[0], ws + 72 * n, n, i);
-  status[i] = pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+  BLS_LANE_F12(F);
+  status[i] = pairing_check_verify_l(pk, hm, sig, F) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }
 
 // G1 decode of many public keys (FastAggregateVerify): affine SoA (24 words) + code per key
@@ -813,7 +818,8 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback(const uint32_t* __restr
   const uint64_t len = *list_len;
   if (len <= pair_upto) return;  // k_rlc_fallback_lg2 takes short lists
   if (j >= len || j >= cap) return;
-  rlc_fallback_lane(list[j], pks, sigs, msg_idx, H, hstride, hslot, status, key_idx, T, tab);
+  BLS_LANE_F12(F);
+  rlc_fallback_lane(F, list[j], pks, sigs, msg_idx, H, hstride, hslot, status, key_idx, T, tab);
 }
 
 // The lane-pair layout (lg2.h): the even lane decodes the key and takes e(pk, H(m)), the odd lane decodes the
@@ -1018,7 +1024,8 @@ __global__ void __launch_bounds__(kBlock) k_verify_keys(const uint32_t* __restri
   g1j xpk;
   const int dp = pubtab_get(pk, xpk, k, T, code, tab);
   const uint64_t o0 = offs[i], o1 = offs[i + 1];
-  status[i] = op_verify_decoded_pk(dp, pk, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i);
+  BLS_LANE_F12(F);
+  status[i] = op_verify_decoded_pk(dp, pk, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i, F);
 }
 
 // ---------------------------------------------------------------- signing roots

@@ -48,14 +48,17 @@ BLS_HD BLS_CALL int pairing_check_verify_sig(const g1a& pk, const g2a& hm, const
 }
 
 // pairing_check_verify_sig with the Miller loop's f in LDS (pairing_lds.h): the C2 kernel k_verify_fused.
+#ifndef BLS_VERIFY_L_CALL
+#define BLS_VERIFY_L_CALL BLS_CALL
+#endif
 template <int S>
-BLS_HD BLS_CALL int pairing_check_verify_sig_l(const g1a& pk, const g2a& hm, const g2a& sig, const f12l<S> F) {
+BLS_HD BLS_VERIFY_L_CALL int pairing_check_verify_sig_l(const g1a& pk, const g2a& hm, const g2a& sig, const f12l<S> F) {
   g1a P1;
   P1.x = G1_GEN_X;
   P1.y = G1_NEG_GEN_Y;
   fp12 f, e;
   g2j T1;
-  miller_loop_2_l(f, F, pk, hm, P1, sig, &T1);
+  miller_loop_2_l<S, true>(f, F, pk, hm, P1, sig, &T1);
   const bool in_g2 = g2_subgroup_from_miller(T1, sig);
   final_exponentiation(e, f);
   if (!in_g2) return HIPBLS_ERR_SIGNATURE;
@@ -284,7 +287,7 @@ BLS_HD BLS_CALL int op_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t 
 
 // op_verify with the Miller loop's f in LDS (F: this lane's slot; pairing_lds.h).
 template <int S>
-BLS_HD BLS_CALL int op_verify_l(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96,
+BLS_HD BLS_VERIFY_L_CALL int op_verify_l(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96,
                                 const f12l<S> F) {
   g1a pk;
   const int dp = g1_decompress(pk, pk48, true);

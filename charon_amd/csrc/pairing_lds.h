@@ -246,10 +246,39 @@ BLS_HD BLS_INLINE void fp12_mul_line2_l(const f12l<S>& F, const fp2& ga0_in, con
 }
 
 // miller_loop_2 (pairing.h) with f in LDS; f_out and T1_out as there.
-template <int S>
-BLS_HD BLS_CALL void miller_loop_2_l(fp12& f_out, const f12l<S> F, const g1a& P0_in, const g2a& Q0, const g1a& P1_in,
+// Register-allocation hint: x's dwords pass through an empty asm statement in accumulation registers, so the
+// allocator keeps a value that waits across a doubling step in AGPRs rather than in scratch.
+#ifndef BLS_ML_PARK
+#define BLS_ML_PARK 0
+#endif
+template <class T>
+BLS_HD BLS_INLINE void park_agpr(T& x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t* w = reinterpret_cast<uint32_t*>(&x);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) asm("" : "+a"(w[i]));
+#endif
+}
+
+#ifndef BLS_ML_DBL
+#define BLS_ML_DBL miller_dbl_step_inl
+#endif
+#ifndef BLS_MILLER_L_CALL
+#define BLS_MILLER_L_CALL BLS_CALL
+#endif
+// P1_NEG_GEN: P1 is -g1 (Verify's second pair), so its coordinates are immediates rematerialized at each use instead
+// of 24 registers live across the loop.
+template <int S, bool P1_NEG_GEN = false>
+BLS_HD BLS_MILLER_L_CALL void miller_loop_2_l(fp12& f_out, const f12l<S> F, const g1a& P0_in, const g2a& Q0, const g1a& P1_in,
                                      const g2a& Q1, g2j* T1_out) {
-  const g1a P0 = P0_in, P1 = P1_in;
+  g1a P0 = P0_in;
+  g1a P1;
+  if (P1_NEG_GEN) {
+    P1.x = G1_GEN_X;
+    P1.y = G1_NEG_GEN_Y;
+  } else {
+    P1 = P1_in;
+  }
   g2j T0, T1;
   T0.x = Q0.x;
   T0.y = Q0.y;
@@ -269,10 +298,23 @@ BLS_HD BLS_CALL void miller_loop_2_l(fp12& f_out, const f12l<S> F, const g1a& P0
     fp12_mul_line2_l(F, a0, a1, ah, g0, g1, h1);
   }
   for (int bit = 61; bit >= 0; --bit) {
+#if BLS_ML_PARK & 1
+    park_agpr(T0);
+    park_agpr(T1);
+#endif
+#if BLS_ML_PARK & 4
+    park_agpr(P0);
+#endif
     fp12_sqr_l(F);
     fp2 a0, a1, ah, g0, g1, h1;
-    miller_dbl_step_inl(T0, a0, a1, ah, P0.x, P0.y);
-    miller_dbl_step_inl(T1, g0, g1, h1, P1.x, P1.y);
+    BLS_ML_DBL(T0, a0, a1, ah, P0.x, P0.y);
+#if BLS_ML_PARK & 2
+    park_agpr(T0);
+    park_agpr(a0);
+    park_agpr(a1);
+    park_agpr(ah);
+#endif
+    BLS_ML_DBL(T1, g0, g1, h1, P1.x, P1.y);
     fp12_mul_line2_l(F, a0, a1, ah, g0, g1, h1);
     if ((X_ABS >> bit) & 1ull) {
       miller_add_step_inl(T0, a0, a1, ah, Q0, P0.x, P0.y);
@@ -284,6 +326,18 @@ BLS_HD BLS_CALL void miller_loop_2_l(fp12& f_out, const f12l<S> F, const g1a& P0
   F.ld12(f);
   fp12_conj(f_out, f);
   if (T1_out) *T1_out = T1;
+}
+
+// e(pk, hm) e(-g1, sig) == 1 on decoded points (ops.h pairing_check_verify) with f in LDS.
+template <int S>
+BLS_HD BLS_CALL bool pairing_check_verify_l(const g1a& pk, const g2a& hm, const g2a& sig, const f12l<S> F) {
+  g1a P1;
+  P1.x = G1_GEN_X;
+  P1.y = G1_NEG_GEN_Y;
+  fp12 f, e;
+  miller_loop_2_l<S, true>(f, F, pk, hm, P1, sig, nullptr);
+  final_exponentiation(e, f);
+  return fp12_is_one(e);
 }
 
 }  // namespace bls

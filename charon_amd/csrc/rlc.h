@@ -168,9 +168,10 @@ BLS_HD BLS_INLINE int pubtab_get(g1a& pk, g1j& xpk, uint64_t k, uint64_t T, cons
   return code[k];
 }
 
-// tbls.Verify with the public key taken from the table (same statuses as op_verify).
+// tbls.Verify with the public key taken from the table (same statuses as op_verify); the Miller loop's f in LDS.
+template <int S>
 BLS_HD BLS_CALL int op_verify_decoded_pk(int dp, const g1a& pk, const uint8_t* msg, uint32_t msg_len,
-                                         const uint8_t* sig96) {
+                                         const uint8_t* sig96, const f12l<S> F) {
   if (dp == DEC_BAD) return HIPBLS_ERR_PUBKEY;
   g2a sig;
   const int ds = g2_decompress(sig, sig96, false);  // G2 membership from the Miller loop (ops.h)
@@ -180,7 +181,7 @@ BLS_HD BLS_CALL int op_verify_decoded_pk(int dp, const g1a& pk, const uint8_t* m
   hash_to_g2(hj, msg, msg_len, DST_POP, 43);
   g2a hm;
   jac_to_aff(hm, hj);
-  return pairing_check_verify_sig(pk, hm, sig);
+  return pairing_check_verify_sig_l(pk, hm, sig, F);
 }
 
 // Multi-Miller loop over up to MAXN pairs with one shared Fp12 squaring chain (pairing.h steps).
@@ -355,7 +356,8 @@ BLS_HD BLS_INLINE int rlc_window_lane(uint64_t w, uint64_t n, const uint32_t* ms
 // Stage 4, item i: still pending after its window failed -> tbls.Verify of the item alone.  Both
 // points already passed decoding and the subgroup tests in stage 1 and H(m) is in the table, so this
 // is the bare pairing check: e(pk, H(m)) * e(-g1, sig) == 1 (about half of a full op_verify).
-BLS_HD BLS_INLINE void rlc_fallback_lane(uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
+template <int S>
+BLS_HD BLS_INLINE void rlc_fallback_lane(const f12l<S>& F, uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
                                          const uint32_t* H, uint64_t hstride, const uint32_t* hslot, int32_t* status,
                                          const uint32_t* key_idx = nullptr, uint64_t T = 0,
                                          const uint32_t* tab = nullptr) {
@@ -368,7 +370,7 @@ BLS_HD BLS_INLINE void rlc_fallback_lane(uint64_t i, const uint8_t* pks, const u
     soa_load<24>(&pk.x.v[0], tab, T, key_idx[i]);
   g2_decompress(sig, sigs + 96 * i, false);
   soa_load<48>(&hm.x.c0.v[0], H, hstride, h_col(hslot, msg_idx[i]));
-  status[i] = pairing_check_verify(pk, hm, sig) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+  status[i] = pairing_check_verify_l(pk, hm, sig, F) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }
 
 }  // namespace bls

@@ -22,6 +22,12 @@ static void fp_in(fp& a, const uint8_t* b) {
   fp_to_mont(a, a);
 }
 
+// The host stand-in for a lane's LDS slot of the Miller-loop f (pairing_lds.h, S = 1)
+static f12l<1> host_f12_slot() {
+  static thread_local u32x4 slot[36];
+  return f12l<1>{slot};
+}
+
 extern "C" {
 
 int ht_sign(const uint8_t* sk, const uint8_t* msg, uint32_t len, uint8_t* out) { return op_sign(out, sk, msg, len); }
@@ -325,7 +331,7 @@ extern "C" int ht_rlc_verify(const uint8_t* pks, const uint8_t* sigs, const uint
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
   mark(2);
-  for (uint32_t i : list) rlc_fallback_lane(i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status);
+  for (uint32_t i : list) rlc_fallback_lane(host_f12_slot(), i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status);
   mark(3);
   stats3[0] = n_win;
   stats3[1] = stats3[2] = 0;
@@ -361,7 +367,7 @@ extern "C" int ht_rlc_verify_keys(const uint8_t* tab_pks, uint64_t T, const uint
     if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
-  for (uint32_t i : list) rlc_fallback_lane(i, nullptr, sigs, msg_idx, H.data(), n_msgs, nullptr, status, key_idx, T, tab.data());
+  for (uint32_t i : list) rlc_fallback_lane(host_f12_slot(), i, nullptr, sigs, msg_idx, H.data(), n_msgs, nullptr, status, key_idx, T, tab.data());
   stats3[0] = n_win;
   stats3[1] = stats3[2] = 0;
   for (int32_t x : win)
@@ -380,7 +386,7 @@ extern "C" int ht_verify_key(const uint8_t* pk48, const uint8_t* msg, uint32_t l
   g1a pk;
   g1j xpk;
   const int dp = pubtab_get(pk, xpk, 0, 1, &code, tab);
-  return op_verify_decoded_pk(dp, pk, msg, len, sig);
+  return op_verify_decoded_pk(dp, pk, msg, len, sig, host_f12_slot());
 }
 
 // ---- batch-wide RLC check with the Pippenger MSM (charon_amd/csrc/rlcb.h), lane by lane ------------------
@@ -500,7 +506,7 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
     if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
-  for (uint32_t i : list) rlc_fallback_lane(i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status);
+  for (uint32_t i : list) rlc_fallback_lane(host_f12_slot(), i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status);
   mark(5);
   return 0;
 }
