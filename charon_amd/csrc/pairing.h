@@ -69,44 +69,40 @@ BLS_HD BLS_INLINE void miller_dbl_step_inl(g2j& T_in, fp2& g0, fp2& g1, fp2& h1,
 }
 BLS_HD BLS_MILLER_CALL void miller_dbl_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const fp& xp_in, const fp& yp_in) { miller_dbl_step_inl(T_in, g0, g1, h1, xp_in, yp_in); }
 
+// Low-liveness order as in the doubling step: the line coefficients first, then each temporary consumed right away.
 BLS_HD BLS_INLINE void miller_add_step_inl(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const g2a& Q_in, const fp& xp_in,
                                          const fp& yp_in) {
-  const g2a Q = Q_in;
   const fp xp = xp_in;
   const fp yp = yp_in;
   g2j T = T_in;
-  fp2 theta, lambda, C, D, E, F, G, H, t;
-  fp2_mul(t, Q.y, T.z);
-  fp2_sub(theta, T.y, t);
-  fp2_mul(t, Q.x, T.z);
-  fp2_sub(lambda, T.x, t);
-  fp2_sqr(C, theta);
-  fp2_sqr(D, lambda);
-  fp2_mul(E, lambda, D);
-  fp2_mul(F, T.z, C);
-  fp2_mul(G, T.x, D);
-  fp2_add(H, E, F);
-  fp2_sub(H, H, G);
-  fp2_sub(H, H, G);
+  fp2 theta, lambda, t, u;
+  fp2_mul(t, Q_in.y, T.z);
+  fp2_sub(theta, T.y, t);  // theta = Y - y2 Z
+  fp2_mul(t, Q_in.x, T.z);
+  fp2_sub(lambda, T.x, t);  // lambda = X - x2 Z
   // line
-  fp2 u;
-  fp2_mul(t, theta, Q.x);
-  fp2_mul(u, lambda, Q.y);
+  fp2_mul(t, theta, Q_in.x);
+  fp2_mul(u, lambda, Q_in.y);
   fp2_sub(g0, t, u);
   fp2_mul_fp(g1, theta, xp);
   fp2_neg(g1, g1);
   fp2_mul_fp(h1, lambda, yp);
   // point
-  fp2 X3, Y3, Z3;
-  fp2_mul(X3, lambda, H);
-  fp2_sub(t, G, H);
-  fp2_mul(Y3, theta, t);
-  fp2_mul(t, T.y, E);
-  fp2_sub(Y3, Y3, t);
-  fp2_mul(Z3, T.z, E);
-  T.x = X3;
-  T.y = Y3;
-  T.z = Z3;
+  fp2 C, D, E, G;
+  fp2_sqr(C, theta);
+  fp2_mul(C, T.z, C);  // F = Z theta^2
+  fp2_sqr(D, lambda);
+  fp2_mul(G, T.x, D);  // G = X lambda^2
+  fp2_mul(E, lambda, D);  // E = lambda^3
+  fp2_mul(T.z, T.z, E);  // Z3 = Z E
+  fp2_mul(t, T.y, E);  // Y E
+  fp2_add(u, E, C);
+  fp2_sub(u, u, G);
+  fp2_sub(u, u, G);  // H = E + F - 2G
+  fp2_mul(T.x, lambda, u);  // X3 = lambda H
+  fp2_sub(u, G, u);
+  fp2_mul(u, theta, u);
+  fp2_sub(T.y, u, t);  // Y3 = theta (G - H) - Y E
   T_in = T;
 }
 BLS_HD BLS_MILLER_CALL void miller_add_step(g2j& T_in, fp2& g0, fp2& g1, fp2& h1, const g2a& Q_in, const fp& xp_in,
@@ -365,6 +361,16 @@ BLS_HD BLS_INLINE void cyc_decompress(fp12& r, const cyc_c& c, const fp2& z1) {
   r.c1.c2 = c.z5;
 }
 BLS_HD BLS_CALL void fp12_cyc_exp_xabs_gs(fp12& r, const fp12& a_in);
+#ifndef BLS_KAR_SQR_RUNS
+#define BLS_KAR_SQR_RUNS 1
+#endif
+// n compressed squarings in place (a wave-uniform count)
+BLS_HD BLS_CALL void cyc_sqr_run(cyc_c& c_io, int n) {
+  cyc_c c = c_io;
+#pragma unroll 1
+  for (int k = 0; k < n; ++k) cyc_sqr_compressed(c);
+  c_io = c;
+}
 // r = a^|x| for a in the cyclotomic subgroup, by compressed squarings
 // Inlined into the final exponentiation's five call sites it measured slower (C2 1.710M -> 1.685M verifies/s; with
 // the nine FE products inlined too 1.666M, profiles/r02_sched_variants.txt), so it stays a call.
@@ -379,6 +385,24 @@ BLS_HD BLS_KAR_EXP_CALL void fp12_cyc_exp_xabs_karabina(fp12& r, const fp12& a_i
   c.z3 = a_in.c0.c2;
   c.z4 = a_in.c0.c1;
   c.z5 = a_in.c1.c2;
+#if BLS_KAR_SQR_RUNS
+  // the squarings in runs between |x|'s set bits, each run a call of its own (cyc_sqr_run): inside it only the
+  // compressed state is live, so the loop needs no scratch; inlined here, the allocator spilled around every
+  // squaring for the sake of the decompression code below (33 scratch instructions per squaring)
+  cyc_sqr_run(c, 16);
+  st[0] = c;
+  cyc_sqr_run(c, 32);
+  st[1] = c;
+  cyc_sqr_run(c, 9);
+  st[2] = c;
+  cyc_sqr_run(c, 3);
+  st[3] = c;
+  cyc_sqr_run(c, 2);
+  st[4] = c;
+  cyc_sqr_run(c, 1);
+  st[5] = c;
+  int s;
+#else
   // one squaring loop with the save points as a wave-uniform test (one inlined copy of the squaring)
   int s = 0;
 #pragma unroll 1
@@ -386,6 +410,7 @@ BLS_HD BLS_KAR_EXP_CALL void fp12_cyc_exp_xabs_karabina(fp12& r, const fp12& a_i
     cyc_sqr_compressed(c);
     if (k == 16 || k == 48 || k == 57 || k == 60 || k == 62 || k == 63) st[s++] = c;
   }
+#endif
   // batch inversion of the six z1 denominators
   fp2 num[6], den[6], pre[6];
 #pragma unroll 1
