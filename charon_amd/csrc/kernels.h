@@ -756,7 +756,8 @@ __global__ void __launch_bounds__(kBlock) k_rlc_window(uint64_t w0, uint64_t w1,
                                                        uint32_t* __restrict__ list, uint32_t* __restrict__ list_len) {
   const uint64_t w = w0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (w >= w1) return;
-  const int left = rlc_window_lane(w, n, msg_idx, rpk, rsig, H, hstride, hslot, status, win_fail);
+  BLS_LANE_F12(F);
+  const int left = rlc_window_lane(F, w, n, msg_idx, rpk, rsig, H, hstride, hslot, status, win_fail);
   if (left == 0) return;
   uint32_t at = atomicAdd(list_len, (uint32_t)left);
   const uint64_t i1 = w * RLC_W + RLC_W < n ? w * RLC_W + RLC_W : n;
@@ -961,10 +962,11 @@ __global__ void __launch_bounds__(kBlock) k_rlcb_chunks(uint64_t n, const int32_
                                                         const uint32_t* __restrict__ hslot, uint32_t* __restrict__ F,
                                                         uint64_t n_chunks, const uint32_t* __restrict__ W) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  BLS_LANE_F12(Lf);
   if (c < n_chunks)
-    rlcb_chunk_lane(c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks + 1);
+    rlcb_chunk_lane(Lf, c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks + 1);
   else if (c == n_chunks)
-    rlcb_sfactor_lane(W, F, n_chunks + 1, n_chunks);
+    rlcb_sfactor_lane(Lf, W, F, n_chunks + 1, n_chunks);
 }
 
 __global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict__ Fin, uint64_t nin,

@@ -245,6 +245,74 @@ BLS_HD BLS_INLINE void fp12_mul_line2_l(const f12l<S>& F, const fp2& ga0_in, con
   F.st(5, c);
 }
 
+// fp6_mul_01 / fp6_mul_1 (tower.h) with a's coefficients fetched at each use.
+template <class A>
+BLS_HD BLS_INLINE void fp6_mul_01_fetch(fp6& r, const A& a, const fp2& b0, const fp2& b1) {
+  fp2 t0, t1, s0, s1, u, c0, c1, c2;
+  fp2_mul(t0, a(0), b0);
+  fp2_mul(t1, a(1), b1);
+  fp2_mul(u, a(2), b1);
+  fp2_mul_xi(u, u);
+  fp2_add(c0, u, t0);  // t0 + xi a2 b1
+  fp2_add_lazy(s0, a(0), a(1));
+  fp2_add(s1, b0, b1);
+  fp2_mul(c1, s0, s1);
+  fp2_sub(c1, c1, t0);
+  fp2_sub(c1, c1, t1);  // (a0 + a1)(b0 + b1) - t0 - t1
+  fp2_mul(c2, a(2), b0);
+  fp2_add(c2, c2, t1);  // a2 b0 + t1
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+template <class A>
+BLS_HD BLS_INLINE void fp6_mul_1_fetch(fp6& r, const A& a, const fp2& b1) {
+  fp2 c0;
+  fp2_mul(c0, a(2), b1);
+  fp2_mul_xi(r.c0, c0);
+  fp2_mul(r.c1, a(0), b1);
+  fp2_mul(r.c2, a(1), b1);
+}
+
+// f <- f l in place for one line (tower.h fp12_mul_line): t0 = F0 (g0 + g1 v), t1 = F1 (h1 v); F0 + F1 overwrites F1,
+// c0 = t0 + v t1 overwrites F0, c1 = (F0 + F1)(g0 + (g1 + h1) v) - (t0 + t1) overwrites F1.
+template <int S>
+BLS_HD BLS_INLINE void fp12_mul_line_l(const f12l<S>& F, const fp2& g0_in, const fp2& g1_in, const fp2& h1_in) {
+  const fp2 g0 = g0_in;
+  const fp2 g1 = g1_in;
+  const fp2 h1 = h1_in;
+  fp6 t0, t1;
+  fp6_mul_01_fetch(t0, [&](int i) { return F.ld(i); }, g0, g1);
+  fp6_mul_1_fetch(t1, [&](int i) { return F.ld(3 + i); }, h1);
+  fp2 c;
+  for (int i = 0; i < 3; ++i) {  // F1 <- F0 + F1
+    fp2_add(c, F.ld(i), F.ld(3 + i));
+    F.st(3 + i, c);
+  }
+  fp6 d;
+  {
+    fp6 vt1;
+    fp6_mul_v(vt1, t1);
+    fp2_add(c, t0.c0, vt1.c0);
+    F.st(0, c);
+    fp2_add(c, t0.c1, vt1.c1);
+    F.st(1, c);
+    fp2_add(c, t0.c2, vt1.c2);
+    F.st(2, c);
+    fp6_add(d, t0, t1);
+  }
+  fp2 gh1;
+  fp2_add(gh1, g1, h1);
+  fp6 s;
+  fp6_mul_01_fetch(s, [&](int i) { return F.ld(3 + i); }, g0, gh1);
+  fp2_sub(c, s.c0, d.c0);
+  F.st(3, c);
+  fp2_sub(c, s.c1, d.c1);
+  F.st(4, c);
+  fp2_sub(c, s.c2, d.c2);
+  F.st(5, c);
+}
+
 // miller_loop_2 (pairing.h) with f in LDS; f_out and T1_out as there.
 // Register-allocation hint: x's dwords pass through an empty asm statement in accumulation registers, so the
 // allocator keeps a value that waits across a doubling step in AGPRs rather than in scratch.

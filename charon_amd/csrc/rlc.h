@@ -228,12 +228,59 @@ BLS_HD BLS_CALL void miller_loop_multi(fp12& f, const g1a* P, const g2a* Q, int 
   if (T0_out) *T0_out = T[0];
 }
 
+// miller_loop_multi with f in LDS (pairing_lds.h): the same steps and the same f; T[] stays in the lane's stack.
+template <int MAXN, int S>
+BLS_HD BLS_CALL void miller_loop_multi_l(fp12& f_out, const f12l<S> F, const g1a* P, const g2a* Q, int n) {
+  g2j T[MAXN];
+  for (int k = 0; k < n; ++k) {
+    T[k].x = Q[k].x;
+    T[k].y = Q[k].y;
+    fp2_set_one(T[k].z);
+  }
+  {
+    fp12 one;
+    fp12_set_one(one);
+    F.st12(one);
+  }
+  fp2 g0, g1, h1;
+  for (int bit = 62; bit >= 0; --bit) {
+    if (bit != 62) fp12_sqr_l(F);
+    for (int k = 0; k < n; k += 2) {
+      if (k + 1 < n) {
+        fp2 a0, a1, ah;
+        miller_dbl_step(T[k], a0, a1, ah, P[k].x, P[k].y);
+        miller_dbl_step(T[k + 1], g0, g1, h1, P[k + 1].x, P[k + 1].y);
+        fp12_mul_line2_l(F, a0, a1, ah, g0, g1, h1);
+      } else {
+        miller_dbl_step(T[k], g0, g1, h1, P[k].x, P[k].y);
+        fp12_mul_line_l(F, g0, g1, h1);
+      }
+    }
+    if ((X_ABS >> bit) & 1ull) {
+      for (int k = 0; k < n; k += 2) {
+        if (k + 1 < n) {
+          fp2 a0, a1, ah;
+          miller_add_step(T[k], a0, a1, ah, Q[k], P[k].x, P[k].y);
+          miller_add_step(T[k + 1], g0, g1, h1, Q[k + 1], P[k + 1].x, P[k + 1].y);
+          fp12_mul_line2_l(F, a0, a1, ah, g0, g1, h1);
+        } else {
+          miller_add_step(T[k], g0, g1, h1, Q[k], P[k].x, P[k].y);
+          fp12_mul_line_l(F, g0, g1, h1);
+        }
+      }
+    }
+  }
+  fp12 f;
+  F.ld12(f);
+  fp12_conj(f_out, f);
+}
+
 // Stage 3, one lane per window [i0, i1): sum the scaled keys per run of equal message index and
 // the scaled signatures over the whole window, run one multi-Miller loop + final exponentiation,
 // and return true when the window verifies (or holds no pending item).
 // Accessors are callables so the same body serves the SoA device buffers and the host test.
-template <class LoadPk, class LoadSig, class LoadH>
-BLS_HD BLS_INLINE bool rlc_window(uint64_t i0, uint64_t i1, const int32_t* status, const uint32_t* msg_idx,
+template <int LS, class LoadPk, class LoadSig, class LoadH>
+BLS_HD BLS_INLINE bool rlc_window(const f12l<LS>& F, uint64_t i0, uint64_t i1, const int32_t* status, const uint32_t* msg_idx,
                                   LoadPk load_pk, LoadSig load_sig, LoadH load_h) {
   g1a P[RLC_W + 1];
   g2a Q[RLC_W + 1];
@@ -278,7 +325,7 @@ BLS_HD BLS_INLINE bool rlc_window(uint64_t i0, uint64_t i1, const int32_t* statu
   }
   if (np == 0) return true;
   fp12 f, e;
-  miller_loop_multi<RLC_W + 1>(f, P, Q, np);
+  miller_loop_multi_l<RLC_W + 1>(f, F, P, Q, np);
   final_exponentiation(e, f);
   return fp12_is_one(e);
 }
@@ -332,7 +379,8 @@ BLS_HD BLS_INLINE void rlc_hash_lane(uint64_t m, const uint8_t* msgs, const uint
 // Stage 3, window w = items [w*RLC_W, ...): on success every pending item becomes HIPBLS_OK,
 // otherwise they stay pending for stage 4.  Returns (and stores in win_fail[w]) the number of items
 // left pending: 0 when the window passed.
-BLS_HD BLS_INLINE int rlc_window_lane(uint64_t w, uint64_t n, const uint32_t* msg_idx, const uint32_t* rpk,
+template <int S>
+BLS_HD BLS_INLINE int rlc_window_lane(const f12l<S>& F, uint64_t w, uint64_t n, const uint32_t* msg_idx, const uint32_t* rpk,
                                       const uint32_t* rsig, const uint32_t* H, uint64_t hstride, const uint32_t* hslot,
                                       int32_t* status, int32_t* win_fail) {
   const uint64_t i0 = w * RLC_W;
@@ -340,7 +388,7 @@ BLS_HD BLS_INLINE int rlc_window_lane(uint64_t w, uint64_t n, const uint32_t* ms
   auto load_pk = [&](g1j& q, uint64_t i) { soa_load<36>(&q.x.v[0], rpk, n, i); };
   auto load_sig = [&](g2j& q, uint64_t i) { soa_load<72>(&q.x.c0.v[0], rsig, n, i); };
   auto load_h = [&](g2a& q, uint32_t m) { soa_load<48>(&q.x.c0.v[0], H, hstride, h_col(hslot, m)); };
-  const bool ok = rlc_window(i0, i1, status, msg_idx, load_pk, load_sig, load_h);
+  const bool ok = rlc_window(F, i0, i1, status, msg_idx, load_pk, load_sig, load_h);
   int left = 0;
   for (uint64_t i = i0; i < i1; ++i)
     if (status[i] == RLC_PENDING) {

@@ -192,7 +192,8 @@ BLS_HD BLS_INLINE void msm_combine(g2j& S, const g2j& W0, const g2j& W1) {
 
 // ---- stage 3: per-chunk multi-Miller loop ----------------------------------------------------------
 // F: Fp12 SoA, 144 words x n_chunks.  Chunks without pending items store 1.
-BLS_HD BLS_INLINE void rlcb_chunk_lane(uint64_t c, uint64_t n, const int32_t* status, const uint32_t* msg_idx,
+template <int S>
+BLS_HD BLS_INLINE void rlcb_chunk_lane(const f12l<S>& Lf, uint64_t c, uint64_t n, const int32_t* status, const uint32_t* msg_idx,
                                        const uint32_t* rpk, const uint32_t* H, uint64_t hstride,
                                        const uint32_t* hslot, uint32_t* F, uint64_t n_chunks) {
   g1a P[RLCB_C];
@@ -228,7 +229,7 @@ BLS_HD BLS_INLINE void rlcb_chunk_lane(uint64_t c, uint64_t n, const int32_t* st
   }
   fp12 f;
   if (np)
-    miller_loop_multi<RLCB_C>(f, P, Q, np);
+    miller_loop_multi_l<RLCB_C>(f, Lf, P, Q, np);
   else
     fp12_set_one(f);
   soa_store<144>(F, n_chunks, c, &f.c0.c0.c0.v[0]);
@@ -236,7 +237,8 @@ BLS_HD BLS_INLINE void rlcb_chunk_lane(uint64_t c, uint64_t n, const int32_t* st
 
 // The S lane of stage 3: S = W0 + [2^16] W1 from the window sums (W: 2 x 72 words, contiguous), then the Miller
 // value of (-g1, S) (1 when S is the point at infinity) into column `col` of F.
-BLS_HD BLS_INLINE void rlcb_sfactor_lane(const uint32_t* W, uint32_t* F, uint64_t stride, uint64_t col) {
+template <int LS>
+BLS_HD BLS_INLINE void rlcb_sfactor_lane(const f12l<LS>& Lf, const uint32_t* W, uint32_t* F, uint64_t stride, uint64_t col) {
   g2j W0, W1, S;
   for (int k = 0; k < 72; ++k) {
     (&W0.x.c0.v[0])[k] = W[k];
@@ -252,7 +254,7 @@ BLS_HD BLS_INLINE void rlcb_sfactor_lane(const uint32_t* W, uint32_t* F, uint64_
     P[0].x = G1_GEN_X;
     P[0].y = G1_NEG_GEN_Y;
     jac_to_aff(Q[0], S);
-    miller_loop_multi<1>(f, P, Q, 1);
+    miller_loop_multi_l<1>(f, Lf, P, Q, 1);
   }
   soa_store<144>(F, stride, col, &f.c0.c0.c0.v[0]);
 }

@@ -327,7 +327,7 @@ extern "C" int ht_rlc_verify(const uint8_t* pks, const uint8_t* sigs, const uint
   mark(1);
   std::vector<uint32_t> list;
   for (uint64_t w = 0; w < n_win; ++w)
-    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
+    if (rlc_window_lane(host_f12_slot(), w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
   mark(2);
@@ -364,7 +364,7 @@ extern "C" int ht_rlc_verify_keys(const uint8_t* tab_pks, uint64_t T, const uint
   for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, H.data(), n_msgs, nullptr);
   std::vector<uint32_t> list;
   for (uint64_t w = 0; w < n_win; ++w)
-    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
+    if (rlc_window_lane(host_f12_slot(), w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
   for (uint32_t i : list) rlc_fallback_lane(host_f12_slot(), i, nullptr, sigs, msg_idx, H.data(), n_msgs, nullptr, status, key_idx, T, tab.data());
@@ -475,9 +475,9 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
   const uint64_t nch = (n + RLCB_C - 1) / RLCB_C;
   std::vector<uint32_t> F(144 * (nch + 1));
   for (uint64_t c = 0; c < nch; ++c)
-    rlcb_chunk_lane(c, n, status, msg_idx, rpk.data(), H.data(), n_msgs, nullptr, F.data(), nch + 1);
+    rlcb_chunk_lane(host_f12_slot(), c, n, status, msg_idx, rpk.data(), H.data(), n_msgs, nullptr, F.data(), nch + 1);
   mark(3);  // the (-g1, S) lane is counted with the product and the verdict (stage 4 of counts6)
-  rlcb_sfactor_lane(Wc.data(), F.data(), nch + 1, nch);
+  rlcb_sfactor_lane(host_f12_slot(), Wc.data(), F.data(), nch + 1, nch);
   uint64_t cur = nch + 1;
   while (cur > 1) {
     const uint64_t nxt = (cur + RLCB_FAN - 1) / RLCB_FAN;
@@ -503,7 +503,7 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
   std::vector<int32_t> win(n_win ? n_win : 1);
   std::vector<uint32_t> list;
   for (uint64_t w = 0; w < n_win; ++w)
-    if (rlc_window_lane(w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
+    if (rlc_window_lane(host_f12_slot(), w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
   for (uint32_t i : list) rlc_fallback_lane(host_f12_slot(), i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status);
