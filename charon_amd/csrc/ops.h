@@ -60,7 +60,7 @@ BLS_HD BLS_VERIFY_L_CALL int pairing_check_verify_sig_l(const g1a& pk, const g2a
   g2j T1;
   miller_loop_2_l<S, true>(f, F, pk, hm, P1, sig, &T1);
   const bool in_g2 = g2_subgroup_from_miller(T1, sig);
-  final_exponentiation(e, f);
+  final_exp_l(e, f, F);
   if (!in_g2) return HIPBLS_ERR_SIGNATURE;
   return fp12_is_one(e) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }

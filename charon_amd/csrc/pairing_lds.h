@@ -396,6 +396,141 @@ BLS_HD BLS_MILLER_L_CALL void miller_loop_2_l(fp12& f_out, const f12l<S> F, cons
   if (T1_out) *T1_out = T1;
 }
 
+// f <- f b in place, b dense in registers (fp12_mul_inl): t0 = F0 b0, t1 = F1 b1; F0 + F1 overwrites F1, c0 = t0 + v t1
+// overwrites F0, c1 = (F0 + F1)(b0 + b1) - (t0 + t1) overwrites F1.
+template <int S>
+BLS_HD BLS_INLINE void fp12_mul_l(const f12l<S>& F, const fp12& b) {
+  fp6 t0, t1;
+  fp6_mul_fetch(t0, [&](int i) { return F.ld(i); }, [&](int i) { return i == 0 ? b.c0.c0 : (i == 1 ? b.c0.c1 : b.c0.c2); });
+  fp6_mul_fetch(t1, [&](int i) { return F.ld(3 + i); }, [&](int i) { return i == 0 ? b.c1.c0 : (i == 1 ? b.c1.c1 : b.c1.c2); });
+  fp2 c;
+  for (int i = 0; i < 3; ++i) {  // F1 <- F0 + F1
+    fp2_add(c, F.ld(i), F.ld(3 + i));
+    F.st(3 + i, c);
+  }
+  fp6 d, sb;
+  {
+    fp6 vt1;
+    fp6_mul_v(vt1, t1);
+    fp2_add(c, t0.c0, vt1.c0);
+    F.st(0, c);
+    fp2_add(c, t0.c1, vt1.c1);
+    F.st(1, c);
+    fp2_add(c, t0.c2, vt1.c2);
+    F.st(2, c);
+    fp6_add(d, t0, t1);
+  }
+  fp6_add(sb, b.c0, b.c1);
+  fp6 s;
+  fp6_mul_fetch(s, [&](int i) { return F.ld(3 + i); }, [&](int i) { return i == 0 ? sb.c0 : (i == 1 ? sb.c1 : sb.c2); });
+  fp2_sub(c, s.c0, d.c0);
+  F.st(3, c);
+  fp2_sub(c, s.c1, d.c1);
+  F.st(4, c);
+  fp2_sub(c, s.c2, d.c2);
+  F.st(5, c);
+}
+
+// fp12_cyc_exp_xabs_karabina (pairing.h) with the decompressed powers' product accumulated in LDS: the tail's
+// accumulator (144 dwords) no longer shares the registers with the power being decompressed and the saved states.
+template <int S>
+BLS_HD BLS_CALL void fp12_cyc_exp_xabs_karabina_l(fp12& r, const fp12& a_in, const f12l<S> F) {
+  static_assert(X_ABS == 0xd201000000010000ull, "the squaring counts below are |x|'s set bits");
+  cyc_c st[6];  // a^(2^k) for k = 16, 48, 57, 60, 62, 63
+  cyc_c c;
+  c.z2 = a_in.c1.c0;
+  c.z3 = a_in.c0.c2;
+  c.z4 = a_in.c0.c1;
+  c.z5 = a_in.c1.c2;
+  cyc_sqr_run(c, 16);
+  st[0] = c;
+  cyc_sqr_run(c, 32);
+  st[1] = c;
+  cyc_sqr_run(c, 9);
+  st[2] = c;
+  cyc_sqr_run(c, 3);
+  st[3] = c;
+  cyc_sqr_run(c, 2);
+  st[4] = c;
+  cyc_sqr_run(c, 1);
+  st[5] = c;
+  fp2 num[6], den[6], pre[6];
+  int s;
+#pragma unroll 1
+  for (s = 0; s < 6; ++s) cyc_z1_parts(num[s], den[s], st[s]);
+  pre[0] = den[0];
+#pragma unroll 1
+  for (s = 1; s < 6; ++s) fp2_mul(pre[s], pre[s - 1], den[s]);
+  const bool degenerate = fp2_is_zero(pre[5]);
+  fp2 inv;
+  fp2_inv(inv, pre[5]);
+#pragma unroll 1
+  for (s = 5; s >= 0; --s) {
+    fp2 is, z1;
+    if (s > 0) {
+      fp2_mul(is, inv, pre[s - 1]);  // 1 / den[s]
+      fp2_mul(inv, inv, den[s]);
+    } else {
+      is = inv;
+    }
+    fp2_mul(z1, num[s], is);
+    fp12 d;
+    cyc_decompress(d, st[s], z1);
+    if (s == 5)
+      F.st12(d);
+    else
+      fp12_mul_l(F, d);
+  }
+  if (degenerate) {  // practically never: the identity or z2 = z3 = 0 at one of the six powers
+    fp12_cyc_exp_xabs_gs(r, a_in);
+    return;
+  }
+  F.ld12(r);
+}
+
+// final_exponentiation (pairing.h) with the a^|x| powers on fp12_cyc_exp_xabs_karabina_l; F is free scratch here.
+template <int S>
+BLS_HD BLS_CALL void final_exponentiation_l(fp12& r, const fp12& f_in, const f12l<S> F) {
+  const fp12 f = f_in;
+  fp12 t, fi, m;
+  fp12_conj(t, f);
+  fp12_inv(fi, f);
+  BLS_FE_MUL(m, t, fi);
+  fp12_frobenius(t, m, 2);
+  BLS_FE_MUL(m, t, m);
+  fp12 t0, t1, t2, u;
+  fp12_cyc_exp_xabs_karabina_l(t0, m, F);
+  BLS_FE_MUL(t0, t0, m);
+  fp12_conj(t0, t0);
+  fp12_cyc_exp_xabs_karabina_l(u, t0, F);
+  BLS_FE_MUL(u, u, t0);
+  fp12_conj(t0, u);
+  fp12_cyc_exp_xabs_karabina_l(u, t0, F);
+  fp12_conj(u, u);
+  fp12_frobenius(t1, t0, 1);
+  BLS_FE_MUL(t1, t1, u);
+  fp12_cyc_exp_xabs_karabina_l(u, t1, F);
+  fp12_cyc_exp_xabs_karabina_l(u, u, F);
+  fp12_frobenius(t2, t1, 2);
+  BLS_FE_MUL(t2, t2, u);
+  fp12_conj(u, t1);
+  BLS_FE_MUL(t2, t2, u);
+  fp12_cyclotomic_sqr(u, m);
+  BLS_FE_MUL(u, u, m);
+  BLS_FE_MUL(r, t2, u);
+}
+#ifndef BLS_FE_LDS
+#define BLS_FE_LDS 1
+#endif
+template <int S>
+BLS_HD BLS_INLINE void final_exp_l(fp12& r, const fp12& f, const f12l<S>& F) {
+#if BLS_FE_LDS
+  final_exponentiation_l(r, f, F);
+#else
+  final_exponentiation(r, f);
+#endif
+}
+
 // e(pk, hm) e(-g1, sig) == 1 on decoded points (ops.h pairing_check_verify) with f in LDS.
 template <int S>
 BLS_HD BLS_CALL bool pairing_check_verify_l(const g1a& pk, const g2a& hm, const g2a& sig, const f12l<S> F) {
@@ -404,7 +539,7 @@ BLS_HD BLS_CALL bool pairing_check_verify_l(const g1a& pk, const g2a& hm, const 
   P1.y = G1_NEG_GEN_Y;
   fp12 f, e;
   miller_loop_2_l<S, true>(f, F, pk, hm, P1, sig, nullptr);
-  final_exponentiation(e, f);
+  final_exp_l(e, f, F);
   return fp12_is_one(e);
 }
 

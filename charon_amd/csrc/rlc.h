@@ -326,7 +326,7 @@ BLS_HD BLS_INLINE bool rlc_window(const f12l<LS>& F, uint64_t i0, uint64_t i1, c
   if (np == 0) return true;
   fp12 f, e;
   miller_loop_multi_l<RLC_W + 1>(f, F, P, Q, np);
-  final_exponentiation(e, f);
+  final_exp_l(e, f, F);
   return fp12_is_one(e);
 }
 

@@ -229,6 +229,16 @@ void ht_final_exp(const uint8_t* in576, uint8_t* out576) {
   for (int i = 0; i < 12; ++i) fp_out(out576 + 48 * i, d[i]);
 }
 
+// final_exponentiation_l (pairing_lds.h: the Karabina tail accumulates in the LDS slot), same layout as ht_final_exp
+void ht_final_exp_l(const uint8_t* in576, uint8_t* out576) {
+  fp12 f, e;
+  fp* c = &f.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) fp_in(c[i], in576 + 48 * i);
+  final_exponentiation_l(e, f, host_f12_slot());
+  const fp* d = &e.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) fp_out(out576 + 48 * i, d[i]);
+}
+
 void ht_fp12_op(int op, const uint8_t* a576, const uint8_t* b576, uint8_t* out576) {
   fp12 a, b, r;
   fp* ca = &a.c0.c0.c0;

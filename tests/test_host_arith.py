@@ -310,6 +310,14 @@ def test_compressed_cyclotomic_exponentiation(L):
     for f in (one, (((rng.randrange(P), rng.randrange(P)), z, z), (z, z, z))):
         L.ht_final_exp(f12_bytes(f), out)
         assert f12_from(out.raw) == one
+        L.ht_final_exp_l(f12_bytes(f), out)  # the LDS-accumulator variant takes the same degenerate branch
+        assert f12_from(out.raw) == one
+    want, got = buf(576), buf(576)
+    for _ in range(2):  # random elements: the LDS-accumulator final exponentiation equals the register one
+        f = rand_f12(rng)
+        L.ht_final_exp(f12_bytes(f), want)
+        L.ht_final_exp_l(f12_bytes(f), got)
+        assert got.raw == want.raw
 
 
 def test_verify_signature_membership_from_miller_loop(L):
