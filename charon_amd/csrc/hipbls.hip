@@ -91,8 +91,8 @@ struct VBatch {
   uint64_t n() const { return off.size() - 1; }
 };
 
-// A wire-format batch in flight on the GPU: its own stream, buffers and pinned status copy, so a second batch can be
-// copied in and launched while the first one runs.
+// A wire-format batch in flight on the GPU: its own buffers, pinned status copy and completion event, so a second
+// batch can be copied in and launched (behind the first, on the queue's stream) while the first one runs.
 struct QSlot {
   hipStream_t stream = nullptr;
   hipEvent_t done_ev = nullptr;
@@ -1312,9 +1312,16 @@ void queue_worker(Context* cp) {
   VerifyQueue& q = c.q;
   bool dev_ok = hipSetDevice(c.device) == hipSuccess &&
                 hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) == hipSuccess;
-  for (int k = 0; dev_ok && k < VerifyQueue::kSlots; ++k)
-    dev_ok = hipStreamCreateWithFlags(&q.slot[k].stream, hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&q.slot[k].done_ev, hipEventDisableTiming) == hipSuccess;
+  // Both slots run on the queue's one stream: the next batch's copies and kernels are enqueued behind the running
+  // batch (no host round trip between them), and the queue occupies one hardware queue.  Every hardware queue that
+  // runs these kernels holds a scratch allocation sized for ~17 KB per lane over the whole device; with a stream per
+  // slot, the context's streams and the queue's together spread over all four of HIP's hardware queues and the
+  // runtime's scratch pool ran out under 64 concurrent callers (HSA_STATUS_ERROR_OUT_OF_RESOURCES on a lane-quad
+  // dispatch).
+  for (int k = 0; dev_ok && k < VerifyQueue::kSlots; ++k) {
+    q.slot[k].stream = q.stream;
+    dev_ok = hipEventCreateWithFlags(&q.slot[k].done_ev, hipEventDisableTiming) == hipSuccess;
+  }
   std::unique_lock<std::mutex> lk(q.mu);
   for (;;) {
     const bool pending = !q.open.empty() && q.open.front()->n() > 0;
