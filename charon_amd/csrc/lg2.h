@@ -238,8 +238,9 @@ __device__ __forceinline__ void cyc_sqr_compressed_pair(cyc_c& c, uint32_t m) {
 #define BLS_LG2_KAR_MUL fp12h_mul_inl  // inlined: n = 10,000 lane-pair Verify 27.82 -> 27.52 ms, C3 +0.9 %
 #endif
 // r = a^|x| (split) by compressed squarings; the six saved powers are decompressed on both lanes (one batch
-// inversion) and multiplied as split values.  Degenerate inputs (a denominator 0) take fp12h_exp_xabs.
-BLS_CALL __device__ void fp12h_exp_xabs_karabina(fp6& r, const fp6& a_in, uint32_t m) {
+// inversion) and multiplied as split values.  Degenerate inputs (a denominator 0) return true with r untouched, and
+// fp12h_exp takes fp12h_exp_xabs from the caller's frame (off this function's stack depth).
+BLS_CALL __device__ bool fp12h_exp_xabs_karabina(fp6& r, const fp6& a_in, uint32_t m) {
   static_assert(X_ABS == 0xd201000000010000ull, "the squaring counts below are |x|'s set bits");
   cyc_c c;
   {
@@ -264,10 +265,7 @@ BLS_CALL __device__ void fp12h_exp_xabs_karabina(fp6& r, const fp6& a_in, uint32
   pre[0] = den[0];
 #pragma unroll 1
   for (s = 1; s < 6; ++s) fp2_mul(pre[s], pre[s - 1], den[s]);
-  if (fp2_is_zero(pre[5])) {  // same on both lanes
-    fp12h_exp_xabs(r, a_in, m);
-    return;
-  }
+  if (fp2_is_zero(pre[5])) return true;  // same on both lanes
   fp2 inv;
   fp2_inv(inv, pre[5]);
   fp6 acc;
@@ -293,6 +291,7 @@ BLS_CALL __device__ void fp12h_exp_xabs_karabina(fp6& r, const fp6& a_in, uint32
     }
   }
   r = acc;
+  return false;
 }
 
 #ifndef BLS_LG2_KARABINA
@@ -300,7 +299,7 @@ BLS_CALL __device__ void fp12h_exp_xabs_karabina(fp6& r, const fp6& a_in, uint32
 #endif
 __device__ __forceinline__ void fp12h_exp(fp6& r, const fp6& a_in, uint32_t m) {
 #if BLS_LG2_KARABINA
-  fp12h_exp_xabs_karabina(r, a_in, m);
+  if (fp12h_exp_xabs_karabina(r, a_in, m)) fp12h_exp_xabs(r, a_in, m);
 #else
   fp12h_exp_xabs(r, a_in, m);
 #endif
@@ -308,37 +307,53 @@ __device__ __forceinline__ void fp12h_exp(fp6& r, const fp6& a_in, uint32_t m) {
 
 // final_exponentiation (pairing.h) on a split value: same formula, split operations.
 BLS_CALL __device__ void final_exponentiation_split(fp6& r, const fp6& f_in, uint32_t m) {
-  const fp6 f = f_in;
-  fp6 t, mm, t0, t1, t2, u;
-  // easy part: f^((p^6-1)(p^2+1)); the inverse is computed on both lanes from the gathered value
-  fp12 full, inv;
-  fp12h_gather(full, f, m);
-  fp12_inv(inv, full);
-  const fp6 fi = sel(m, inv.c1, inv.c0);
-  fp12h_conj(t, f, m);
-  fp12h_mul(mm, t, fi, m);
-  fp12h_frobenius(t, mm, 2, m);
-  fp12h_mul(mm, t, mm, m);
+  // temporaries scoped so their frame slots can be shared (pairing_lds.h final_exponentiation_l); r may alias f_in
+  fp6 mm;
+  {  // easy part: f^((p^6-1)(p^2+1)); the inverse is computed on both lanes from the gathered value
+    fp6 t;
+    fp6 fi;
+    {
+      fp12 full, inv;
+      fp12h_gather(full, f_in, m);
+      fp12_inv(inv, full);
+      fi = sel(m, inv.c1, inv.c0);
+    }
+    fp12h_conj(t, f_in, m);
+    fp12h_mul(mm, t, fi, m);
+    fp12h_frobenius(t, mm, 2, m);
+    fp12h_mul(mm, t, mm, m);
+  }
   // hard part
-  fp12h_exp(t0, mm, m);
-  fp12h_mul(t0, t0, mm, m);
-  fp12h_conj(t0, t0, m);
-  fp12h_exp(u, t0, m);
-  fp12h_mul(u, u, t0, m);
-  fp12h_conj(t0, u, m);
-  fp12h_exp(u, t0, m);
-  fp12h_conj(u, u, m);
-  fp12h_frobenius(t1, t0, 1, m);
-  fp12h_mul(t1, t1, u, m);
-  fp12h_exp(u, t1, m);
-  fp12h_exp(u, u, m);
-  fp12h_frobenius(t2, t1, 2, m);
-  fp12h_mul(t2, t2, u, m);
-  fp12h_conj(u, t1, m);
-  fp12h_mul(t2, t2, u, m);
-  fp12h_cyc_sqr(u, mm, m);
-  fp12h_mul(u, u, mm, m);
-  fp12h_mul(r, t2, u, m);
+  fp6 t1;
+  {
+    fp6 t0, u;
+    fp12h_exp(t0, mm, m);
+    fp12h_mul(t0, t0, mm, m);
+    fp12h_conj(t0, t0, m);
+    fp12h_exp(u, t0, m);
+    fp12h_mul(u, u, t0, m);
+    fp12h_conj(t0, u, m);
+    fp12h_exp(u, t0, m);
+    fp12h_conj(u, u, m);
+    fp12h_frobenius(t1, t0, 1, m);
+    fp12h_mul(t1, t1, u, m);
+  }
+  fp6 t2;
+  {
+    fp6 u;
+    fp12h_exp(u, t1, m);
+    fp12h_exp(u, u, m);
+    fp12h_frobenius(t2, t1, 2, m);
+    fp12h_mul(t2, t2, u, m);
+    fp12h_conj(u, t1, m);
+    fp12h_mul(t2, t2, u, m);
+  }
+  {
+    fp6 u;
+    fp12h_cyc_sqr(u, mm, m);
+    fp12h_mul(u, u, mm, m);
+    fp12h_mul(r, t2, u, m);
+  }
 }
 
 // Is the split value 1?  Even half must be (1, 0, 0), odd half 0; both lanes get the answer.
@@ -611,7 +626,9 @@ __device__ __forceinline__ void cyc_sqr_compressed_quad(cyc_c& c, const quad_m& 
 // r = a^|x| on a quad (a in the cyclotomic subgroup, in full on every lane), pairing.h fp12_cyc_exp_xabs_karabina's
 // steps; the degenerate case (a saved power with z2 = z3 = 0) takes the one-lane Granger-Scott exponentiation on
 // every lane.
-BLS_CALL __device__ void fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, const quad_m& qm) {
+// Returns true, r untouched, in the degenerate case (fp12q_exp_xabs then takes Granger-Scott from the caller's frame,
+// keeping that chain off this function's stack depth).
+BLS_CALL __device__ bool fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, const quad_m& qm) {
   static_assert(X_ABS == 0xd201000000010000ull, "the squaring counts below are |x|'s set bits");
   cyc_c c;
   c.z2 = a_in.c1.c0;
@@ -631,10 +648,7 @@ BLS_CALL __device__ void fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, cons
   pre[0] = den[0];
 #pragma unroll 1
   for (s = 1; s < 6; ++s) fp2_mul(pre[s], pre[s - 1], den[s]);
-  if (fp2_is_zero(pre[5])) {  // the same on all four lanes
-    fp12_cyc_exp_xabs_gs(r, a_in);
-    return;
-  }
+  if (fp2_is_zero(pre[5])) return true;  // the same on all four lanes
   fp2 inv;
   fp2_inv(inv, pre[5]);
   fp12 acc;
@@ -659,37 +673,54 @@ BLS_CALL __device__ void fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, cons
     }
   }
   r = acc;
+  return false;
+}
+BLS_HD BLS_INLINE void fp12q_exp_xabs(fp12& r, const fp12& a_in, const quad_m& qm) {
+  if (fp12q_exp_xabs_karabina(r, a_in, qm)) fp12_cyc_exp_xabs_gs(r, a_in);
 }
 
 // final_exponentiation (pairing.h) on a quad: the same formula and the same result on every lane.
 BLS_CALL __device__ void final_exponentiation_quad(fp12& r, const fp12& f_in, const quad_m& qm) {
-  const fp12 f = f_in;
-  fp12 t, fi, m;
-  fp12_conj(t, f);
-  fp12_inv(fi, f);
-  fp12q_mul(m, t, fi, qm);
-  fp12_frobenius(t, m, 2);
-  fp12q_mul(m, t, m, qm);
-  fp12 t0, t1, t2, u;
-  fp12q_exp_xabs_karabina(t0, m, qm);
-  fp12q_mul(t0, t0, m, qm);
-  fp12_conj(t0, t0);
-  fp12q_exp_xabs_karabina(u, t0, qm);
-  fp12q_mul(u, u, t0, qm);
-  fp12_conj(t0, u);
-  fp12q_exp_xabs_karabina(u, t0, qm);
-  fp12_conj(u, u);
-  fp12_frobenius(t1, t0, 1);
-  fp12q_mul(t1, t1, u, qm);
-  fp12q_exp_xabs_karabina(u, t1, qm);
-  fp12q_exp_xabs_karabina(u, u, qm);
-  fp12_frobenius(t2, t1, 2);
-  fp12q_mul(t2, t2, u, qm);
-  fp12_conj(u, t1);
-  fp12q_mul(t2, t2, u, qm);
-  fp12_cyclotomic_sqr(u, m);
-  fp12q_mul(u, u, m, qm);
-  fp12q_mul(r, t2, u, qm);
+  // temporaries scoped so their frame slots can be shared (pairing_lds.h final_exponentiation_l); r may alias f_in
+  fp12 m;
+  {
+    fp12 t, fi;
+    fp12_conj(t, f_in);
+    fp12_inv(fi, f_in);
+    fp12q_mul(m, t, fi, qm);
+    fp12_frobenius(t, m, 2);
+    fp12q_mul(m, t, m, qm);
+  }
+  fp12 t1;
+  {
+    fp12 t0, u;
+    fp12q_exp_xabs(t0, m, qm);
+    fp12q_mul(t0, t0, m, qm);
+    fp12_conj(t0, t0);
+    fp12q_exp_xabs(u, t0, qm);
+    fp12q_mul(u, u, t0, qm);
+    fp12_conj(t0, u);
+    fp12q_exp_xabs(u, t0, qm);
+    fp12_conj(u, u);
+    fp12_frobenius(t1, t0, 1);
+    fp12q_mul(t1, t1, u, qm);
+  }
+  fp12 t2;
+  {
+    fp12 u;
+    fp12q_exp_xabs(u, t1, qm);
+    fp12q_exp_xabs(u, u, qm);
+    fp12_frobenius(t2, t1, 2);
+    fp12q_mul(t2, t2, u, qm);
+    fp12_conj(u, t1);
+    fp12q_mul(t2, t2, u, qm);
+  }
+  {
+    fp12 u;
+    fp12_cyclotomic_sqr(u, m);
+    fp12q_mul(u, u, m, qm);
+    fp12q_mul(r, t2, u, qm);
+  }
 }
 
 #ifndef BLS_LQ4_FE_QUAD

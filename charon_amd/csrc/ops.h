@@ -56,13 +56,16 @@ BLS_HD BLS_VERIFY_L_CALL int pairing_check_verify_sig_l(const g1a& pk, const g2a
   g1a P1;
   P1.x = G1_GEN_X;
   P1.y = G1_NEG_GEN_Y;
-  fp12 f, e;
-  g2j T1;
-  miller_loop_2_l<S, true>(f, F, pk, hm, P1, sig, &T1);
-  const bool in_g2 = g2_subgroup_from_miller(T1, sig);
-  final_exp_l(e, f, F);
+  fp12 f;
+  bool in_g2;
+  {
+    g2j T1;
+    miller_loop_2_l<S, true>(f, F, pk, hm, P1, sig, &T1);
+    in_g2 = g2_subgroup_from_miller(T1, sig);
+  }
+  final_exp_l(f, f, F);  // in place: one Fp12 less in this frame (final_exponentiation_l allows r == f_in)
   if (!in_g2) return HIPBLS_ERR_SIGNATURE;
-  return fp12_is_one(e) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+  return fp12_is_one(f) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }
 
 // Statuses for the infinity cases (herumi: a valid infinity key or signature fails KeyValidate / the check), once the

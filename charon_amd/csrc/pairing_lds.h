@@ -433,8 +433,11 @@ BLS_HD BLS_INLINE void fp12_mul_l(const f12l<S>& F, const fp12& b) {
 
 // fp12_cyc_exp_xabs_karabina (pairing.h) with the decompressed powers' product accumulated in LDS: the tail's
 // accumulator (144 dwords) no longer shares the registers with the power being decompressed and the saved states.
+// Returns true, leaving r untouched, in the degenerate case: the caller then takes the Granger-Scott exponentiation
+// (fp12_cyc_exp_xabs_l), so that rarely used call chain adds to the caller's stack depth, not to this one's -- every
+// kernel's private segment is sized by its deepest chain (~3 KB less per lane here).
 template <int S>
-BLS_HD BLS_CALL void fp12_cyc_exp_xabs_karabina_l(fp12& r, const fp12& a_in, const f12l<S> F) {
+BLS_HD BLS_CALL bool fp12_cyc_exp_xabs_karabina_l(fp12& r, const fp12& a_in, const f12l<S> F) {
   static_assert(X_ABS == 0xd201000000010000ull, "the squaring counts below are |x|'s set bits");
   cyc_c st[6];  // a^(2^k) for k = 16, 48, 57, 60, 62, 63
   cyc_c c;
@@ -461,7 +464,7 @@ BLS_HD BLS_CALL void fp12_cyc_exp_xabs_karabina_l(fp12& r, const fp12& a_in, con
   pre[0] = den[0];
 #pragma unroll 1
   for (s = 1; s < 6; ++s) fp2_mul(pre[s], pre[s - 1], den[s]);
-  const bool degenerate = fp2_is_zero(pre[5]);
+  if (fp2_is_zero(pre[5])) return true;  // practically never: the identity or z2 = z3 = 0 at one of the six powers
   fp2 inv;
   fp2_inv(inv, pre[5]);
 #pragma unroll 1
@@ -481,43 +484,60 @@ BLS_HD BLS_CALL void fp12_cyc_exp_xabs_karabina_l(fp12& r, const fp12& a_in, con
     else
       fp12_mul_l(F, d);
   }
-  if (degenerate) {  // practically never: the identity or z2 = z3 = 0 at one of the six powers
-    fp12_cyc_exp_xabs_gs(r, a_in);
-    return;
-  }
   F.ld12(r);
+  return false;
+}
+template <int S>
+BLS_HD BLS_INLINE void fp12_cyc_exp_xabs_l(fp12& r, const fp12& a_in, const f12l<S>& F) {
+  if (fp12_cyc_exp_xabs_karabina_l(r, a_in, F)) fp12_cyc_exp_xabs_gs(r, a_in);
 }
 
 // final_exponentiation (pairing.h) with the a^|x| powers on fp12_cyc_exp_xabs_karabina_l; F is free scratch here.
 template <int S>
 BLS_HD BLS_CALL void final_exponentiation_l(fp12& r, const fp12& f_in, const f12l<S> F) {
-  const fp12 f = f_in;
-  fp12 t, fi, m;
-  fp12_conj(t, f);
-  fp12_inv(fi, f);
-  BLS_FE_MUL(m, t, fi);
-  fp12_frobenius(t, m, 2);
-  BLS_FE_MUL(m, t, m);
-  fp12 t0, t1, t2, u;
-  fp12_cyc_exp_xabs_karabina_l(t0, m, F);
-  BLS_FE_MUL(t0, t0, m);
-  fp12_conj(t0, t0);
-  fp12_cyc_exp_xabs_karabina_l(u, t0, F);
-  BLS_FE_MUL(u, u, t0);
-  fp12_conj(t0, u);
-  fp12_cyc_exp_xabs_karabina_l(u, t0, F);
-  fp12_conj(u, u);
-  fp12_frobenius(t1, t0, 1);
-  BLS_FE_MUL(t1, t1, u);
-  fp12_cyc_exp_xabs_karabina_l(u, t1, F);
-  fp12_cyc_exp_xabs_karabina_l(u, u, F);
-  fp12_frobenius(t2, t1, 2);
-  BLS_FE_MUL(t2, t2, u);
-  fp12_conj(u, t1);
-  BLS_FE_MUL(t2, t2, u);
-  fp12_cyclotomic_sqr(u, m);
-  BLS_FE_MUL(u, u, m);
-  BLS_FE_MUL(r, t2, u);
+  // The temporaries are scoped so their stack slots can share space: every Fp12 here is passed by address to a real
+  // call, so it lives in the frame, and at function scope each one held its own 576 B for the whole function (the
+  // frame is part of every verify kernel's private segment).  f_in is read only by the easy part and r written only
+  // at the end, so r may alias f_in.
+  fp12 m;
+  {  // easy part: f^((p^6-1)(p^2+1))
+    fp12 t, fi;
+    fp12_conj(t, f_in);
+    fp12_inv(fi, f_in);
+    BLS_FE_MUL(m, t, fi);
+    fp12_frobenius(t, m, 2);
+    BLS_FE_MUL(m, t, m);
+  }
+  fp12 t1;
+  {  // t0 = m^((x-1)^2), t1 = t0^(x+p)
+    fp12 t0, u;
+    fp12_cyc_exp_xabs_l(t0, m, F);
+    BLS_FE_MUL(t0, t0, m);
+    fp12_conj(t0, t0);
+    fp12_cyc_exp_xabs_l(u, t0, F);
+    BLS_FE_MUL(u, u, t0);
+    fp12_conj(t0, u);
+    fp12_cyc_exp_xabs_l(u, t0, F);
+    fp12_conj(u, u);
+    fp12_frobenius(t1, t0, 1);
+    BLS_FE_MUL(t1, t1, u);
+  }
+  fp12 t2;
+  {  // t2 = t1^(x^2+p^2-1)
+    fp12 u;
+    fp12_cyc_exp_xabs_l(u, t1, F);
+    fp12_cyc_exp_xabs_l(u, u, F);
+    fp12_frobenius(t2, t1, 2);
+    BLS_FE_MUL(t2, t2, u);
+    fp12_conj(u, t1);
+    BLS_FE_MUL(t2, t2, u);
+  }
+  {  // r = t2 m^3
+    fp12 u;
+    fp12_cyclotomic_sqr(u, m);
+    BLS_FE_MUL(u, u, m);
+    BLS_FE_MUL(r, t2, u);
+  }
 }
 #ifndef BLS_FE_LDS
 #define BLS_FE_LDS 1
@@ -537,10 +557,10 @@ BLS_HD BLS_CALL bool pairing_check_verify_l(const g1a& pk, const g2a& hm, const 
   g1a P1;
   P1.x = G1_GEN_X;
   P1.y = G1_NEG_GEN_Y;
-  fp12 f, e;
+  fp12 f;
   miller_loop_2_l<S, true>(f, F, pk, hm, P1, sig, nullptr);
-  final_exp_l(e, f, F);
-  return fp12_is_one(e);
+  final_exp_l(f, f, F);  // in place (final_exponentiation_l allows r == f_in)
+  return fp12_is_one(f);
 }
 
 }  // namespace bls

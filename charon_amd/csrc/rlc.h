@@ -324,10 +324,10 @@ BLS_HD BLS_INLINE bool rlc_window(const f12l<LS>& F, uint64_t i0, uint64_t i1, c
     ++np;
   }
   if (np == 0) return true;
-  fp12 f, e;
+  fp12 f;
   miller_loop_multi_l<RLC_W + 1>(f, F, P, Q, np);
-  final_exp_l(e, f, F);
-  return fp12_is_one(e);
+  final_exp_l(f, f, F);  // in place (final_exponentiation_l allows r == f_in)
+  return fp12_is_one(f);
 }
 
 // ---- lane bodies of the four stages (kernels in hipbls.hip; host loop in tests/native) --------

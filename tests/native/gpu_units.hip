@@ -7,8 +7,8 @@
 //                       halves c0 | c1 of element i.  Covers the lane-pair Karabina fallback (fp2_is_zero(pre[5]) ->
 //                       fp12h_exp_xabs with DPP exchanges), reached when a saved compressed power has z2 = z3 = 0,
 //                       e.g. for the identity and for Fp2 elements (ADVICE r02, lg2.h:263).
-//   gu_exp_xabs_split   fp12h_exp_xabs_karabina on a split value (no easy part): the raw a^|x| of the pair.
-//   gu_quad             final_exponentiation_quad / fp12q_exp_xabs_karabina (lg2.h), a lane quad per element, the
+//   gu_exp_xabs_split   fp12h_exp (Karabina, Granger-Scott when degenerate) on a split value (no easy part): the raw a^|x| of the pair.
+//   gu_quad             final_exponentiation_quad / fp12q_exp_xabs (lg2.h), a lane quad per element, the
 //                       value in full on all four lanes; each lane's result is returned, so the test sees that the four
 //                       agree.  Fp2 elements and the identity take the quad's degenerate branch (Granger-Scott).
 // Elements cross the ABI as 12 big-endian 48-byte Fp coefficients (c0.c0.c0 .. c1.c2.c1), canonical, not Montgomery.
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(64) k_gu_final_exp(const uint8_t* in, uint8_t*
   f12_out(out + 576 * i, r);
 }
 
-// op 0: final_exponentiation_split; op 1: fp12h_exp_xabs_karabina; op 2: fp12h_exp_xabs (Granger-Scott, the fallback)
+// op 0: final_exponentiation_split; op 1: fp12h_exp (Karabina); op 2: fp12h_exp_xabs (Granger-Scott, the fallback)
 __global__ void __launch_bounds__(64) k_gu_split(const uint8_t* in, uint8_t* out, uint64_t n, int op) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t i = t >> 1;
@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(64) k_gu_split(const uint8_t* in, uint8_t* out
   if (op == 0)
     final_exponentiation_split(r, h, m);
   else if (op == 1)
-    fp12h_exp_xabs_karabina(r, h, m);
+    fp12h_exp(r, h, m);  // Karabina, degenerate inputs through the Granger-Scott fallback
   else
     fp12h_exp_xabs(r, h, m);
   fp12 full;
@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(64) k_gu_split(const uint8_t* in, uint8_t* out
   if (!m) f12_out(out + 576 * i, full);
 }
 
-// op 0: final_exponentiation_quad; op 1: fp12q_exp_xabs_karabina.  out holds 4 results per element (lanes 0..3).
+// op 0: final_exponentiation_quad; op 1: fp12q_exp_xabs.  out holds 4 results per element (lanes 0..3).
 __global__ void __launch_bounds__(64) k_gu_quad(const uint8_t* in, uint8_t* out, uint64_t n, int op) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t i = t >> 2;
@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(64) k_gu_quad(const uint8_t* in, uint8_t* out,
   if (op == 0)
     final_exponentiation_quad(r, f, qm);
   else
-    fp12q_exp_xabs_karabina(r, f, qm);
+    fp12q_exp_xabs(r, f, qm);
   f12_out(out + 576 * t, r);
 }
 
