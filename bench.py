@@ -151,7 +151,7 @@ def make_c3(impl, g_lo, g_hi, t=7, n=10):
     assert set(st) <= {0}
     dv_pks, st = impl.secret_to_public_key_batch([s.to_bytes(32, "big") for s in secrets_])
     assert set(st) <= {0}
-    return psigs, part_ids, offs, dv_pks, roots
+    return psigs, part_ids, offs, dv_pks, roots, secrets_
 
 
 def c4_item(tag, v, j, nk, corrupt=True):
@@ -449,7 +449,7 @@ def main():
         G_node = args.tagg_groups * world
         g_lo, g_hi = shard_range(G_node, rank, world)
         G = g_hi - g_lo
-        psigs, pids, poffs, dv_pks, droots = make_c3(impl, g_lo, g_hi)
+        psigs, pids, poffs, dv_pks, droots, dsecrets = make_c3(impl, g_lo, g_hi)
         log("rank %d: C3 slice [%d, %d) of %d validators in %.1fs" % (rank, g_lo, g_hi, G_node, time.time() - t0))
         d_psig = u8(psigs)
         d_pid = torch.tensor(pids, dtype=torch.int64).to(dev)
@@ -477,6 +477,11 @@ def main():
         tagg_kms = kernel_ms(lib, ("tagg_scale", "tagg_sum", "tagg_unscale", "tv_prep_pk",
                                          "verify_pair_lq4", "verify_pair_lg2", "verify_pair_single"))
         assert set(d_gst.cpu().tolist()) == {0} and set(d_vst.cpu().tolist()) == {0}, "aggregate mismatch"
+        # the 96-byte aggregates themselves (herumi.go:244-283 returns exactly these bytes, sigagg.go:149-154 injects
+        # them): each equals Sign(secret) made by the separate sign kernel
+        want_aggs, st_s = impl.sign_batch([s.to_bytes(32, "big") for s in dsecrets], droots)
+        assert set(st_s) <= {0}
+        assert bytes(d_agg.cpu().numpy().tobytes()) == b"".join(want_aggs), "C3 aggregate bytes != Sign(secret)"
         if world > 1:
             assert torch.equal(node_aggs[0][96 * g_lo:96 * g_hi], d_agg), "gathered aggregates differ from local"
             assert bool(node_aggs[1].all()), "an aggregate of the node batch failed Verify"

@@ -33,6 +33,14 @@ def build(force=False, verbose=True, extra=(), out=LIB):
     if verbose:
         print("[hipbls] " + " ".join(cmd), flush=True)
     subprocess.check_call(cmd)
+    # scratch budget per lane (charon_amd/codeobj.py): a deeper kernel fails the build here instead of
+    # exhausting the hardware queues' scratch under load (HSA_STATUS_ERROR_OUT_OF_RESOURCES aborts the process)
+    from charon_amd import codeobj
+    try:
+        codeobj.check_budget(out + ".tmp")
+    except Exception:
+        os.remove(out + ".tmp")
+        raise
     os.replace(out + ".tmp", out)
     return out
 

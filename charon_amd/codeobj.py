@@ -1,0 +1,111 @@
+"""Kernel resource metadata of the built library, read from its gfx950 code object (no GPU, no ROCm tools needed).
+
+libhipbls.so carries a clang offload bundle (section .hip_fatbin, magic __CLANG_OFFLOAD_BUNDLE__) whose
+`hipv4-amdgcn-amd-amdhsa--gfx950` entry is an AMDGPU ELF code object.  Its NT_AMDGPU_METADATA note (msgpack) lists
+every kernel with `.private_segment_fixed_size` (scratch bytes per lane), `.vgpr_count`, `.group_segment_fixed_size`
+(LDS) and the rest.
+
+Why it matters: each hardware queue that runs a kernel holds a scratch allocation sized by that
+kernel's private segment over the waves the device can hold, and HIP spreads a process's streams over
+GPU_MAX_HW_QUEUES (4) hardware queues.  Round 3 saw HSA_STATUS_ERROR_OUT_OF_RESOURCES (a process abort, not an error
+code) under 32-64 concurrent callers once every queue carried ~17.9 KB/lane kernels; the fix was headroom
+(12.7 KB/lane) plus one stream per queue.  `build.py` now refuses a library whose deepest kernel exceeds
+PRIVATE_SEGMENT_BUDGET, so a regression fails the build instead of aborting a node under load.
+"""
+import struct
+
+# Bytes of scratch per lane that any kernel may use (round-3 maximum: k_verify_pair_lq4, 12,744 B).
+PRIVATE_SEGMENT_BUDGET = 13312
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+NT_AMDGPU_METADATA = 32
+
+
+def code_object(path: str, target: str = TARGET) -> bytes:
+    """The code object of `target` inside the library's offload bundle."""
+    with open(path, "rb") as f:
+        d = f.read()
+    i = d.find(BUNDLE_MAGIC)
+    if i < 0:
+        raise ValueError("%s: no clang offload bundle (compressed bundles are not expected here)" % path)
+    (n,) = struct.unpack_from("<Q", d, i + 24)
+    p = i + 32
+    for _ in range(n):
+        off, size, idlen = struct.unpack_from("<QQQ", d, p)
+        tid = d[p + 24:p + 24 + idlen].decode()
+        p += 24 + idlen
+        if tid == target:
+            return d[i + off:i + off + size]
+    raise ValueError("%s: no %s code object" % (path, target))
+
+
+def _notes(elf: bytes):
+    """(name, type, desc) of every note in the ELF64 little-endian image's SHT_NOTE sections."""
+    if elf[:4] != b"\x7fELF" or elf[4] != 2 or elf[5] != 1:
+        raise ValueError("not an ELF64 little-endian code object")
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", elf, 0x3A)
+    for k in range(shnum):
+        sh = shoff + k * shentsize
+        sh_type, = struct.unpack_from("<I", elf, sh + 4)
+        if sh_type != 7:  # SHT_NOTE
+            continue
+        off, size = struct.unpack_from("<QQ", elf, sh + 0x18)
+        p, end = off, off + size
+        while p + 12 <= end:
+            namesz, descsz, ntype = struct.unpack_from("<III", elf, p)
+            p += 12
+            name = elf[p:p + namesz].rstrip(b"\0").decode()
+            p += (namesz + 3) & ~3
+            desc = elf[p:p + descsz]
+            p += (descsz + 3) & ~3
+            yield name, ntype, desc
+
+
+def kernels(path: str):
+    """{kernel symbol name: metadata dict} from the library's gfx950 code object."""
+    import msgpack
+    for name, ntype, desc in _notes(code_object(path)):
+        if name == "AMDGPU" and ntype == NT_AMDGPU_METADATA:
+            md = msgpack.unpackb(desc, raw=False)
+            return {k[".name"]: k for k in md["amdhsa.kernels"]}
+    raise ValueError("%s: no AMDGPU metadata note" % path)
+
+
+def short_name(mangled: str) -> str:
+    """k_verify_fused from _ZN12_GLOBAL__N_114k_verify_fusedEPKh... (anonymous-namespace kernels)."""
+    s = mangled
+    if s.startswith("_ZN12_GLOBAL__N_1"):
+        s = s[len("_ZN12_GLOBAL__N_1"):]
+        j = 0
+        while j < len(s) and s[j].isdigit():
+            j += 1
+        if j:
+            return s[j:j + int(s[:j])]
+    return mangled
+
+
+def resource_table(path: str):
+    """[(kernel, scratch B/lane, VGPRs incl. AGPRs, LDS B)] sorted by scratch, deepest first."""
+    rows = [(short_name(n), int(k.get(".private_segment_fixed_size", 0)), int(k.get(".vgpr_count", 0)),
+             int(k.get(".group_segment_fixed_size", 0))) for n, k in kernels(path).items()]
+    return sorted(rows, key=lambda r: -r[1])
+
+
+def check_budget(path: str, budget: int = PRIVATE_SEGMENT_BUDGET):
+    """Raises if any kernel's private segment exceeds the budget; returns the resource table otherwise."""
+    rows = resource_table(path)
+    over = [r for r in rows if r[1] > budget]
+    if over:
+        raise RuntimeError("kernel private segment above the %d B/lane budget (DESIGN.md 5.1.1): %s"
+                           % (budget, ", ".join("%s %d B" % (r[0], r[1]) for r in over)))
+    return rows
+
+
+if __name__ == "__main__":
+    import os
+    import sys
+    lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                              "libhipbls.so")
+    for r in resource_table(lib):
+        print("%-28s scratch %6d B/lane  vgpr %4d  lds %6d B" % r)

@@ -21,6 +21,7 @@
 //     entry point binds its context's device on the calling thread before it touches memory or streams.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <chrono>
@@ -45,6 +46,12 @@ namespace {
 
 // ============================================================================ device contexts
 thread_local std::string g_last_error;
+
+// Library streams per device: the library stream, the two fork sub-streams (RLC sub-batches, sigagg) and the
+// submission queue's stream.  HIP maps a process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues, and each
+// hardware queue that runs these kernels sizes its scratch by the deepest private segment (charon_amd/codeobj.py
+// PRIVATE_SEGMENT_BUDGET): four streams keep the library's own launches one hardware queue apiece.
+constexpr int kStreamsPerDevice = 4;
 
 struct DevBuf {
   void* p = nullptr;
@@ -146,7 +153,10 @@ struct Context {
   hipEvent_t ev_fork = nullptr, ev_hash = nullptr, ev_join[kSub] = {};
   // Last workspace user's completion (cross-stream ordering), per workspace group: the general buffers (b_*, v_ws) and
   // the RLC ones (r_*, m_*, the H(m) cache), so an RLC batch and, say, a FastAggregateVerify on another stream (the C5
-  // slot mix) overlap instead of queueing behind each other.
+  // slot mix) overlap instead of queueing behind each other.  The two groups still SHARE the fork sub-streams
+  // (sub[0], sub[1], the device's) and the fork/join events (ev_fork, ev_hash, ev_join): launch_rlc,
+  // launch_rlc_batch and launch_tagg_verify issue every record/wait pair on those within one call under c.mu, which
+  // is what makes the sharing safe; a sigagg call queued behind an RLC batch's sub-stream work waits for it there.
   hipEvent_t ws_done = nullptr, ws_done_rlc = nullptr;
   uint64_t r_windows = 0;        // window count of this context's last RLC call (hipbls_rlc_stats)
   uint64_t r_call = 0;           // entry-point call that call belonged to
@@ -174,6 +184,7 @@ struct Context {
 
 // The context list is written once, under g_init_mu, before g_nctx is published; contexts live for the process.
 std::vector<Context*> g_ctxs;
+std::map<int, int> g_streams_per_device;  // library streams created per device (written once at init)
 std::atomic<int> g_nctx{0};
 std::mutex g_init_mu;
 std::atomic<bool> g_timing{false};
@@ -207,18 +218,32 @@ int init_locked(const std::vector<int>& ids) {
   for (int d : ids)
     if (d < 0 || d >= ndev) return arg_err("device index out of range");
   std::vector<Context*> made;
+  std::map<int, std::array<hipStream_t, kStreamsPerDevice>> dev_streams;
   for (size_t k = 0; k < ids.size(); ++k) {
     Context* c = new Context();
     c->device = ids[k];
     c->slot = (int)k;
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // One set of library streams per DEVICE, shared by every context on it (streams only add ordering, and every
+    // event a context records or waits on is its own): the library never holds more than kStreamsPerDevice streams
+    // on a device, whatever the number of contexts.
+    auto it = dev_streams.find(c->device);
+    if (it == dev_streams.end()) {
+      std::array<hipStream_t, kStreamsPerDevice> ss{};
+      for (auto& x : ss) HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+      it = dev_streams.emplace(c->device, ss).first;
+    }
+    c->stream = it->second[0];
+    c->sub[0] = it->second[1];
+    c->sub[1] = it->second[2];
+    c->q.stream = it->second[3];
     HIP_TRY(hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ws_done_rlc, hipEventDisableTiming));
     made.push_back(c);
   }
   const char* t = getenv("HIPBLS_TIMING");
   if (t && t[0] == '1') g_timing = true;
+  for (auto& kv : dev_streams) g_streams_per_device[kv.first] = (int)kv.second.size();
   g_ctxs = made;
   g_nctx.store((int)made.size(), std::memory_order_release);
   return HIPBLS_OK;
@@ -510,9 +535,8 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
                      int32_t* d_status, hipStream_t s, const uint32_t* d_kidx, uint32_t* d_H, uint64_t hstride,
                      const uint32_t* d_hslot, const uint32_t* d_mlist, uint64_t n_hash);
 
-int ensure_rlc_streams(Context& c) {
+int ensure_rlc_streams(Context& c) {  // the sub-streams are the device's (init_locked); the events are the context's
   if (c.ev_fork) return HIPBLS_OK;
-  for (int k = 0; k < Context::kSub; ++k) HIP_TRY(hipStreamCreateWithFlags(&c.sub[k], hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&c.ev_hash, hipEventDisableTiming));
   for (int k = 0; k < Context::kSub; ++k) HIP_TRY(hipEventCreateWithFlags(&c.ev_join[k], hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
@@ -1310,8 +1334,7 @@ void batch_done(VerifyQueue& q, VBatch& b, int rc) {
 void queue_worker(Context* cp) {
   Context& c = *cp;
   VerifyQueue& q = c.q;
-  bool dev_ok = hipSetDevice(c.device) == hipSuccess &&
-                hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) == hipSuccess;
+  bool dev_ok = hipSetDevice(c.device) == hipSuccess && q.stream != nullptr;  // the device's queue stream
   // Both slots run on the queue's one stream: the next batch's copies and kernels are enqueued behind the running
   // batch (no host round trip between them), and the queue occupies one hardware queue.  Every hardware queue that
   // runs these kernels holds a scratch allocation sized for ~17 KB per lane over the whole device; with a stream per
@@ -1348,6 +1371,9 @@ void queue_worker(Context* cp) {
       QSlot& sl = q.slot[k];
       sl.b = b;
       sl.rc = dev_ok ? wire_launch(c, sl, *b) : HIPBLS_ERR_DEVICE;
+      // A launch that failed after its first copy was queued never records done_ev, and batch_done frees the batch's
+      // host vectors as soon as it is collected: drain the stream first so no queued copy reads freed memory.
+      if (sl.rc != HIPBLS_OK && dev_ok) (void)hipStreamSynchronize(sl.stream);
       lk.lock();
       if (!q.inflight.empty()) q.overlapped += 1;
       q.inflight.push_back(k);
@@ -1754,6 +1780,12 @@ int hipbls_device_count(void) {
 
 int hipbls_current_device(void) { return nctx() ? ctx(0).device : -1; }
 
+int hipbls_device_streams(int device) {
+  if (!nctx()) return 0;
+  auto it = g_streams_per_device.find(device);
+  return it == g_streams_per_device.end() ? 0 : it->second;
+}
+
 int hipbls_device_slots(int32_t* ids, uint32_t cap) {
   const int n = nctx();
   for (int k = 0; k < n && ids && (uint32_t)k < cap; ++k) ids[k] = ctx(k).device;
@@ -2079,20 +2111,27 @@ int hipbls_aggregate(const uint8_t* sigs, uint64_t n, uint8_t* out_sig, int32_t*
     });
   std::vector<uint8_t> part(96 * k);
   std::vector<int32_t> pst(k, HIPBLS_OK);
+  std::vector<char> filled(k, 0);
   int rc = run_ranges(b, [&](Context& c, uint64_t lo, uint64_t hi) {
-    const size_t j = (size_t)c.slot;  // range j runs on context j
+    // the range's own index (the last bound <= lo: an empty range before it shares its start), not the context's
+    const size_t j = (size_t)(std::upper_bound(b.begin(), b.end() - 1, lo) - b.begin()) - 1;
+    filled[j] = 1;
     return aggregate_host(c, sigs + 96 * lo, hi - lo, part.data() + 96 * j, &pst[j]);
   });
   if (rc) return rc;
-  for (size_t j = 0; j < k; ++j)
+  std::vector<uint8_t> parts;  // the non-empty ranges' sums only (an empty range left 96 zero bytes, not a point)
+  for (size_t j = 0; j < k; ++j) {
+    if (!filled[j]) continue;
     if (pst[j] != HIPBLS_OK) {
       *status = pst[j];
       memset(out_sig, 0, 96);
       return HIPBLS_OK;
     }
+    parts.insert(parts.end(), part.begin() + 96 * j, part.begin() + 96 * (j + 1));
+  }
   Context& c0 = ctx(0);
   ENTER_CTX(c0);
-  return aggregate_host(c0, part.data(), k, out_sig, status);
+  return aggregate_host(c0, parts.data(), parts.size() / 96, out_sig, status);
 }
 
 int hipbls_aggregate_device(const uint8_t* d_sigs, uint64_t n, uint8_t* d_out_sig, int32_t* d_status, void* stream) {

@@ -89,6 +89,7 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_abi_version": ([], ctypes.c_int),
         "hipbls_init": ([ctypes.c_int], ctypes.c_int),
         "hipbls_device_count": ([], ctypes.c_int),
+        "hipbls_device_streams": ([ctypes.c_int], ctypes.c_int),
         "hipbls_last_error": ([], ctypes.c_char_p),
         "hipbls_verify_batch": ([u8p, u8p, u64p, u8p, u64, i32p], ctypes.c_int),
         "hipbls_threshold_aggregate_batch": ([u8p, i64p, u64p, u64, u8p, i32p], ctypes.c_int),
@@ -141,7 +142,7 @@ def exported_symbols() -> List[str]:
         "hipbls_hcache_config", "hipbls_hcache_stats", "hipbls_set_pair_mode",
         "hipbls_rlc_set_mode", "hipbls_rlc_batch_stats", "hipbls_threshold_aggregate_verify_batch",
         "hipbls_threshold_aggregate_verify_batch_device", "hipbls_init_devices", "hipbls_device_slots",
-        "hipbls_plan_ranges", "hipbls_queue_keyed_batches", "hipbls_deserialize_status",
+        "hipbls_plan_ranges", "hipbls_queue_keyed_batches", "hipbls_deserialize_status", "hipbls_device_streams",
     ]
 
 

@@ -61,7 +61,7 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 10
+#define HIPBLS_ABI_VERSION 11
 int hipbls_abi_version(void);
 
 /* Bind the library to the n devices ids[0..n) (n <= 64; a device may repeat: each entry is one context, e.g. to
@@ -80,6 +80,10 @@ int hipbls_device_slots(int32_t* ids, uint32_t cap);
 int hipbls_plan_ranges(uint64_t n, uint32_t parts, const uint32_t* run_keys, uint64_t* bounds);
 /* Number of visible HIP devices (0 when none). */
 int hipbls_device_count(void);
+/* Streams the library created on `device` (its library stream, two fork sub-streams and the submission queue's
+ * stream), shared by every context bound to that device: at most 4 whatever the number of contexts, so the library's
+ * launches never need more than GPU_MAX_HW_QUEUES hardware queues.  0 for a device without a context. */
+int hipbls_device_streams(int device);
 /* Thread-local text of the last HIPBLS_ERR_DEVICE / HIPBLS_ERR_ARG. */
 const char* hipbls_last_error(void);
 /* Device index the library is bound to (-1 before the first call). */

@@ -89,6 +89,8 @@ def main():
         x.join()
     out["queue"] = np.array(got, dtype=np.int32)
     out["queue_keyed"] = np.array([impl.queue_keyed_batches()], dtype=np.int64)
+    # K contexts on one device share the device's library streams: at most 4, not 4 K
+    out["streams"] = np.array([impl.lib.hipbls_device_streams(0)], dtype=np.int64)
     np.savez(dst, **out)
     print("multidev child: %d contexts ok" % k)
 

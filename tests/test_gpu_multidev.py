@@ -137,3 +137,4 @@ def test_three_contexts_equal_unsplit(impl, tmp_path):
     # the window statistics of the split RLC call cover the whole batch; the queue's batches ran keyed
     assert got["rlc_stats"][0] >= (n + 7) // 8
     assert got["queue_keyed"][0] > 0
+    assert got["streams"][0] == 4  # three contexts on device 0, one set of library streams
