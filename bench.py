@@ -42,6 +42,11 @@ RLC_FPMUL = {"item": 5802, "hash": 4790, "window_2msg": 21906, "window_1msg": 17
 # (2 points x 2 windows of mixed additions; the bucket/segment folds add ~15 per item at 1M items and are left
 # out), and one multi-Miller loop per 16-item chunk with 4 message runs (one root per 4-partial validator).
 RLCB_FPMUL = {"item": 4306, "msm_per_item": 116, "chunk_4runs": 18948}
+# sigagg in one call (C3), per aggregate of 7 partials, same unit and source (tests/native/host_ops.cpp
+# ht_count_tagg_verify, tests/test_work_counts.py): the 7 partials' decode + subgroup test + c_k sig_k (k_tagg_scale),
+# the sum S (k_tagg_sum_s), [L^-1] S + compress (k_tagg_unscale), the root key's decode + subgroup test + [L] pk +
+# hash_to_G2 (k_tv_prep_pk), and the pairing check on S against [L] pk (k_verify_pair_lq4).
+TAGG_FPMUL = {"scale_7": 17209, "sum": 274, "unscale": 4071, "key_prep": 6493, "pairing": 17012}
 # gfx950 32x32->64 integer multiply-add peak (v_mad_u64_u32): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 # at half rate (measured: profiles/r01_mad_probe.txt) = 39.3e12 MAD/s.
 MAD_PEAK_T = 39.3
@@ -63,8 +68,13 @@ def parse():
                     help="C4 node batch in validators (x4 partials; 262,144 = 1M partials), sliced over the ranks "
                          "with shard_range (0 = skip)")
     ap.add_argument("--rlc-steps", type=int, default=3)
+    ap.add_argument("--rlc-variants", default="i,ii,all_valid",
+                    help="C4 variants to time: i (one root per validator), ii (committee roots), all_valid")
     ap.add_argument("--c5", type=int, default=1, help="time the C5 full-slot mix (0 = skip)")
     ap.add_argument("--keys", type=int, default=1, help="also time C2 / C4 with the resident pubshare table (0 = skip)")
+    ap.add_argument("--latency-calls", type=int, default=200,
+                    help="synchronous n = 1 tbls.Verify calls (hipbls_verify on an idle queue) timed one after another, "
+                         "the unpatched parsigex loop's shape (0 = skip; rank 0 only)")
     return ap.parse_args()
 
 
@@ -421,6 +431,28 @@ def main():
     lib.hipbls_kernel_timing(b"verify", ctypes.byref(avg_ms), ctypes.byref(launches))
     value = n_node * args.steps / elapsed
 
+    # ---- drop-in latency: the unpatched callers run tbls.Verify one item at a time, synchronously
+    # (core/parsigex/parsigex.go:86-91 verifies a peer's set in series, validatorapi.go:246-283 every attestation):
+    # each call is one n = 1 batch through the submission queue, so the serial rate is 1 / latency.  Rank 0, untimed
+    # by the step loop (it is a latency, not a throughput).
+    latency = None
+    if args.latency_calls > 0 and rank == 0:
+        k = min(args.latency_calls, n)
+        assert impl.verify_queued(pks[0], roots[0], sigs[0]) == st[0]  # starts the queue worker
+        lat = []
+        t0 = time.perf_counter()
+        for j in range(k):
+            a = time.perf_counter()
+            got = impl.verify_queued(pks[j], roots[j], sigs[j])
+            lat.append(time.perf_counter() - a)
+            assert got == st[j], "queued Verify differs from the batch call"
+        tot = time.perf_counter() - t0
+        lat.sort()
+        latency = {"calls": k, "p50_ms": round(1000 * lat[k // 2], 3), "p90_ms": round(1000 * lat[(9 * k) // 10], 3),
+                   "min_ms": round(1000 * lat[0], 3), "serial_verifies_per_s": round(k / tot, 1),
+                   "seconds_per_1000_serial": round(1000 * tot / k, 2),
+                   "path": "hipbls_verify (submission queue, n = 1 batch: prep + lane-quad pairing check)"}
+
     # ---- C2 with the resident pubshare table (extra field): same items, keys by index
     keys_rate = None
     if args.keys:
@@ -444,6 +476,7 @@ def main():
     # slice; the 96-byte aggregates and the verify bitmap are all-gathered inside the timed step
     tagg = None
     tagg_kms = {}
+    tagg_roofline = None
     if args.tagg_groups > 0:
         t0 = time.time()
         G_node = args.tagg_groups * world
@@ -486,6 +519,24 @@ def main():
             assert torch.equal(node_aggs[0][96 * g_lo:96 * g_hi], d_agg), "gathered aggregates differ from local"
             assert bool(node_aggs[1].all()), "an aggregate of the node batch failed Verify"
         tagg = G_node * args.tagg_steps / tel
+        # C3 roofline: the counted per-aggregate unit over the whole call's wall time (the pipeline), and per stage over
+        # its kernel's average launch time (HIP events on the launch stream)
+        unit = sum(TAGG_FPMUL.values())
+        ach = unit * MADS_PER_FPMUL * G * args.tagg_steps / tel / 1e12
+
+        def kfrac(name, fpmul):
+            a, c = kernel_stats(lib, name)
+            return round(fpmul * MADS_PER_FPMUL / (a * 1e-3) / 1e12 / MAD_PEAK_T, 4) if c else None
+
+        tagg_roofline = {
+            "algorithmic_unit": "%d Fp-mul-equivalents x %d MADs per aggregate (7 partials + Verify)" % (unit,
+                                                                                                     MADS_PER_FPMUL),
+            "achieved": round(ach, 3), "peak": MAD_PEAK_T, "unit": "Tmad/s", "frac": round(ach / MAD_PEAK_T, 4),
+            "note": "whole sigagg call (5 kernels on 3 streams) over wall time",
+            "stage_frac": {"tagg_scale": kfrac("tagg_scale", TAGG_FPMUL["scale_7"] * G),
+                           "tv_prep_pk": kfrac("tv_prep_pk", TAGG_FPMUL["key_prep"] * G),
+                           "tagg_unscale": kfrac("tagg_unscale", TAGG_FPMUL["unscale"] * G),
+                           "verify_pair_lq4": kfrac("verify_pair_lq4", TAGG_FPMUL["pairing"] * G)}}
 
     # ---- C4: RLC BatchVerify of the 1M-partial node batch, validator-index slices over the ranks (strong scaling:
     # the node batch is fixed); node bitmap all-gathered inside the timed step
@@ -495,9 +546,12 @@ def main():
         V = args.rlc_node_validators
         v_lo, v_hi = shard_range(V, rank, world)
         keys4 = share_keys(impl, 4096, "c4")
+        chosen = set(args.rlc_variants.split(","))
         for variant, tag, n_roots, corrupt in (("i_root_per_validator", "c4i", 0, True),
                                                ("ii_committee_roots", "c4ii", max(1, V // 128), True),
                                                ("i_all_valid", "c4h", 0, False)):
+            if {"i_root_per_validator": "i", "ii_committee_roots": "ii", "i_all_valid": "all_valid"}[variant] not in chosen:
+                continue
             # the mode HIPBLS_RLC_AUTO settles on for each stream: windows while invalid partials keep arriving
             # (its batch-wide check keeps failing), the batch-wide check for an all-valid stream
             impl.set_rlc_mode(RLC_BATCH if not corrupt else RLC_WINDOWS)
@@ -695,9 +749,11 @@ def main():
                        "items_per_gpu": args.n, "node_items": n_node,
                        "parallelism": "shard-by-validator-index x %d (RCCL all-gather of the verify bitmaps)" % world},
             "pairings_per_s": round(2 * value, 1),
+            "drop_in_latency": latency,
             "verified_partial_sigs_per_s_pubshare_table": round(keys_rate, 1) if keys_rate else None,
             "threshold_aggregates_per_s": round(tagg, 1) if tagg else None,
             "threshold_aggregate_kernel_avg_ms": tagg_kms or None,
+            "threshold_aggregate_roofline": tagg_roofline,
             "threshold_aggregate_workload": "C3: %d validators per GPU x 7-of-10 Lagrange in G2 + Verify of each "
                                             "aggregate (hipbls_threshold_aggregate_verify_batch_device, sigagg in one "
                                             "call); aggregates and bitmap all-gathered" % args.tagg_groups

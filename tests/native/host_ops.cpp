@@ -298,6 +298,67 @@ void ht_count_verify(const uint8_t* pk, const uint8_t* msg, uint32_t len, const 
   out2[1] = g_fp_sqr_count;
 }
 
+// Fp-multiplication counts (mul + sqr) of ONE sigagg group through the stages of hipbls_threshold_aggregate_verify
+// (kernels.h): out5[0] every partial's k_tagg_scale work (decode, subgroup test, c_k sig_k or lambda_k sig_k),
+// out5[1] k_tagg_sum_s (the sum S, affine), out5[2] k_tagg_unscale ([L^-1] S, compress), out5[3] the key side of
+// k_tv_prep_pk (decode + subgroup test, [L] pk, hash_to_G2), out5[4] the pairing check on S against [L] pk (what
+// k_verify_pair_lq4 splits over a lane quad).  Returns the verify status.  The C3 roofline unit (bench.py
+// TAGG_FPMUL, tests/test_work_counts.py).
+int ht_count_tagg_verify(const uint8_t* sigs, const int64_t* ids, int t, const uint8_t* pk48, const uint8_t* msg,
+                         uint32_t len, uint64_t* out5) {
+  auto take = [](uint64_t* o) {
+    *o = g_fp_mul_count + g_fp_sqr_count;
+    g_fp_mul_count = 0;
+    g_fp_sqr_count = 0;
+  };
+  if (t < 1 || t > 16) return HIPBLS_ERR_COMBINE;
+  g_fp_mul_count = 0;
+  g_fp_sqr_count = 0;
+  g2j part[16];
+  for (int me = 0; me < t; ++me) {  // k_tagg_scale, one lane per partial
+    int64_t c = 0;
+    uint64_t L = 0;
+    const bool small = lagrange_small(ids, t, me, c, L);
+    g2a s;
+    if (g2_decompress(s, sigs + 96 * me, !small) != DEC_OK) return HIPBLS_ERR_SIGNATURE;
+    g2j sj;
+    jac_from_aff(sj, s);
+    if (small) {
+      if (!g2_subgroup_and_mul_i64(part[me], sj, c)) return HIPBLS_ERR_SIGNATURE;
+    } else {
+      tagg_scale_point(part[me], sj, ids, t, me);
+    }
+  }
+  take(&out5[0]);
+  g2j acc;  // k_tagg_sum_s
+  jac_set_inf(acc);
+  for (int me = 0; me < t; ++me) {
+    g2j x = acc;
+    jac_add(acc, x, part[me]);
+  }
+  const bool inf = jac_is_inf(acc);
+  g2a S;
+  if (!inf) jac_to_aff(S, acc);
+  take(&out5[1]);
+  g2j u = acc;  // k_tagg_unscale
+  if (!inf) jac_from_aff(u, S);
+  tagg_unscale(u, ids, t);
+  uint8_t sig[96];
+  g2_compress(sig, u);
+  take(&out5[2]);
+  g1a pk;  // k_tv_prep_pk
+  if (g1_decompress(pk, pk48, true) != DEC_OK) return HIPBLS_ERR_PUBKEY;
+  g1_scale_affine(pk, tagg_group_L(ids, t));
+  g2j hj;
+  hash_to_g2(hj, msg, len, DST_POP, 43);
+  g2a hm;
+  jac_to_aff(hm, hj);
+  take(&out5[3]);
+  const int st = inf ? HIPBLS_ERR_VERIFY : pairing_check_verify_sig(pk, hm, S);  // k_verify_pair_lq4
+  take(&out5[4]);
+  return st;
+}
+
 void ht_reset_counts(void) {
   g_fp_mul_count = 0;
   g_fp_sqr_count = 0;

@@ -1,0 +1,113 @@
+"""The Go side of the drop-in ships as files (VERDICT r03 "Next round" 9): integration/charon/ holds the new charon
+files (tbls/hipbls, the suite hook, the app feature switch) and integration/patches/ the unified diffs against the
+reference tree.  No Go toolchain exists here, so these CPU checks pin what can be pinned without one:
+
+* the patch series applies cleanly, in order, to the reference's own files (when /root/reference is present) and
+  touches exactly the insertion points INTEGRATION.md names;
+* the new files inside 0002/0004 are byte-identical to integration/charon/ (no drift between the two forms);
+* every C.hipbls_* function and C.HIPBLS_* constant the cgo code uses is declared by include/hipbls.h, and the ABI
+  version the package checks is the header's;
+* every tbls.Implementation method of the reference interface (tbls/tbls.go:28-69) has a HipBLS method.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INT = os.path.join(ROOT, "integration")
+PATCHES = sorted(os.path.join(INT, "patches", f) for f in os.listdir(os.path.join(INT, "patches"))
+                 if f.endswith(".patch"))
+REF = "/root/reference"
+HEADER = os.path.join(ROOT, "include", "hipbls.h")
+
+
+def _patched_files(patch):
+    return re.findall(r"^\+\+\+ b/(\S+)", open(patch).read(), flags=re.M)
+
+
+def _new_file_body(patch, path):
+    """The added lines of a /dev/null -> b/path hunk."""
+    txt = open(patch).read()
+    m = re.search(r"^--- /dev/null\n\+\+\+ b/" + re.escape(path) + r"\n@@[^\n]*@@\n((?:\+[^\n]*\n|\\[^\n]*\n)*)", txt,
+                  flags=re.M)
+    assert m, path
+    return "".join(line[1:] + "\n" for line in m.group(1).splitlines() if line.startswith("+"))
+
+
+def test_patch_series_targets():
+    touched = [f for p in PATCHES for f in _patched_files(p)]
+    for f in ("tbls/tbls.go", "core/parsigex/parsigex.go", "core/validatorapi/validatorapi.go", "core/sigagg/sigagg.go",
+              "core/eth2signeddata.go", "app/app.go", "app/featureset/featureset.go", "tbls/hipbls/hipbls.go",
+              "tbls/hipbls/batch.go", "tbls/hipbls_suite_test.go"):
+        assert f in touched, f
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree absent (GPU box)")
+def test_patch_series_applies_to_reference(tmp_path):
+    for p in PATCHES:
+        for f in _patched_files(p):
+            src = os.path.join(REF, f)
+            if os.path.exists(src) and not os.path.exists(tmp_path / f):
+                os.makedirs(os.path.dirname(tmp_path / f), exist_ok=True)
+                shutil.copy(src, tmp_path / f)
+    for p in PATCHES:
+        r = subprocess.run(["patch", "-p1", "--forward", "-s", "-d", str(tmp_path), "-i", p], capture_output=True,
+                           text=True)
+        assert r.returncode == 0, (p, r.stdout, r.stderr)
+    s = open(tmp_path / "tbls" / "tbls.go").read()
+    assert "type BatchVerifier interface" in s and "func Impl() Implementation" in s
+    assert "verifySetFunc" in open(tmp_path / "core" / "parsigex" / "parsigex.go").read()
+    assert "tbls.BatchThresholdAggregate(groups)" in open(tmp_path / "core" / "sigagg" / "sigagg.go").read()
+
+
+def test_new_files_match_integration_tree():
+    for p in PATCHES:
+        for f in _patched_files(p):
+            local = os.path.join(INT, "charon", f)
+            if "--- /dev/null\n+++ b/" + f in open(p).read():
+                assert os.path.exists(local), f
+                assert _new_file_body(p, f) == open(local).read(), f
+
+
+def _header_names():
+    h = open(HEADER).read()
+    funcs = set(re.findall(r"\b(hipbls_[a-z0-9_]+)\s*\(", h))
+    consts = set(re.findall(r"\b(HIPBLS_[A-Z0-9_]+)\b", h))
+    abi = int(re.search(r"#define HIPBLS_ABI_VERSION (\d+)", h).group(1))
+    return funcs, consts, abi
+
+
+def test_cgo_uses_only_header_symbols():
+    funcs, consts, abi = _header_names()
+    src = ""
+    for dirpath, _, files in os.walk(os.path.join(INT, "charon")):
+        for f in files:
+            if f.endswith(".go"):
+                src += open(os.path.join(dirpath, f)).read()
+    used_f = set(re.findall(r"\bC\.(hipbls_[a-z0-9_]+)\(", src))
+    used_c = set(re.findall(r"\bC\.(HIPBLS_[A-Z0-9_]+)\b", src))
+    assert used_f and used_f <= funcs, used_f - funcs
+    assert used_c and used_c <= consts, used_c - consts
+    m = re.search(r"const abiVersion = (\d+)", open(os.path.join(INT, "charon", "tbls", "hipbls", "hipbls.go")).read())
+    assert m and int(m.group(1)) == abi
+
+
+def test_every_implementation_method_bound():
+    methods = ["GenerateSecretKey", "GenerateInsecureKey", "SecretToPublicKey", "ThresholdSplitInsecure",
+               "ThresholdSplit", "RecoverSecret", "ThresholdAggregate", "Verify", "Sign", "VerifyAggregate",
+               "Aggregate"]
+    if os.path.isdir(REF):  # the interface as the reference declares it
+        iface = open(os.path.join(REF, "tbls", "tbls.go")).read()
+        body = iface[iface.index("type Implementation interface"):]
+        body = body[:body.index("\n}\n")]
+        assert sorted(set(re.findall(r"^\t([A-Z]\w*)\(", body, flags=re.M))) == sorted(methods)
+    src = open(os.path.join(INT, "charon", "tbls", "hipbls", "hipbls.go")).read()
+    for m in methods:
+        assert re.search(r"^func \((?:\w+ )?HipBLS\) " + m + r"\(", src, flags=re.M), m
+    batch = open(os.path.join(INT, "charon", "tbls", "hipbls", "batch.go")).read()
+    for m in ("BatchVerify", "BatchVerifyRLC", "BatchThresholdAggregate", "BatchVerifyAggregate",
+              "BatchThresholdAggregateVerify"):
+        assert re.search(r"^func \((?:\w+ )?HipBLS\) " + m + r"\(", batch, flags=re.M), m

@@ -81,3 +81,31 @@ def test_bench_rlcb_stage_counts_match():
     want = bench.RLCB_FPMUL
     assert abs(cnt[0] / n - want["item"]) / want["item"] < 0.02
     assert abs(cnt[3] / 4 - want["chunk_4runs"]) / want["chunk_4runs"] < 0.02
+
+
+def test_bench_tagg_counts_match():
+    """bench.TAGG_FPMUL (the C3 roofline's per-aggregate unit) against the host build of the fused sigagg stages over
+    seeded 7-of-10 groups on ids 1..10 (the small-integer Lagrange path the bench's groups take)."""
+    import bench
+    L = lib()
+    rng = random.Random(0xC3)
+    tot = [0] * 5
+    N = 4
+    for _ in range(N):
+        secret = rng.randrange(1, bls.R)
+        poly = [secret] + [rng.randrange(bls.R) for _ in range(6)]
+        ids = sorted(rng.sample(range(1, 11), 7))
+        msg = rng.randbytes(32)
+        sigs = []
+        for i in ids:
+            acc = 0
+            for c in reversed(poly):
+                acc = (acc * i + c) % bls.R
+            sigs.append(bls.sign(acc.to_bytes(32, "big"), msg))
+        pk = bls.secret_to_public_key(secret.to_bytes(32, "big"))
+        out = (ctypes.c_uint64 * 5)()
+        assert L.ht_count_tagg_verify(b"".join(sigs), (ctypes.c_int64 * 7)(*ids), 7, pk, msg, 32, out) == 0
+        tot = [a + b for a, b in zip(tot, out)]
+    want = bench.TAGG_FPMUL
+    for k, got in zip(("scale_7", "sum", "unscale", "key_prep", "pairing"), tot):
+        assert abs(got / N - want[k]) / want[k] < 0.03, (k, got / N)
