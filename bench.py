@@ -507,8 +507,8 @@ def main():
         torch.cuda.synchronize(dev)
         lib.hipbls_kernel_timing_reset()
         tel = timed_loop(tstep, args.tagg_steps, dev, barrier, world)
-        tagg_kms = kernel_ms(lib, ("tagg_scale", "tagg_sum", "tagg_unscale", "tv_prep_pk", "tv_pk_loop",
-                                         "tv_check_lq4", "verify_pair_lq4", "verify_pair_lg2", "verify_pair_single"))
+        tagg_kms = kernel_ms(lib, ("tagg_scale", "tagg_sum", "tagg_unscale", "tv_prep_pk",
+                                         "verify_pair_lq4", "verify_pair_lg2", "verify_pair_single"))
         assert set(d_gst.cpu().tolist()) == {0} and set(d_vst.cpu().tolist()) == {0}, "aggregate mismatch"
         # the 96-byte aggregates themselves (herumi.go:244-283 returns exactly these bytes, sigagg.go:149-154 injects
         # them): each equals Sign(secret) made by the separate sign kernel
@@ -528,10 +528,6 @@ def main():
             a, c = kernel_stats(lib, name)
             return round(fpmul * MADS_PER_FPMUL / (a * 1e-3) / 1e12 / MAD_PEAK_T, 4) if c else None
 
-        def kfrac2(names, fpmul):  # work of both kernels over the sum of their average launch times
-            t = sum(kernel_stats(lib, k)[0] for k in names)
-            return round(fpmul * MADS_PER_FPMUL / (t * 1e-3) / 1e12 / MAD_PEAK_T, 4) if t > 0 else None
-
         tagg_roofline = {
             "algorithmic_unit": "%d Fp-mul-equivalents x %d MADs per aggregate (7 partials + Verify)" % (unit,
                                                                                                      MADS_PER_FPMUL),
@@ -540,10 +536,7 @@ def main():
             "stage_frac": {"tagg_scale": kfrac("tagg_scale", TAGG_FPMUL["scale_7"] * G),
                            "tv_prep_pk": kfrac("tv_prep_pk", TAGG_FPMUL["key_prep"] * G),
                            "tagg_unscale": kfrac("tagg_unscale", TAGG_FPMUL["unscale"] * G),
-                           # the pairing check's two halves (key-side loop early, then the aggregate's loop + final
-                           # exponentiation): the unit split as the host count's Miller loops and exponentiation
-                           "tv_pk_loop+tv_check_lq4": kfrac2(("tv_pk_loop", "tv_check_lq4"),
-                                                             TAGG_FPMUL["pairing"] * G)}}
+                           "verify_pair_lq4": kfrac("verify_pair_lq4", TAGG_FPMUL["pairing"] * G)}}
 
     # ---- C4: RLC BatchVerify of the 1M-partial node batch, validator-index slices over the ranks (strong scaling:
     # the node batch is fixed); node bitmap all-gathered inside the timed step

@@ -141,7 +141,6 @@ struct Context {
   DevBuf r_pk, r_sig, r_h, r_win, r_midx, r_list, r_cnt, r_slot, r_mlist;  // RLC BatchVerify workspaces
   DevBuf t_code, t_tab, b_kidx;                                            // resident pubshare table + key indices
   DevBuf v_ws;                                                             // lane-pair Verify points (SoA)
-  DevBuf v_hpk;                                                            // sigagg: key-side Miller values (split)
   uint64_t t_size = 0;
   // pubshare bytes -> table index (host side), for the submission queue's keyed path
   std::unordered_map<std::string, uint32_t> t_index;
@@ -951,30 +950,16 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
                          d_moffs, n_groups, d_ids, d_goffs, ws, d_vstatus);
   });
   if (rc) return rc;
-  // Quads: the key side's Miller loop e([L] pk, H(m)) needs nothing from the aggregation, so it runs here, beside the
-  // partials' scaling (whose second round of waves leaves most SIMDs free), and the check after the join only runs
-  // e(-g1, S)'s loop and the final exponentiation (k_tv_check_lq4).
-  const bool quads = use_quads(n_groups);
-  uint32_t* hpk = nullptr;
-  if (quads) {
-    HIP_TRY(c.v_hpk.ensure(n_groups * 144 * 4));
-    hpk = (uint32_t*)c.v_hpk.p;
-    rc = timed(c, "tv_pk_loop", s1, [&] {
-      hipLaunchKernelGGL(k_tv_pk_loop, dim3((unsigned)grid_for(2 * n_groups)), dim3(kBlock), 0, s1,
-                         (const uint32_t*)ws, n_groups, (const int32_t*)d_vstatus, hpk);
-    });
-    if (rc) return rc;
-  }
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));
   HIP_TRY(hipStreamWaitEvent(s, c.ev_join[0], 0));
   HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
   hipLaunchKernelGGL(k_tv_join, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s, n_groups,
                      (const int32_t*)d_astatus, (const int32_t*)agg_inf, d_vstatus);
   HIP_TRY(hipGetLastError());
-  if (quads)
-    rc = timed(c, "tv_check_lq4", s, [&] {
-      hipLaunchKernelGGL(k_tv_check_lq4, dim3((unsigned)grid_for(4 * n_groups)), dim3(kBlock), 0, s,
-                         (const uint32_t*)ws, (const uint32_t*)hpk, n_groups, d_vstatus);
+  if (use_quads(n_groups))
+    rc = timed(c, "verify_pair_lq4", s, [&] {
+      hipLaunchKernelGGL(k_verify_pair_lq4, dim3((unsigned)grid_for(4 * n_groups)), dim3(kBlock), 0, s,
+                         (const uint32_t*)ws, n_groups, d_vstatus);
     });
   else if (use_pairs(n_groups, kLg2MaxVerify))
     rc = timed(c, "verify_pair_lg2", s, [&] {

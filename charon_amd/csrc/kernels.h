@@ -414,44 +414,6 @@ __global__ void __launch_bounds__(kBlock) k_tv_prep_pk2(const uint8_t* __restric
   vstatus[i] = st;
 }
 
-// sigagg's key-side Miller loop ahead of the aggregate (lane pair per group, beside k_tagg_scale): e([L] pk, H(m))
-// split over the pair (lg2.h miller_loop_split), the split value to hpk (144 words per group: column 2i + parity of a
-// 72-word SoA).  Only groups the key prep left pending; k_tv_check_lq4 reads it on the quad's first pair.
-__global__ void __launch_bounds__(kBlock) k_tv_pk_loop(const uint32_t* __restrict__ ws, uint64_t n,
-                                                       const int32_t* __restrict__ vstatus, uint32_t* __restrict__ hpk) {
-  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  const uint64_t i = t >> 1;
-  if (i >= n || vstatus[i] != RLC_PENDING) return;  // the same on both lanes of the pair
-  const uint32_t m = (t & 1) ? ~0u : 0u;
-  g1a pk;
-  g2a hm;
-  soa_load<24>(&pk.x.v[0], ws, n, i);
-  soa_load<48>(&hm.x.c0.v[0], ws + 24 * n, n, i);
-  fp6 h;
-  miller_loop_split(h, pk, hm, m);
-  soa_store<72>(hpk, 2 * n, t, &h.c0.c0.v[0]);
-}
-
-// The rest of the check on a lane quad per group (lg2.h lq4_verify_pre): the second pair runs e(-g1, S)'s loop, the
-// first takes k_tv_pk_loop's value, then the quad's final exponentiation.  Same statuses as k_verify_pair_lq4.
-__global__ void __launch_bounds__(kBlock) k_tv_check_lq4(const uint32_t* __restrict__ ws,
-                                                         const uint32_t* __restrict__ hpk, uint64_t n,
-                                                         int32_t* __restrict__ status) {
-  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  const uint64_t i = t >> 2;
-  const int q = (int)(t & 3);
-  if (i >= n || status[i] != RLC_PENDING) return;  // the same on all four lanes of the quad
-  g2a sig;
-  soa_load<48>(&sig.x.c0.v[0], ws + 72 * n, n, i);
-  fp6 h;
-  if (q < 2)
-    soa_load<72>(&h.c0.c0.v[0], hpk, 2 * n, 2 * i + (uint64_t)q);
-  else
-    fp6_set_zero(h);
-  const int st = lq4_verify_pre(h, sig, q);
-  if (q == 0) status[i] = st;
-}
-
 // Join: a group whose aggregation failed reports that status for its Verify too; otherwise the key's status
 // stands (Verify checks the key first), and an aggregate at infinity is "signature not verified".
 __global__ void __launch_bounds__(kBlock) k_tv_join(uint64_t n, const int32_t* __restrict__ astatus,

@@ -775,40 +775,6 @@ __device__ int lq4_verify(const g1a& pk, const g2a& hm, const g2a& sig, int q) {
   return !sig_in_g2 ? HIPBLS_ERR_SIGNATURE : (ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY);
 }
 
-// lq4_verify with the first pair's Miller loop already run (sigagg's key side, k_tv_pk_loop: e([L] pk, H(m)) does not
-// wait for the aggregate, so it runs beside the partials' scaling).  h_pk is that loop's split value on lanes 0, 1
-// (ignored on lanes 2, 3); lanes 2, 3 run e(-g1, sig)'s loop, then the quad combines and exponentiates exactly as
-// lq4_verify: the same statuses on every input.
-__device__ int lq4_verify_pre(const fp6& h_pk, const g2a& sig, int q) {
-  const uint32_t m = (q & 1) ? ~0u : 0u;
-  const bool second = q >= 2;
-  fp6 h = h_pk;
-  uint32_t mine = 0;
-  if (second) {  // pair-uniform: both lanes of the second pair take it
-    g1a P;
-    P.x = G1_GEN_X;
-    P.y = G1_NEG_GEN_Y;
-    g2j T;
-    miller_loop_split(h, P, sig, m, &T);
-    mine = g2_subgroup_from_miller(T, sig) ? 1u : 0u;
-  }
-  const uint32_t other = quad_swap(mine);
-  const uint32_t sig_in_g2 = second ? mine : other;
-  fp12 fm, fo, f0, f1, r, e;
-  fp12h_gather(fm, h, m);
-  quad_swap(fo.c0, fm.c0);
-  quad_swap(fo.c1, fm.c1);
-  const quad_m qm(q);
-  f0.c0 = sel(qm.hi, fo.c0, fm.c0);
-  f0.c1 = sel(qm.hi, fo.c1, fm.c1);
-  f1.c0 = sel(qm.hi, fm.c0, fo.c0);
-  f1.c1 = sel(qm.hi, fm.c1, fo.c1);
-  fp12q_mul(r, f0, f1, qm);
-  final_exponentiation_quad(e, r, qm);
-  const bool ok = fp12_is_one(e);
-  return !sig_in_g2 ? HIPBLS_ERR_SIGNATURE : (ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY);
-}
-
 template <int MAXN>
 __device__ bool lg2_check_pairs(const g1a* P, const g2a* Q, int k, uint32_t m) {
   fp12 f;
