@@ -815,14 +815,13 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_msm, 0));
   HIP_TRY(hipStreamWaitEvent(s1, c.ev_hash, 0));
   rc = timed(c, "rlcb_chunks", s1, [&] {
-    hipLaunchKernelGGL(k_rlcb_chunks, dim3((unsigned)grid_for(nch + 1)), dim3(kBlock), 0, s1, n,
-                       (const int32_t*)d_status, d_midx, (const uint32_t*)rpk, (const uint32_t*)d_H, hstride, d_hslot,
-                       (uint32_t*)c.m_F.p, nch, (const uint32_t*)c.m_W.p);
+    hipLaunchKernelGGL(k_rlcb_chunks, dim3((unsigned)grid_for(nch)), dim3(kBlock), 0, s1, n, (const int32_t*)d_status,
+                       d_midx, (const uint32_t*)rpk, (const uint32_t*)d_H, hstride, d_hslot, (uint32_t*)c.m_F.p, nch);
   });
   if (rc) return rc;
   uint32_t* src = (uint32_t*)c.m_F.p;
   uint32_t* dst = (uint32_t*)c.m_F2.p;
-  uint64_t cur = nch + 1;
+  uint64_t cur = nch;
   rc = timed(c, "rlcb_product", s1, [&] {
     while (cur > 1) {
       const uint64_t nxt = (cur + RLCB_FAN - 1) / RLCB_FAN;
@@ -838,7 +837,7 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));
   HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
   rc = timed(c, "rlcb_final", s, [&] {
-    hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, flag);
+    hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, (const uint32_t*)c.m_W.p, flag);
   });
   if (rc) return rc;
   rc = timed(c, "rlcb_mark", s, [&] {

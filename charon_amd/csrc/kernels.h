@@ -951,22 +951,19 @@ __global__ void __launch_bounds__(kSumBlock) k_msm_window(const uint32_t* __rest
     for (int k = 0; k < 72; ++k) W[72 * w + k] = (&acc.x.c0.v[0])[k];
 }
 
-// Stage 3: lanes [0, n_chunks) are the chunks; lane n_chunks (the last workgroup's first free lane) forms S from the
-// MSM window sums and stores the Miller value of (-g1, S) as column n_chunks, so the product tree multiplies it in
-// and the verdict kernel only exponentiates.  F has n_chunks + 1 columns.  Launched after the MSM, so the MSM's
-// small kernels never wait for SIMDs this kernel holds (profiles/r02_kernel_stats.csv: k_msm_scan 33 ms).
+// Stage 3: one lane per chunk, n_chunks lanes exactly.  The (-g1, S) Miller value is NOT an extra lane here: at the
+// bench's 1M items n_chunks = 65,536 is exactly one wave per SIMD (four 36-KiB-LDS workgroups per CU), and one lane
+// more was a 1,025th workgroup -- a second round of waves, doubling the kernel (profiles/r04: 41 ms for ~21 ms of
+// chunk work).  k_rlcb_final computes it, split over its lane pair.
 __global__ void __launch_bounds__(kBlock) k_rlcb_chunks(uint64_t n, const int32_t* __restrict__ status,
                                                         const uint32_t* __restrict__ msg_idx,
                                                         const uint32_t* __restrict__ rpk,
                                                         const uint32_t* __restrict__ H, uint64_t hstride,
                                                         const uint32_t* __restrict__ hslot, uint32_t* __restrict__ F,
-                                                        uint64_t n_chunks, const uint32_t* __restrict__ W) {
+                                                        uint64_t n_chunks) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   BLS_LANE_F12(Lf);
-  if (c < n_chunks)
-    rlcb_chunk_lane(Lf, c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks + 1);
-  else if (c == n_chunks)
-    rlcb_sfactor_lane(Lf, W, F, n_chunks + 1, n_chunks);
+  if (c < n_chunks) rlcb_chunk_lane(Lf, c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks);
 }
 
 __global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict__ Fin, uint64_t nin,
@@ -975,17 +972,35 @@ __global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict
   if (g < nout) fp12_prod_lane(g, Fin, nin, Fout, nout, fan);
 }
 
-// The verdict, on lanes 0 and 1 as a pair (lg2.h): lane 1 holds the product of all Miller values (the chunks' and
-// (-g1, S)'s), lane 0 the identity; split final exponentiation; flag[0] = 1 when the product is 1.
-__global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restrict__ Ftot, int32_t* __restrict__ flag) {
+// The verdict, on lanes 0 and 1 as a pair (lg2.h): S = W0 + [2^16] W1 from the MSM's window sums (rlcb.h
+// msm_combine, on both lanes), the Miller value of (-g1, S) split over the pair (miller_loop_split: the same f as
+// rlcb_sfactor_lane's one-lane loop) and gathered; lane 0 keeps it, lane 1 takes the product of the chunks' Miller
+// values; lg2_finish multiplies the two and runs the split final exponentiation.  flag[0] = 1 when the product is 1.
+__global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restrict__ Ftot, const uint32_t* __restrict__ W,
+                                                       int32_t* __restrict__ flag) {
   const int t = threadIdx.x;
   if (t >= 2) return;
   const uint32_t m = t ? ~0u : 0u;
+  g2j W0, W1, S;
+  for (int k = 0; k < 72; ++k) {
+    (&W0.x.c0.v[0])[k] = W[k];
+    (&W1.x.c0.v[0])[k] = W[72 + k];
+  }
+  msm_combine(S, W0, W1);
   fp12 f;
-  if (t)
-    soa_load<144>(&f.c0.c0.c0.v[0], Ftot, 1, 0);
-  else
+  if (jac_is_inf(S)) {  // the same on both lanes
     fp12_set_one(f);
+  } else {
+    g1a P;
+    P.x = G1_GEN_X;
+    P.y = G1_NEG_GEN_Y;
+    g2a Q;
+    jac_to_aff(Q, S);
+    fp6 h;
+    miller_loop_split(h, P, Q, m);
+    fp12h_gather(f, h, m);
+  }
+  if (t) soa_load<144>(&f.c0.c0.c0.v[0], Ftot, 1, 0);
   const bool ok = lg2_finish(f, m);
   if (t == 0) flag[0] = ok ? 1 : 0;
 }

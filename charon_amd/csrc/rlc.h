@@ -55,6 +55,35 @@ BLS_HD BLS_INLINE void soa_load(uint32_t* dst, const uint32_t* base, uint64_t st
   for (int k = 0; k < WORDS; ++k) dst[k] = base[(uint64_t)k * stride + i];
 }
 
+// ---- AoS (point-major) storage: element i at base[WORDS * i ...], 16-byte aligned (WORDS % 4 == 0): for data a lane
+// gathers by index, one element is WORDS / 4 contiguous 16-byte loads instead of WORDS scattered cache lines --------
+template <int WORDS>
+BLS_HD BLS_INLINE void aos_store(uint32_t* base, uint64_t i, const uint32_t* src) {
+  static_assert(WORDS % 4 == 0, "16-byte groups");
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint4* d = (uint4*)__builtin_assume_aligned(base + (uint64_t)WORDS * i, 16);
+  for (int k = 0; k < WORDS / 4; ++k) d[k] = make_uint4(src[4 * k], src[4 * k + 1], src[4 * k + 2], src[4 * k + 3]);
+#else
+  for (int k = 0; k < WORDS; ++k) base[(uint64_t)WORDS * i + k] = src[k];
+#endif
+}
+template <int WORDS>
+BLS_HD BLS_INLINE void aos_load(uint32_t* dst, const uint32_t* base, uint64_t i) {
+  static_assert(WORDS % 4 == 0, "16-byte groups");
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4* s = (const uint4*)__builtin_assume_aligned(base + (uint64_t)WORDS * i, 16);
+  for (int k = 0; k < WORDS / 4; ++k) {
+    const uint4 v = s[k];
+    dst[4 * k] = v.x;
+    dst[4 * k + 1] = v.y;
+    dst[4 * k + 2] = v.z;
+    dst[4 * k + 3] = v.w;
+  }
+#else
+  for (int k = 0; k < WORDS; ++k) dst[k] = base[(uint64_t)WORDS * i + k];
+#endif
+}
+
 // [a] P + [b] Q with one shared doubling chain (Shamir's trick), 32-bit a, b
 template <class F>
 BLS_HD BLS_CALL void jac_mul2_u32(jac<F>& r, const jac<F>& P_in, const jac<F>& Q_in, uint32_t a, uint32_t b) {

@@ -52,7 +52,9 @@ BLS_HD BLS_INLINE uint32_t bls_serial_add_u32(uint32_t* p, uint32_t v) {  // hos
 #endif
 
 // ---- stage 1 ------------------------------------------------------------------------------------
-// pts: affine G2 SoA with 2n columns (sig_i at i, psi(sig_i) at n + i); sc: 2n scalars (a_i, then b_i).
+// pts: 2n affine G2 points, point-major (AoS, 48 contiguous words each: sig_i at i, psi(sig_i) at n + i), because
+// the bucket stage gathers them by index -- limb-major SoA made every gathered point 48 separate cache lines
+// (profiles/r04: k_msm_bucket moved 23 GB per launch for 0.8 GB of points); sc: 2n scalars (a_i, then b_i).
 BLS_HD BLS_INLINE void rlcb_items_lane(uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
                                        uint64_t n, uint64_t n_msgs, const rlc_seed& seed, uint32_t* rpk,
                                        uint32_t* pts, uint32_t* sc, int32_t* status,
@@ -97,8 +99,8 @@ BLS_HD BLS_INLINE void rlcb_items_lane(uint64_t i, const uint8_t* pks, const uin
     }
   }
   soa_store<36>(rpk, n, i, &rp.x.v[0]);
-  soa_store<48>(pts, 2 * n, i, &sig.x.c0.v[0]);
-  soa_store<48>(pts, 2 * n, n + i, &psig.x.c0.v[0]);
+  aos_store<48>(pts, i, &sig.x.c0.v[0]);
+  aos_store<48>(pts, n + i, &psig.x.c0.v[0]);
   sc[i] = a;
   sc[n + i] = b;
   status[i] = st;
@@ -138,10 +140,10 @@ BLS_HD BLS_INLINE void msm_bucket_lane(uint32_t w, uint32_t j, const uint32_t* o
   jac_set_inf(acc);
   const uint32_t k0 = off[w * (MSM_NB + 1) + j], k1 = off[w * (MSM_NB + 1) + j + 1];
   g2a q;
-  if (k0 < k1) soa_load<48>(&q.x.c0.v[0], pts, npts, list[(uint64_t)w * npts + k0]);
+  if (k0 < k1) aos_load<48>(&q.x.c0.v[0], pts, list[(uint64_t)w * npts + k0]);
   for (uint32_t k = k0; k < k1; ++k) {
     const g2a cur = q;
-    if (k + 1 < k1) soa_load<48>(&q.x.c0.v[0], pts, npts, list[(uint64_t)w * npts + k + 1]);
+    if (k + 1 < k1) aos_load<48>(&q.x.c0.v[0], pts, list[(uint64_t)w * npts + k + 1]);
     g2j x = acc, y;
     jac_add_aff(y, x, cur);
     acc = y;
@@ -286,8 +288,8 @@ BLS_HD BLS_INLINE void rlcb_mark_lane(uint64_t i, uint64_t n, bool pass, int32_t
     return;
   }
   g2a s, ps;
-  soa_load<48>(&s.x.c0.v[0], pts, 2 * n, i);
-  soa_load<48>(&ps.x.c0.v[0], pts, 2 * n, n + i);
+  aos_load<48>(&s.x.c0.v[0], pts, i);
+  aos_load<48>(&ps.x.c0.v[0], pts, n + i);
   g2j sj, psj, rs;
   jac_from_aff(sj, s);
   jac_from_aff(psj, ps);

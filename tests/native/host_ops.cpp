@@ -464,7 +464,7 @@ extern "C" int ht_verify_key(const uint8_t* pk48, const uint8_t* msg, uint32_t l
 #include "../../charon_amd/csrc/rlcb.h"
 
 namespace {
-// Pippenger over npts affine SoA points with 32-bit scalars: the device stages run serially; W = the window sums.
+// Pippenger over npts affine AoS points (rlcb.h layout) with 32-bit scalars: the device stages run serially; W = the window sums.
 void host_msm(g2j* W, const uint32_t* pts, const uint32_t* sc, uint64_t npts) {
   std::vector<uint32_t> cnt(MSM_WINDOWS * MSM_NB, 0), off(MSM_WINDOWS * (MSM_NB + 1)), cur(MSM_WINDOWS * MSM_NB);
   std::vector<uint32_t> list(MSM_WINDOWS * (npts ? npts : 1));
@@ -504,7 +504,7 @@ extern "C" void ht_msm_g2(const uint8_t* pts192, const uint32_t* sc, uint64_t n,
     fp_in(a.x.c1, pts192 + 192 * i + 48);
     fp_in(a.y.c0, pts192 + 192 * i + 96);
     fp_in(a.y.c1, pts192 + 192 * i + 144);
-    soa_store<48>(pts.data(), n, i, &a.x.c0.v[0]);
+    aos_store<48>(pts.data(), i, &a.x.c0.v[0]);
   }
   g2j W[MSM_WINDOWS], S;
   host_msm(W, pts.data(), sc, n);
