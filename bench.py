@@ -40,8 +40,9 @@ MADS_PER_FPMUL = 300
 RLC_FPMUL = {"item": 5802, "hash": 4790, "window_2msg": 21906, "window_1msg": 17485, "fallback": 18394}
 # Batch-wide check (charon_amd/csrc/rlcb.h), same unit and source: stage 1 per item, the Pippenger MSM per item
 # (2 points x 2 windows of mixed additions; the bucket/segment folds add ~15 per item at 1M items and are left
-# out), and one multi-Miller loop per 16-item chunk with 4 message runs (one root per 4-partial validator).
-RLCB_FPMUL = {"item": 4306, "msm_per_item": 116, "chunk_4runs": 18948}
+# out), and one multi-Miller loop per 16-item chunk with 4 message runs (one root per 4-partial validator) or with one
+# run (committee roots, C4(ii)).
+RLCB_FPMUL = {"item": 4306, "msm_per_item": 116, "chunk_4runs": 18948, "chunk_1run": 6909}
 # sigagg in one call (C3), per aggregate of 7 partials, same unit and source (tests/native/host_ops.cpp
 # ht_count_tagg_verify, tests/test_work_counts.py): the 7 partials' decode + subgroup test + c_k sig_k (k_tagg_scale),
 # the sum S (k_tagg_sum_s), [L^-1] S + compress (k_tagg_unscale), the root key's decode + subgroup test + [L] pk +
@@ -68,8 +69,9 @@ def parse():
                     help="C4 node batch in validators (x4 partials; 262,144 = 1M partials), sliced over the ranks "
                          "with shard_range (0 = skip)")
     ap.add_argument("--rlc-steps", type=int, default=3)
-    ap.add_argument("--rlc-variants", default="i,ii,all_valid",
-                    help="C4 variants to time: i (one root per validator), ii (committee roots), all_valid")
+    ap.add_argument("--rlc-variants", default="i,ii,all_valid,ii_all_valid",
+                    help="C4 variants to time: i (one root per validator), ii (committee roots), all_valid (i, no "
+                         "invalid partial), ii_all_valid (ii, no invalid partial)")
     ap.add_argument("--c5", type=int, default=1, help="time the C5 full-slot mix (0 = skip)")
     ap.add_argument("--keys", type=int, default=1, help="also time C2 / C4 with the resident pubshare table (0 = skip)")
     ap.add_argument("--latency-calls", type=int, default=200,
@@ -549,8 +551,10 @@ def main():
         chosen = set(args.rlc_variants.split(","))
         for variant, tag, n_roots, corrupt in (("i_root_per_validator", "c4i", 0, True),
                                                ("ii_committee_roots", "c4ii", max(1, V // 128), True),
-                                               ("i_all_valid", "c4h", 0, False)):
-            if {"i_root_per_validator": "i", "ii_committee_roots": "ii", "i_all_valid": "all_valid"}[variant] not in chosen:
+                                               ("i_all_valid", "c4h", 0, False),
+                                               ("ii_all_valid", "c4hii", max(1, V // 128), False)):
+            if {"i_root_per_validator": "i", "ii_committee_roots": "ii", "i_all_valid": "all_valid",
+                "ii_all_valid": "ii_all_valid"}[variant] not in chosen:
                 continue
             # the mode HIPBLS_RLC_AUTO settles on for each stream: windows while invalid partials keep arriving
             # (its batch-wide check keeps failing), the batch-wide check for an all-valid stream
@@ -597,7 +601,7 @@ def main():
                      + RLC_FPMUL["fallback"] * fb.value)
             if b_pass1 > b_pass0:  # the batch-wide check decided alone: no window pairing work
                 fpmul = ((RLCB_FPMUL["item"] + RLCB_FPMUL["msm_per_item"]) * n4 + RLC_FPMUL["hash"] * len(roots4)
-                         + RLCB_FPMUL["chunk_4runs"] * ((n4 + 15) // 16))
+                         + RLCB_FPMUL["chunk_1run" if n_roots else "chunk_4runs"] * ((n4 + 15) // 16))
             ach = fpmul * MADS_PER_FPMUL * args.rlc_steps / tel / 1e12
             rlc[variant] = {"verified_partial_sigs_per_s": round(4 * V * args.rlc_steps / tel, 1),
                             "node_items": 4 * V, "items_this_gpu": n4, "distinct_roots_this_gpu": len(roots4),
@@ -610,7 +614,7 @@ def main():
                             "batch_checks": {"attempted": b_att1 - b_att0, "passed": b_pass1 - b_pass0},
                             "kernel_avg_ms": kernel_ms(lib, ("rlc_items", "rlc_hash", "rlc_window", "rlc_window_lg2",
                                                              "rlc_fallback", "rlc_fallback_lg2", "rlcb_items",
-                                                             "rlcb_msm", "rlcb_chunks", "rlcb_product", "rlcb_final",
+                                                             "rlcb_msm", "rlcb_chunks", "rlcb_sfactor", "rlcb_product", "rlcb_final",
                                                              "rlcb_mark")),
                             "stage_frac": stage_fracs(lib, {
                                 "rlc_items": RLC_FPMUL["item"] * n4, "rlc_hash": RLC_FPMUL["hash"] * len(roots4),
@@ -620,7 +624,8 @@ def main():
                                 "rlc_fallback": RLC_FPMUL["fallback"] * fb.value,
                                 "rlc_fallback_lg2": RLC_FPMUL["fallback"] * fb.value,
                                 "rlcb_items": RLCB_FPMUL["item"] * n4,
-                                "rlcb_chunks": RLCB_FPMUL["chunk_4runs"] * ((n4 + 15) // 16)}, args.rlc_steps)}
+                                "rlcb_chunks": RLCB_FPMUL["chunk_1run" if n_roots else "chunk_4runs"]
+                                * ((n4 + 15) // 16)}, args.rlc_steps)}
             if corrupt and variant == "i_root_per_validator":
                 # the library's default policy (HIPBLS_RLC_AUTO) on the same stream: one failing batch-wide check,
                 # then windows while it backs off (rlc_mode comment above)

@@ -161,7 +161,9 @@ struct Context {
   uint64_t r_windows = 0;        // window count of this context's last RLC call (hipbls_rlc_stats)
   uint64_t r_call = 0;           // entry-point call that call belonged to
   // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
-  DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_flag;
+  DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_flag, m_Fs;
+  hipEvent_t rlcb_ev_sf = nullptr;  // the (-g1, S) Miller value is in m_Fs
+  uint64_t slots = 0;               // waves in flight at one wave per SIMD: 4 x compute units (wave_slots)
   // Verdicts come back through a ring of pinned slots, one per batch check in flight, so a launch only waits
   // on the host when kRlcbSlots checks are still unread (never in the enqueue-only *_device paths otherwise).
   static constexpr int kRlcbSlots = 8;
@@ -423,6 +425,17 @@ const uint64_t* rebase(const uint64_t* offs, uint64_t lo, uint64_t hi, std::vect
 }
 
 uint64_t grid_for(uint64_t n) { return (n + kBlock - 1) / kBlock; }
+
+// Waves the device runs at once at one wave per SIMD (4 SIMDs per compute unit): a kernel of exactly a multiple of this
+// many waves leaves nothing free for a kernel beside it (rlcb.h rlcb_chunk_count).
+uint64_t wave_slots(Context& c) {
+  if (!c.slots) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess || cus <= 0) cus = 256;
+    c.slots = 4 * (uint64_t)cus;
+  }
+  return c.slots;
+}
 // Verify batches up to this size hash each message on a lane pair in the prep stage (k_verify_prep pair_hash).
 constexpr uint64_t kPairHashMaxVerify = 16384;
 
@@ -738,13 +751,14 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   const int32_t* tcode = (const int32_t*)c.t_code.p;
   const uint32_t* tab = (const uint32_t*)c.t_tab.p;
   const uint64_t npts = 2 * n;
-  const uint64_t nch = (n + RLCB_C - 1) / RLCB_C;
+  const uint64_t nch = rlcb_chunk_count(n, wave_slots(c));
   const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
   if (!c.rlcb_host_flag) {
     HIP_TRY(hipHostMalloc((void**)&c.rlcb_host_flag, Context::kRlcbSlots * sizeof(int32_t), hipHostMallocDefault));
     for (int k = 0; k < Context::kRlcbSlots; ++k) HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_items, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_msm, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_sf, hipEventDisableTiming));
   }
   int rc = ensure_rlc_streams(c);
   if (rc) return rc;
@@ -763,6 +777,7 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   HIP_TRY(c.m_F.ensure((nch + 1) * 144 * 4));
   HIP_TRY(c.m_F2.ensure(((nch + RLCB_FAN) / RLCB_FAN) * 144 * 4));
   HIP_TRY(c.m_flag.ensure(4));
+  HIP_TRY(c.m_Fs.ensure(144 * 4));
   uint32_t* rpk = (uint32_t*)c.r_pk.p;
   uint32_t* rsig = (uint32_t*)c.r_sig.p;
   uint32_t* pts = (uint32_t*)c.m_pts.p;
@@ -812,6 +827,12 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.rlcb_ev_msm, s0));
+  // (-g1, S) on a lane pair beside the chunks, on the SIMD rlcb_chunk_count leaves free
+  rc = timed(c, "rlcb_sfactor", s0, [&] {
+    hipLaunchKernelGGL(k_rlcb_sfactor, dim3(1), dim3(kBlock), 0, s0, (const uint32_t*)c.m_W.p, (uint32_t*)c.m_Fs.p);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c.rlcb_ev_sf, s0));
   HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_msm, 0));
   HIP_TRY(hipStreamWaitEvent(s1, c.ev_hash, 0));
   rc = timed(c, "rlcb_chunks", s1, [&] {
@@ -836,8 +857,9 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));
   HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
+  HIP_TRY(hipStreamWaitEvent(s, c.rlcb_ev_sf, 0));
   rc = timed(c, "rlcb_final", s, [&] {
-    hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, (const uint32_t*)c.m_W.p, flag);
+    hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, (const uint32_t*)c.m_Fs.p, flag);
   });
   if (rc) return rc;
   rc = timed(c, "rlcb_mark", s, [&] {

@@ -951,10 +951,10 @@ __global__ void __launch_bounds__(kSumBlock) k_msm_window(const uint32_t* __rest
     for (int k = 0; k < 72; ++k) W[72 * w + k] = (&acc.x.c0.v[0])[k];
 }
 
-// Stage 3: one lane per chunk, n_chunks lanes exactly.  The (-g1, S) Miller value is NOT an extra lane here: at the
-// bench's 1M items n_chunks = 65,536 is exactly one wave per SIMD (four 36-KiB-LDS workgroups per CU), and one lane
-// more was a 1,025th workgroup -- a second round of waves, doubling the kernel (profiles/r04: 41 ms for ~21 ms of
-// chunk work).  k_rlcb_final computes it, split over its lane pair.
+// Stage 3: one lane per chunk, n_chunks lanes exactly (rlcb.h rlcb_chunk_count).  The (-g1, S) Miller value is NOT an
+// extra lane here: at the bench's 1M items 65,536 chunks were exactly one wave per SIMD (four 36-KiB-LDS workgroups
+// per CU) and one lane more made a 1,025th workgroup -- a second round of waves (profiles/r04: 41 ms for 28 ms of
+// chunk work).  k_rlcb_sfactor computes it on the SIMD rlcb_chunk_count leaves free.
 __global__ void __launch_bounds__(kBlock) k_rlcb_chunks(uint64_t n, const int32_t* __restrict__ status,
                                                         const uint32_t* __restrict__ msg_idx,
                                                         const uint32_t* __restrict__ rpk,
@@ -963,7 +963,7 @@ __global__ void __launch_bounds__(kBlock) k_rlcb_chunks(uint64_t n, const int32_
                                                         uint64_t n_chunks) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   BLS_LANE_F12(Lf);
-  if (c < n_chunks) rlcb_chunk_lane(Lf, c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks);
+  if (c < n_chunks) rlcb_chunk_lane(Lf, c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks, n_chunks);
 }
 
 __global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict__ Fin, uint64_t nin,
@@ -972,12 +972,10 @@ __global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict
   if (g < nout) fp12_prod_lane(g, Fin, nin, Fout, nout, fan);
 }
 
-// The verdict, on lanes 0 and 1 as a pair (lg2.h): S = W0 + [2^16] W1 from the MSM's window sums (rlcb.h
-// msm_combine, on both lanes), the Miller value of (-g1, S) split over the pair (miller_loop_split: the same f as
-// rlcb_sfactor_lane's one-lane loop) and gathered; lane 0 keeps it, lane 1 takes the product of the chunks' Miller
-// values; lg2_finish multiplies the two and runs the split final exponentiation.  flag[0] = 1 when the product is 1.
-__global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restrict__ Ftot, const uint32_t* __restrict__ W,
-                                                       int32_t* __restrict__ flag) {
+// The Miller value of (-g1, S), S = W0 + [2^16] W1 from the MSM's window sums (rlcb.h msm_combine): lanes 0, 1 as a
+// pair (lg2.h miller_loop_split, the same f as rlcb_sfactor_lane's one-lane loop), gathered, 144 words to Fs.  One
+// wave, beside the chunk kernel.
+__global__ void __launch_bounds__(kBlock) k_rlcb_sfactor(const uint32_t* __restrict__ W, uint32_t* __restrict__ Fs) {
   const int t = threadIdx.x;
   if (t >= 2) return;
   const uint32_t m = t ? ~0u : 0u;
@@ -1000,8 +998,25 @@ __global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restric
     miller_loop_split(h, P, Q, m);
     fp12h_gather(f, h, m);
   }
-  if (t) soa_load<144>(&f.c0.c0.c0.v[0], Ftot, 1, 0);
-  const bool ok = lg2_finish(f, m);
+  if (t == 0)
+    for (int k = 0; k < 144; ++k) Fs[k] = (&f.c0.c0.c0.v[0])[k];
+}
+
+// The verdict on a lane quad (lg2.h): the chunks' product (Ftot, one column) times the (-g1, S) value (Fs), one
+// Fp6 product per lane, then the quad's final exponentiation; flag[0] = 1 when the result is 1.
+__global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restrict__ Ftot, const uint32_t* __restrict__ Fs,
+                                                       int32_t* __restrict__ flag) {
+  const int t = threadIdx.x;
+  if (t >= 4) return;
+  fp12 a, b, r, e;
+  for (int k = 0; k < 144; ++k) {
+    (&a.c0.c0.c0.v[0])[k] = Fs[k];
+    (&b.c0.c0.c0.v[0])[k] = Ftot[k];
+  }
+  const quad_m qm(t);
+  fp12q_mul(r, a, b, qm);
+  final_exponentiation_quad(e, r, qm);
+  const bool ok = fp12_is_one(e);
   if (t == 0) flag[0] = ok ? 1 : 0;
 }
 

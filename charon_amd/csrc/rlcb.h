@@ -30,7 +30,8 @@
 
 namespace bls {
 
-constexpr int RLCB_C = 16;                     // items per Miller chunk
+constexpr int RLCB_C = 16;                     // items per Miller chunk (target)
+constexpr int RLCB_CMAX = 18;                  // most items a chunk lane may get (rlcb_chunk_count)
 constexpr int MSM_BITS = 16;                   // Pippenger window width
 constexpr int MSM_WINDOWS = 2;                 // 32-bit scalars
 constexpr uint32_t MSM_NB = 1u << MSM_BITS;    // buckets per window (bucket 0 unused)
@@ -193,18 +194,31 @@ BLS_HD BLS_INLINE void msm_combine(g2j& S, const g2j& W0, const g2j& W1) {
 }
 
 // ---- stage 3: per-chunk multi-Miller loop ----------------------------------------------------------
-// F: Fp12 SoA, 144 words x n_chunks.  Chunks without pending items store 1.
+// How many chunks for n items: ceil(n / RLCB_C), unless that fills whole rounds of waves exactly (`slots` = the waves
+// the device runs at once at one wave per SIMD): then one wave fewer, items spread over the lanes (16 or 17 each), so
+// a SIMD stays free for the (-g1, S) Miller value beside the chunks (k_rlcb_sfactor).  At the bench's 1M items:
+// 65,536 chunks = 1,024 waves = every SIMD, so 65,472.
+BLS_HD BLS_INLINE uint64_t rlcb_chunk_count(uint64_t n, uint64_t slots) {
+  const uint64_t nch = (n + RLCB_C - 1) / RLCB_C;
+  const uint64_t waves = (nch + 63) / 64;
+  if (slots == 0 || waves <= 1 || waves < slots || waves % slots != 0) return nch;
+  const uint64_t fewer = (waves - 1) * 64;
+  return (n + fewer - 1) / fewer <= (uint64_t)RLCB_CMAX ? fewer : nch;
+}
+
+// F: Fp12 SoA, 144 words x n_chunks.  Chunk c covers items [c n / n_chunks, (c + 1) n / n_chunks) (at most RLCB_CMAX).
+// Chunks without pending items store 1.
 template <int S>
 BLS_HD BLS_INLINE void rlcb_chunk_lane(const f12l<S>& Lf, uint64_t c, uint64_t n, const int32_t* status, const uint32_t* msg_idx,
                                        const uint32_t* rpk, const uint32_t* H, uint64_t hstride,
-                                       const uint32_t* hslot, uint32_t* F, uint64_t n_chunks) {
-  g1a P[RLCB_C];
-  g2a Q[RLCB_C];
+                                       const uint32_t* hslot, uint32_t* F, uint64_t n_chunks, uint64_t fstride) {
+  g1a P[RLCB_CMAX];
+  g2a Q[RLCB_CMAX];
   int np = 0;
   g1j run;
   jac_set_inf(run);
   uint32_t run_msg = 0xffffffffu;
-  const uint64_t i0 = c * RLCB_C, i1 = i0 + RLCB_C < n ? i0 + RLCB_C : n;
+  const uint64_t i0 = c * n / n_chunks, i1 = (c + 1) * n / n_chunks;
   for (uint64_t i = i0; i < i1; ++i) {
     if (status[i] != RLC_PENDING) continue;
     g1j qp;
@@ -231,10 +245,10 @@ BLS_HD BLS_INLINE void rlcb_chunk_lane(const f12l<S>& Lf, uint64_t c, uint64_t n
   }
   fp12 f;
   if (np)
-    miller_loop_multi_l<RLCB_C>(f, Lf, P, Q, np);
+    miller_loop_multi_l<RLCB_CMAX>(f, Lf, P, Q, np);
   else
     fp12_set_one(f);
-  soa_store<144>(F, n_chunks, c, &f.c0.c0.c0.v[0]);
+  soa_store<144>(F, fstride, c, &f.c0.c0.c0.v[0]);
 }
 
 // The S lane of stage 3: S = W0 + [2^16] W1 from the window sums (W: 2 x 72 words, contiguous), then the Miller

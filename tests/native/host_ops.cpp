@@ -5,6 +5,8 @@
 #define BLS_COUNT_OPS 1
 #include "../../charon_amd/csrc/ops.h"
 
+static uint64_t g_rlcb_slots = 0;   // device wave slots rlcb_chunk_count plans for (ht_rlcb_set_slots)
+static uint64_t g_rlcb_chunks = 0;  // test override of the chunk count (0: rlcb_chunk_count)
 namespace bls {
 thread_local uint64_t g_fp_mul_count = 0;
 thread_local uint64_t g_fp_sqr_count = 0;
@@ -359,6 +361,7 @@ int ht_count_tagg_verify(const uint8_t* sigs, const int64_t* ids, int t, const u
   return st;
 }
 
+
 void ht_reset_counts(void) {
   g_fp_mul_count = 0;
   g_fp_sqr_count = 0;
@@ -543,10 +546,11 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
   }
   mark(2);
   // stage 3 as the device runs it: the chunks, then the (-g1, S) lane as the last column
-  const uint64_t nch = (n + RLCB_C - 1) / RLCB_C;
+  const uint64_t nch = g_rlcb_chunks ? g_rlcb_chunks : rlcb_chunk_count(n, g_rlcb_slots);
   std::vector<uint32_t> F(144 * (nch + 1));
   for (uint64_t c = 0; c < nch; ++c)
-    rlcb_chunk_lane(host_f12_slot(), c, n, status, msg_idx, rpk.data(), H.data(), n_msgs, nullptr, F.data(), nch + 1);
+    rlcb_chunk_lane(host_f12_slot(), c, n, status, msg_idx, rpk.data(), H.data(), n_msgs, nullptr, F.data(), nch,
+                    nch + 1);
   mark(3);  // the (-g1, S) lane is counted with the product and the verdict (stage 4 of counts6)
   rlcb_sfactor_lane(host_f12_slot(), Wc.data(), F.data(), nch + 1, nch);
   uint64_t cur = nch + 1;
@@ -592,3 +596,7 @@ extern "C" void ht_fp_inv(const uint32_t* x12, int gcd, uint32_t* out12) {
     fp_inv_pow(r, x);
   for (int i = 0; i < 12; ++i) out12[i] = r.v[i];
 }
+
+extern "C" void ht_rlcb_set_slots(uint64_t slots) { g_rlcb_slots = slots; }
+extern "C" void ht_rlcb_set_chunks(uint64_t nch) { g_rlcb_chunks = nch; }
+extern "C" uint64_t ht_rlcb_chunk_count(uint64_t n, uint64_t slots) { return rlcb_chunk_count(n, slots); }

@@ -100,12 +100,15 @@ def test_c4_full_node_batch_every_mode(impl, keys4, variant):
     _oracle_sample(pks, sigs, midx, roots, bad, results["windows"], 0xC4 + len(roots))
 
 
-def test_c4_all_valid_node_batch_decided_by_batch_check(impl, keys4):
-    """An all-valid 1M-partial node batch: the batch-wide Pippenger check alone passes it (no window pairing work);
-    WINDOWS gives the same all-zero bitmap."""
+@pytest.mark.parametrize("variant", ["i_root_per_validator", "ii_committee_roots"])
+def test_c4_all_valid_node_batch_decided_by_batch_check(impl, keys4, variant):
+    """An all-valid 1M-partial node batch, one root per validator (i) or 2,048 committee roots (ii): the batch-wide
+    Pippenger check alone passes it (no window pairing work); WINDOWS gives the same all-zero bitmap."""
     import bench
     from charon_amd.tbls import RLC_AUTO, RLC_BATCH, RLC_WINDOWS
-    pks, sigs, midx, roots, bad = bench.make_c4(impl, keys4, "c4h", 0, V, V, 0, corrupt=False)
+    tag, n_roots = ("c4h", 0) if variant.startswith("i_") else ("c4hii", V // 128)
+    pks, sigs, midx, roots, bad = bench.make_c4(impl, keys4, tag, 0, V, V, n_roots, corrupt=False)
+    assert len(roots) == (n_roots or V)
     assert not bad
     seed = os.urandom(32)
     try:

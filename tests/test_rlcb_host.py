@@ -94,3 +94,36 @@ def test_rlcb_fixture_statuses():
     pks, msgs, sigs, want = fixture_batch()
     got, _ = rlcb(L, pks, msgs, sigs)
     assert got == want
+
+
+def test_chunk_count_leaves_a_simd_free():
+    """rlcb.h rlcb_chunk_count: ceil(n / 16) chunks unless they fill whole rounds of waves exactly, then one wave
+    fewer (at most 18 items per lane); the bench's 1M items on 1,024 wave slots get 65,472 chunks."""
+    L = lib()
+    f = L.ht_rlcb_chunk_count
+    f.restype = ctypes.c_uint64
+    f.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+    assert f(1 << 20, 1024) == 65472            # 1,024 waves -> 1,023
+    assert f(1 << 20, 0) == 65536               # no device information: plain ceil(n / 16)
+    assert f((1 << 20) - 16, 1024) == 65472     # 65,535 chunks: still 1,024 waves, every SIMD -> one wave fewer
+    assert f(16 * 64 * 1000, 1024) == 64000     # 1,000 waves: a SIMD is free already
+    assert f(16 * 64 * 2048, 1024) == 64 * 2047  # two whole rounds -> one wave fewer
+    assert f(100, 1) == 7                       # one wave: never reduced
+    assert f(16 * 64 * 9, 9) == 16 * 64 * 9 // 18  # 9 waves -> 8, 18 items per lane (the cap)
+    assert f(16 * 64 * 8, 8) == 16 * 64 * 8 // 16  # 8 waves -> 7 would need > 18 per lane: kept
+
+
+def test_rlcb_uneven_chunks_same_verdicts():
+    """Chunks of 17 and 18 items (a chunk count that does not divide the batch, as rlcb_chunk_count makes on the
+    device) give the same verdicts: the honest batch passes, the cancellation case fails and falls back exactly."""
+    L = lib()
+    L.ht_rlcb_set_chunks(ctypes.c_uint64(4))
+    try:
+        pks, msgs, sigs, want = validator_batch(host_sign(L), host_pk(L), 14, 5, seed=24)  # 70 items
+        got, passed = rlcb(L, pks, msgs, sigs)
+        assert got == want == [0] * 70 and passed == 1
+        sigs[5], sigs[6] = sigs[6], sigs[5]  # same root, swapped: only the scalars catch it
+        got, passed = rlcb(L, pks, msgs, sigs)
+        assert passed == 0 and got == [0] * 5 + [3, 3] + [0] * 63
+    finally:
+        L.ht_rlcb_set_chunks(ctypes.c_uint64(0))

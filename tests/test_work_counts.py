@@ -81,6 +81,16 @@ def test_bench_rlcb_stage_counts_match():
     want = bench.RLCB_FPMUL
     assert abs(cnt[0] / n - want["item"]) / want["item"] < 0.02
     assert abs(cnt[3] / 4 - want["chunk_4runs"]) / want["chunk_4runs"] < 0.02
+    # committee roots: 16 items of one root per chunk, one run (C4(ii))
+    pks, msgs, sigs, _ = validator_batch(host_sign(L), host_pk(L), 4, 16, seed=6)
+    table, idx = message_table(msgs)
+    offs = (ctypes.c_uint64 * (len(table) + 1))(*[32 * i for i in range(len(table) + 1)])
+    arr = (ctypes.c_uint32 * len(pks))(*idx)
+    st = (ctypes.c_int32 * len(pks))()
+    L.ht_rlcb_verify(b"".join(pks), b"".join(sigs), arr, ctypes.c_uint64(len(pks)), b"".join(table), offs,
+                     ctypes.c_uint64(len(table)), bytes(32), st, ctypes.byref(passed), cnt)
+    assert passed.value == 1
+    assert abs(cnt[3] / 4 - want["chunk_1run"]) / want["chunk_1run"] < 0.02
 
 
 def test_bench_tagg_counts_match():
