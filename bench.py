@@ -614,7 +614,8 @@ def main():
                             "batch_checks": {"attempted": b_att1 - b_att0, "passed": b_pass1 - b_pass0},
                             "kernel_avg_ms": kernel_ms(lib, ("rlc_items", "rlc_hash", "rlc_window", "rlc_window_lg2",
                                                              "rlc_fallback", "rlc_fallback_lg2", "rlcb_items",
-                                                             "rlcb_msm", "rlcb_chunks", "rlcb_sfactor", "rlcb_product", "rlcb_final",
+                                                             "rlcb_msm", "rlcb_g1plan", "rlcb_g1sort", "rlcb_g1msm",
+                                                             "rlcb_g1miller", "rlcb_chunks", "rlcb_sfactor", "rlcb_product", "rlcb_final",
                                                              "rlcb_mark")),
                             "stage_frac": stage_fracs(lib, {
                                 "rlc_items": RLC_FPMUL["item"] * n4, "rlc_hash": RLC_FPMUL["hash"] * len(roots4),

@@ -1,0 +1,221 @@
+// The G1 half of the batch-wide RLC check's Pippenger MSM (BASELINE.json north star: "a Pippenger MSM over G1/G2"):
+// for every message with many items -- committee roots, where one signing root is shared by a whole committee's
+// partials (/root/reference/core/validatorapi/validatorapi.go:246-283, grouped by root in core/parsigdb/memory.go:
+// 198-225) -- one bucket-method sum
+//     R_m = sum_{i : msg i = m} [r_i] pk_i = sum_i [a_i] pk_i + [b_i] ([x] pk_i)          (r_i = a_i + b_i x, rlc.h)
+// replaces the per-item Shamir multiplication [r_i] pk_i of rlcb.h stage 1, and ONE Miller pair (R_m, H(m)) per such
+// message replaces its share of the chunk Miller loops.  The other messages keep the per-item path; the verdict and
+// every status are unchanged (the batch equation is the same group element either way).
+//
+// Layout (one "large" message L = its dense index among messages with >= min items):
+//   * slots: the large messages' items, message by message (soff[L] .. soff[L + 1]); slot s holds pk_s affine
+//     (24 words at gpts + 24 s) and [x] pk_s Jacobian as the subgroup check left it (36 words at gxp + 36 s, gxp =
+//     gpts + 24 n: no inversion per item), both point-major so the bucket lanes gather them by index, and the
+//     scalars (a_s, b_s); an item that did not decode keeps zero scalars and adds nothing;
+//   * buckets: per (L, kind, window w of 4 bits, digit d = 1..15), kind 0 = pk with a's digits (mixed additions),
+//     kind 1 = [x] pk with b's digits (full additions); each kind has 128 bucket indices of which 120 are used, so a
+//     wave of bucket lanes never mixes the two addition formulas (256 per large message);
+//   * counting sort of the slots by bucket (histogram, scan, scatter), one lane per bucket sums its entries, one lane
+//     per (L, w) folds sum_d d (B_{0,w,d} + B_{1,w,d}) with running sums, and one lane pair per L combines the
+//     windows (R = sum_w [16^w] W_w) and runs the split Miller loop of (R, H(m)) -> a column of the product tree
+//     (the value 1 for an empty R).
+#pragma once
+#include "rlc.h"
+// included by rlcb.h after BLS_ATOMIC_ADD_U32
+
+namespace bls {
+
+constexpr int G1M_BITS = 4;
+constexpr int G1M_WIN = 8;                              // 32-bit scalars in 4-bit windows
+constexpr uint32_t G1M_ND = (1u << G1M_BITS) - 1;       // non-zero digits per window
+constexpr uint32_t G1M_KSTR = 128;                      // bucket indices per (L, kind): 8 x 15 used
+constexpr uint32_t G1M_NBL = 2 * G1M_KSTR;              // bucket indices per large message
+constexpr uint32_t G1M_NONE = 0xffffffffu;
+constexpr uint32_t G1M_MIN = 64;                        // items per message for the G1 MSM (hipbls_rlc_g1_msm_min)
+
+// ---- plan: which messages are large, where their slots start --------------------------------------------------
+// cnt[m] items per message -> lid[m] (dense large index or G1M_NONE), lmsg[L] = m, soff[L] = first slot of L
+// (soff[nl] = total slots), meta[0] = nl, meta[1] = total slots.  The serial form (host build; the device runs the
+// same decisions as a one-workgroup scan, kernels.h k_g1m_plan).
+BLS_HD BLS_INLINE void g1m_plan_serial(const uint32_t* cnt, uint64_t n_msgs, uint32_t min, uint32_t* lid,
+                                       uint32_t* lmsg, uint32_t* soff, uint32_t* meta) {
+  uint32_t nl = 0, tot = 0;
+  for (uint64_t m = 0; m < n_msgs; ++m) {
+    if (cnt[m] >= min) {
+      lid[m] = nl;
+      lmsg[nl] = (uint32_t)m;
+      soff[nl] = tot;
+      ++nl;
+      tot += cnt[m];
+    } else {
+      lid[m] = G1M_NONE;
+    }
+  }
+  soff[nl] = tot;
+  meta[0] = nl;
+  meta[1] = tot;
+}
+
+// item i -> its slot (pos[i]) and the slot's message (slot_l), cursor zeroed per large message
+BLS_HD BLS_INLINE void g1m_rank_lane(uint64_t i, const uint32_t* msg_idx, uint64_t n_msgs, const uint32_t* lid,
+                                     const uint32_t* soff, uint32_t* cursor, uint32_t* pos, uint32_t* slot_l) {
+  const uint32_t m = msg_idx[i];
+  const uint32_t L = m < n_msgs ? lid[m] : G1M_NONE;
+  if (L == G1M_NONE) {
+    pos[i] = G1M_NONE;
+    return;
+  }
+  const uint32_t s = soff[L] + BLS_ATOMIC_ADD_U32(&cursor[L], 1u);
+  pos[i] = s;
+  slot_l[s] = L;
+}
+
+// stage 1's G1 part for an item of a large message (rlcb_items_lane): pk and [x] pk into the slot, with the
+// item's scalars; zero scalars when the item already has its final status.  n = the slot capacity (gxp offset).
+BLS_HD BLS_INLINE void g1m_store_slot(uint32_t* gpts, uint32_t* gsc, uint64_t n, uint32_t s, bool pending,
+                                      const g1a& pk, const g1j& xpk, uint32_t a, uint32_t b) {
+  aos_store<24>(gpts, s, &pk.x.v[0]);
+  aos_store<36>(gpts + 24 * n, s, &xpk.x.v[0]);
+  gsc[2 * (uint64_t)s] = pending ? a : 0u;
+  gsc[2 * (uint64_t)s + 1] = pending ? b : 0u;
+}
+
+BLS_HD BLS_INLINE uint32_t g1m_digit(uint32_t k, int w) { return (k >> (G1M_BITS * w)) & G1M_ND; }
+BLS_HD BLS_INLINE uint64_t g1m_bucket(uint32_t L, int kind, int w, uint32_t d) {
+  return (uint64_t)L * G1M_NBL + (uint64_t)kind * G1M_KSTR + (uint64_t)w * G1M_ND + d - 1;
+}
+
+// histogram / scatter of slot s's entries (kind 0 with a, kind 1 with b; one per non-zero digit) over its
+// message's buckets
+BLS_HD BLS_INLINE void g1m_hist_lane(uint64_t s, const uint32_t* meta, const uint32_t* gsc, const uint32_t* slot_l,
+                                     uint32_t* bcnt) {
+  if (s >= meta[1]) return;
+  const uint32_t L = slot_l[s];
+  for (int kind = 0; kind < 2; ++kind) {
+    const uint32_t k = gsc[2 * s + kind];
+    for (int w = 0; w < G1M_WIN; ++w) {
+      const uint32_t d = g1m_digit(k, w);
+      if (d) BLS_ATOMIC_ADD_U32(&bcnt[g1m_bucket(L, kind, w, d)], 1u);
+    }
+  }
+}
+BLS_HD BLS_INLINE void g1m_scatter_lane(uint64_t s, const uint32_t* meta, const uint32_t* gsc,
+                                        const uint32_t* slot_l, uint32_t* bcur, uint32_t* list) {
+  if (s >= meta[1]) return;
+  const uint32_t L = slot_l[s];
+  for (int kind = 0; kind < 2; ++kind) {
+    const uint32_t k = gsc[2 * s + kind];
+    for (int w = 0; w < G1M_WIN; ++w) {
+      const uint32_t d = g1m_digit(k, w);
+      if (d) list[BLS_ATOMIC_ADD_U32(&bcur[g1m_bucket(L, kind, w, d)], 1u)] = (uint32_t)s;
+    }
+  }
+}
+
+// bucket b: the sum of its entries, gathered by slot (the next one loaded before the current addition, as
+// rlcb.h msm_bucket_lane); B: Jacobian, 36 words, AoS.  boff: exclusive offsets over all nl * G1M_NBL indices.
+BLS_HD BLS_INLINE void g1m_bucket_lane(uint64_t b, const uint32_t* meta, const uint32_t* boff, const uint32_t* list,
+                                       const uint32_t* gpts, uint64_t n, uint32_t* B) {
+  if (b >= (uint64_t)meta[0] * G1M_NBL) return;
+  g1j acc;
+  jac_set_inf(acc);
+  const uint32_t k0 = boff[b], k1 = boff[b + 1];
+  if ((b / G1M_KSTR) & 1) {  // [x] pk, Jacobian
+    const uint32_t* gxp = gpts + 24 * n;
+    g1j q;
+    if (k0 < k1) aos_load<36>(&q.x.v[0], gxp, list[k0]);
+    for (uint32_t k = k0; k < k1; ++k) {
+      const g1j cur = q;
+      if (k + 1 < k1) aos_load<36>(&q.x.v[0], gxp, list[k + 1]);
+      g1j x = acc, y;
+      jac_add(y, x, cur);
+      acc = y;
+    }
+  } else {  // pk, affine
+    g1a q;
+    if (k0 < k1) aos_load<24>(&q.x.v[0], gpts, list[k0]);
+    for (uint32_t k = k0; k < k1; ++k) {
+      const g1a cur = q;
+      if (k + 1 < k1) aos_load<24>(&q.x.v[0], gpts, list[k + 1]);
+      g1j x = acc, y;
+      jac_add_aff(y, x, cur);
+      acc = y;
+    }
+  }
+  aos_store<36>(B, b, &acc.x.v[0]);
+}
+
+// (L, w): sum_{d=1..15} d (B_{L,0,w,d} + B_{L,1,w,d}) by running sums (top digit first): R = sum_{d' >= d} B_d',
+// T = sum_d R
+BLS_HD BLS_INLINE void g1m_fold_lane(uint64_t q, const uint32_t* meta, const uint32_t* B, uint32_t* Wv) {
+  if (q >= (uint64_t)meta[0] * G1M_WIN) return;
+  const uint32_t L = (uint32_t)(q / G1M_WIN);
+  const int w = (int)(q % G1M_WIN);
+  g1j R, T;
+  jac_set_inf(R);
+  jac_set_inf(T);
+  for (uint32_t d = G1M_ND; d >= 1; --d) {
+    for (int kind = 0; kind < 2; ++kind) {
+      g1j b;
+      aos_load<36>(&b.x.v[0], B, g1m_bucket(L, kind, w, d));
+      g1j x = R, y;
+      jac_add(y, x, b);
+      R = y;
+    }
+    g1j u = T, v;
+    jac_add(v, u, R);
+    T = v;
+  }
+  aos_store<36>(Wv, q, &T.x.v[0]);
+}
+
+// R_L = sum_w [16^w] W_{L,w} (Horner from the top window)
+BLS_HD BLS_INLINE void g1m_combine(g1j& R, const uint32_t* Wv, uint64_t L) {
+  aos_load<36>(&R.x.v[0], Wv, L * G1M_WIN + (G1M_WIN - 1));
+  for (int w = G1M_WIN - 2; w >= 0; --w) {
+    for (int k = 0; k < G1M_BITS; ++k) {
+      g1j t;
+      jac_dbl_body(t, R);
+      R = t;
+    }
+    g1j t;
+    aos_load<36>(&t.x.v[0], Wv, L * G1M_WIN + (uint64_t)w);
+    g1j x = R, y;
+    jac_add(y, x, t);
+    R = y;
+  }
+}
+
+// the windows' fallback after a failed batch check needs [r_i] pk_i per item: from the slot (Shamir, as stage 1)
+BLS_HD BLS_INLINE void g1m_item_rpk(g1j& rp, const uint32_t* gpts, uint64_t n, const uint32_t* gsc, uint32_t s) {
+  g1a pk;
+  g1j pj, xj;
+  aos_load<24>(&pk.x.v[0], gpts, s);
+  aos_load<36>(&xj.x.v[0], gpts + 24 * n, s);
+  jac_from_aff(pj, pk);
+  jac_mul2_u32(rp, pj, xj, gsc[2 * (uint64_t)s], gsc[2 * (uint64_t)s + 1]);
+}
+
+// the Miller value of (R_L, H(m_L)) on one lane into column col of F (host build; the device splits it over a lane
+// pair, kernels.h k_g1m_miller); the value 1 for L >= nl or an empty R
+template <int S>
+BLS_HD BLS_INLINE void g1m_miller_lane(const f12l<S>& Lf, uint64_t L, const uint32_t* meta, const uint32_t* lmsg,
+                                       const uint32_t* Wv, const uint32_t* H, uint64_t hstride, const uint32_t* hslot,
+                                       uint32_t* F, uint64_t col, uint64_t fstride) {
+  fp12 f;
+  fp12_set_one(f);
+  if (L < meta[0]) {
+    g1j R;
+    g1m_combine(R, Wv, L);
+    if (!jac_is_inf(R)) {
+      g1a P[1];
+      g2a Q[1];
+      jac_to_aff(P[0], R);
+      soa_load<48>(&Q[0].x.c0.v[0], H, hstride, h_col(hslot, lmsg[L]));
+      miller_loop_multi_l<1>(f, Lf, P, Q, 1);
+    }
+  }
+  soa_store<144>(F, fstride, col, &f.c0.c0.c0.v[0]);
+}
+
+}  // namespace bls

@@ -162,7 +162,7 @@ struct Context {
   uint64_t r_call = 0;           // entry-point call that call belonged to
   // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
   DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_flag, m_Fs;
-  hipEvent_t rlcb_ev_sf = nullptr;  // the (-g1, S) Miller value is in m_Fs
+  DevBuf g1_ws;  // the G1 MSM per large message (g1msm.h), carved by G1mLayout; its Miller values go to m_F
   uint64_t slots = 0;               // waves in flight at one wave per SIMD: 4 x compute units (wave_slots)
   // Verdicts come back through a ring of pinned slots, one per batch check in flight, so a launch only waits
   // on the host when kRlcbSlots checks are still unread (never in the enqueue-only *_device paths otherwise).
@@ -701,6 +701,43 @@ int launch_rlc(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const ui
 // them; one whose batches pass keeps the cheap path).  The verdict comes back asynchronously (pinned copy +
 // event), so the policy never blocks a launch.
 std::atomic<int> g_rlc_mode{HIPBLS_RLC_AUTO};
+// G1 MSM per message (g1msm.h, hipbls_rlc_set_g1_msm_min): messages with >= g_g1m_min items get one bucket-method
+// sum instead of per-item [r_i] pk_i, when the batch averages >= kG1mAvg items per message (committee roots).
+std::atomic<uint32_t> g_g1m_min{G1M_MIN};
+constexpr uint64_t kG1mAvg = 8;
+
+// The G1 MSM's workspace for n items over n_msgs messages, at most nl_max of them large; word offsets into one
+// buffer (each region 64-word aligned).
+struct G1mLayout {
+  uint64_t nl_max = 0, nb = 0, nparts = 0;
+  uint64_t cnt, lid, lmsg, soff, cur, meta, pos, slotl, pts, sc, bcnt, boff, bcur, list, B, Wv, part, words = 0;
+  G1mLayout(uint64_t n, uint64_t n_msgs, uint64_t nl) : nl_max(nl) {
+    nb = nl * G1M_NBL;
+    nparts = (nb + kScanBlk - 1) / kScanBlk;
+    auto take = [&](uint64_t w) {
+      const uint64_t at = words;
+      words += (w + 63) & ~(uint64_t)63;
+      return at;
+    };
+    cnt = take(n_msgs);
+    lid = take(n_msgs);
+    lmsg = take(nl);
+    soff = take(nl + 1);
+    cur = take(nl);
+    meta = take(2);
+    pos = take(n);
+    slotl = take(n);
+    pts = take(60 * n);
+    sc = take(2 * n);
+    bcnt = take(nb);
+    boff = take(nb + 1);
+    bcur = take(nb);
+    list = take(2 * (uint64_t)G1M_WIN * n);
+    B = take(36 * nb);
+    Wv = take(36 * nl * G1M_WIN);
+    part = take(nparts + 1);
+  }
+};
 constexpr uint64_t kRlcbMinItems = 1024;
 constexpr int kRlcbBackoff = 8;
 
@@ -753,12 +790,16 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   const uint64_t npts = 2 * n;
   const uint64_t nch = rlcb_chunk_count(n, wave_slots(c));
   const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
+  const uint32_t g1min = g_g1m_min.load();
+  const bool g1 = g1min > 0 && n_msgs > 0 && n >= kG1mAvg * n_msgs && n >= g1min;
+  const uint64_t nl_max = g1 ? std::min<uint64_t>(n_msgs, n / g1min) : 0;
+  const uint64_t cols = nch + nl_max;  // product-tree columns: the chunks, then one per large message
+  const G1mLayout gl(n, n_msgs, nl_max);
   if (!c.rlcb_host_flag) {
     HIP_TRY(hipHostMalloc((void**)&c.rlcb_host_flag, Context::kRlcbSlots * sizeof(int32_t), hipHostMallocDefault));
     for (int k = 0; k < Context::kRlcbSlots; ++k) HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_items, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_msm, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_sf, hipEventDisableTiming));
   }
   int rc = ensure_rlc_streams(c);
   if (rc) return rc;
@@ -774,8 +815,11 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   HIP_TRY(c.m_B.ensure((uint64_t)MSM_WINDOWS * MSM_NB * 72 * 4));
   HIP_TRY(c.m_Sg.ensure((uint64_t)MSM_WINDOWS * MSM_NSEG * 72 * 4));
   HIP_TRY(c.m_W.ensure((uint64_t)MSM_WINDOWS * 72 * 4));
-  HIP_TRY(c.m_F.ensure((nch + 1) * 144 * 4));
-  HIP_TRY(c.m_F2.ensure(((nch + RLCB_FAN) / RLCB_FAN) * 144 * 4));
+  HIP_TRY(c.m_F.ensure(cols * 144 * 4));
+  HIP_TRY(c.m_F2.ensure(((cols + RLCB_FAN - 1) / RLCB_FAN) * 144 * 4));
+  if (g1) HIP_TRY(c.g1_ws.ensure(gl.words * 4));
+  uint32_t* gw = (uint32_t*)c.g1_ws.p;
+  auto G = [&](uint64_t off) { return g1 ? gw + off : nullptr; };
   HIP_TRY(c.m_flag.ensure(4));
   HIP_TRY(c.m_Fs.ensure(144 * 4));
   uint32_t* rpk = (uint32_t*)c.r_pk.p;
@@ -783,11 +827,12 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   uint32_t* pts = (uint32_t*)c.m_pts.p;
   uint32_t* sc = (uint32_t*)c.m_sc.p;
   int32_t* flag = (int32_t*)c.m_flag.p;
-  // Streams: the caller's stream s hashes the messages while sub[0] runs the items and then the MSM's short
-  // kernels; sub[1] runs the chunk Miller loops (plus the (-g1, S) lane) and their product once the MSM and the
-  // hash are done -- after the MSM, because the chunk kernel holds every SIMD for its whole run and a short kernel
-  // queued behind it waits that long (round 2: k_msm_scan 33 ms beside k_rlcb_chunks 37.7 ms).  s joins for the
-  // verdict and the window stages.
+  // Streams: the caller's stream s hashes the messages while sub[0] runs the items and then the G2 MSM's short
+  // kernels; sub[1] runs the G1 MSM of the large messages beside the G2 MSM (both only need the items) and their
+  // Miller values, then the chunk Miller loops and the product once the G2 MSM and the hash are done -- after the
+  // MSM, because the chunk kernel holds every SIMD for its whole run and a short kernel queued behind it waits that
+  // long (round 2: k_msm_scan 33 ms beside k_rlcb_chunks 37.7 ms).  s, idle after the hash, runs the (-g1, S) lane
+  // pair once the G2 MSM is done (beside the chunks or the G1 Miller values), then the verdict and the windows.
   hipStream_t s0 = c.sub[0], s1 = c.sub[1];
   rc = ws_begin(c, s, WS_RLC);
   if (rc) return rc;
@@ -803,9 +848,24 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   }
   HIP_TRY(hipEventRecord(c.ev_hash, s));
   HIP_TRY(hipStreamWaitEvent(s0, c.ev_fork, 0));
+  const unsigned gn256 = (unsigned)((n + 255) / 256);
+  if (g1) {  // which messages are large, and each of their items' slot (g1msm.h)
+    HIP_TRY(hipMemsetAsync(G(gl.cnt), 0, n_msgs * 4, s0));
+    HIP_TRY(hipMemsetAsync(G(gl.cur), 0, nl_max * 4, s0));
+    HIP_TRY(hipMemsetAsync(G(gl.bcnt), 0, gl.nb * 4, s0));
+    rc = timed(c, "rlcb_g1plan", s0, [&] {
+      hipLaunchKernelGGL(k_g1m_count, dim3(gn256), dim3(256), 0, s0, n, d_midx, n_msgs, G(gl.cnt));
+      hipLaunchKernelGGL(k_g1m_plan, dim3(1), dim3(kPlanThreads), 0, s0, (const uint32_t*)G(gl.cnt), n_msgs, g1min,
+                         G(gl.lid), G(gl.lmsg), G(gl.soff), G(gl.meta));
+      hipLaunchKernelGGL(k_g1m_rank, dim3(gn256), dim3(256), 0, s0, n, d_midx, n_msgs, (const uint32_t*)G(gl.lid),
+                         (const uint32_t*)G(gl.soff), G(gl.cur), G(gl.pos), G(gl.slotl));
+    });
+    if (rc) return rc;
+  }
   rc = timed(c, "rlcb_items", s0, [&] {
     hipLaunchKernelGGL(k_rlcb_items, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s0, n, d_pks, d_sigs, d_midx, n_msgs,
-                       seed, rpk, pts, sc, d_status, d_kidx, T, tcode, tab);
+                       seed, rpk, pts, sc, d_status, d_kidx, T, tcode, tab, (const uint32_t*)G(gl.pos), G(gl.pts),
+                       G(gl.sc));
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.rlcb_ev_items, s0));
@@ -827,22 +887,53 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.rlcb_ev_msm, s0));
-  // (-g1, S) on a lane pair beside the chunks, on the SIMD rlcb_chunk_count leaves free
-  rc = timed(c, "rlcb_sfactor", s0, [&] {
-    hipLaunchKernelGGL(k_rlcb_sfactor, dim3(1), dim3(kBlock), 0, s0, (const uint32_t*)c.m_W.p, (uint32_t*)c.m_Fs.p);
+  if (g1) {  // the large messages' sums R_L and their Miller values, beside the G2 MSM
+    HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_items, 0));
+    rc = timed(c, "rlcb_g1sort", s1, [&] {
+      hipLaunchKernelGGL(k_g1m_hist, dim3(gn256), dim3(256), 0, s1, n, (const uint32_t*)G(gl.meta),
+                         (const uint32_t*)G(gl.sc), (const uint32_t*)G(gl.slotl), G(gl.bcnt));
+      hipLaunchKernelGGL(k_scan_part, dim3((unsigned)gl.nparts), dim3(kScanBlk), 0, s1, (const uint32_t*)G(gl.bcnt),
+                         gl.nb, G(gl.part));
+      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlk), 0, s1, G(gl.part), gl.nparts);
+      hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)gl.nparts), dim3(kScanBlk), 0, s1, (const uint32_t*)G(gl.bcnt),
+                         gl.nb, (const uint32_t*)G(gl.part), gl.nparts, G(gl.boff), G(gl.bcur));
+      hipLaunchKernelGGL(k_g1m_scatter, dim3(gn256), dim3(256), 0, s1, n, (const uint32_t*)G(gl.meta),
+                         (const uint32_t*)G(gl.sc), (const uint32_t*)G(gl.slotl), G(gl.bcur), G(gl.list));
+    });
+    if (rc) return rc;
+    rc = timed(c, "rlcb_g1msm", s1, [&] {
+      hipLaunchKernelGGL(k_g1m_bucket, dim3((unsigned)grid_for(gl.nb)), dim3(kBlock), 0, s1, gl.nb,
+                         (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.boff), (const uint32_t*)G(gl.list),
+                         (const uint32_t*)G(gl.pts), n, G(gl.B));
+      hipLaunchKernelGGL(k_g1m_fold, dim3((unsigned)grid_for(nl_max * G1M_WIN)), dim3(kBlock), 0, s1,
+                         nl_max * G1M_WIN, (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.B), G(gl.Wv));
+    });
+    if (rc) return rc;
+    HIP_TRY(hipStreamWaitEvent(s1, c.ev_hash, 0));
+    rc = timed(c, "rlcb_g1miller", s1, [&] {
+      hipLaunchKernelGGL(k_g1m_miller, dim3((unsigned)grid_for(2 * nl_max)), dim3(kBlock), 0, s1, nl_max,
+                         (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.lmsg), (const uint32_t*)G(gl.Wv),
+                         (const uint32_t*)d_H, hstride, d_hslot, (uint32_t*)c.m_F.p, nch, cols);
+    });
+    if (rc) return rc;
+  }
+  HIP_TRY(hipStreamWaitEvent(s, c.rlcb_ev_msm, 0));
+  // (-g1, S) on a lane pair on s (after the hash), beside the chunks on the SIMD rlcb_chunk_count leaves free
+  rc = timed(c, "rlcb_sfactor", s, [&] {
+    hipLaunchKernelGGL(k_rlcb_sfactor, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)c.m_W.p, (uint32_t*)c.m_Fs.p);
   });
   if (rc) return rc;
-  HIP_TRY(hipEventRecord(c.rlcb_ev_sf, s0));
   HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_msm, 0));
   HIP_TRY(hipStreamWaitEvent(s1, c.ev_hash, 0));
   rc = timed(c, "rlcb_chunks", s1, [&] {
     hipLaunchKernelGGL(k_rlcb_chunks, dim3((unsigned)grid_for(nch)), dim3(kBlock), 0, s1, n, (const int32_t*)d_status,
-                       d_midx, (const uint32_t*)rpk, (const uint32_t*)d_H, hstride, d_hslot, (uint32_t*)c.m_F.p, nch);
+                       d_midx, (const uint32_t*)rpk, (const uint32_t*)d_H, hstride, d_hslot, (uint32_t*)c.m_F.p, nch,
+                       cols);
   });
   if (rc) return rc;
   uint32_t* src = (uint32_t*)c.m_F.p;
   uint32_t* dst = (uint32_t*)c.m_F2.p;
-  uint64_t cur = nch;
+  uint64_t cur = cols;
   rc = timed(c, "rlcb_product", s1, [&] {
     while (cur > 1) {
       const uint64_t nxt = (cur + RLCB_FAN - 1) / RLCB_FAN;
@@ -857,14 +948,14 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));
   HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
-  HIP_TRY(hipStreamWaitEvent(s, c.rlcb_ev_sf, 0));
   rc = timed(c, "rlcb_final", s, [&] {
     hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, (const uint32_t*)c.m_Fs.p, flag);
   });
   if (rc) return rc;
   rc = timed(c, "rlcb_mark", s, [&] {
     hipLaunchKernelGGL(k_rlcb_mark, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, n, (const int32_t*)flag, d_status,
-                       (const uint32_t*)pts, (const uint32_t*)sc, rsig);
+                       (const uint32_t*)pts, (const uint32_t*)sc, rsig, (const uint32_t*)G(gl.pos),
+                       (const uint32_t*)G(gl.pts), (const uint32_t*)G(gl.sc), rpk);
   });
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(c.rlcb_host_flag + slot, flag, 4, hipMemcpyDeviceToHost, s));
@@ -1826,6 +1917,8 @@ int hipbls_set_timing(int enabled) {
   g_timing = enabled != 0;
   return HIPBLS_OK;
 }
+
+int hipbls_rlc_set_g1_msm_min(uint32_t min) { return (int)g_g1m_min.exchange(min); }
 
 int hipbls_rlc_set_mode(int mode) {
   if (mode != HIPBLS_RLC_AUTO && mode != HIPBLS_RLC_WINDOWS && mode != HIPBLS_RLC_BATCH)

@@ -868,9 +868,199 @@ __global__ void __launch_bounds__(kBlock) k_rlcb_items(uint64_t n, const uint8_t
                                                        int32_t* __restrict__ status,
                                                        const uint32_t* __restrict__ key_idx, uint64_t T,
                                                        const int32_t* __restrict__ tcode,
-                                                       const uint32_t* __restrict__ tab) {
+                                                       const uint32_t* __restrict__ tab,
+                                                       const uint32_t* __restrict__ g1pos, uint32_t* __restrict__ gpts,
+                                                       uint32_t* __restrict__ gsc) {
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (i < n) rlcb_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk, pts, sc, status, key_idx, T, tcode, tab);
+  if (i < n)
+    rlcb_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk, pts, sc, status, key_idx, T, tcode, tab, g1pos, gpts,
+                    gsc);
+}
+
+// ---------------------------------------------------------------- the G1 MSM per large message (g1msm.h)
+__global__ void __launch_bounds__(256) k_g1m_count(uint64_t n, const uint32_t* __restrict__ msg_idx, uint64_t n_msgs,
+                                                   uint32_t* __restrict__ cnt) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < n && msg_idx[i] < n_msgs) atomicAdd(&cnt[msg_idx[i]], 1u);
+}
+
+// g1msm.h g1m_plan_serial as one workgroup: each thread a contiguous range of messages, an LDS scan of the ranges'
+// (large messages, slots) counts, then the same assignments in message order.
+constexpr int kPlanThreads = 1024;
+__global__ void __launch_bounds__(kPlanThreads) k_g1m_plan(const uint32_t* __restrict__ cnt, uint64_t n_msgs,
+                                                           uint32_t min, uint32_t* __restrict__ lid,
+                                                           uint32_t* __restrict__ lmsg, uint32_t* __restrict__ soff,
+                                                           uint32_t* __restrict__ meta) {
+  __shared__ uint32_t s_nl[kPlanThreads], s_tot[kPlanThreads];
+  const int t = threadIdx.x;
+  const uint64_t span = (n_msgs + kPlanThreads - 1) / kPlanThreads;
+  const uint64_t m0 = t * span, m1 = m0 + span < n_msgs ? m0 + span : n_msgs;
+  uint32_t nl = 0, tot = 0;
+  for (uint64_t m = m0; m < m1; ++m)
+    if (cnt[m] >= min) {
+      ++nl;
+      tot += cnt[m];
+    }
+  s_nl[t] = nl;
+  s_tot[t] = tot;
+  __syncthreads();
+  if (t == 0) {  // serial exclusive scan of 1,024 pairs
+    uint32_t a = 0, b = 0;
+    for (int k = 0; k < kPlanThreads; ++k) {
+      const uint32_t x = s_nl[k], y = s_tot[k];
+      s_nl[k] = a;
+      s_tot[k] = b;
+      a += x;
+      b += y;
+    }
+    soff[a] = b;
+    meta[0] = a;
+    meta[1] = b;
+  }
+  __syncthreads();
+  nl = s_nl[t];
+  tot = s_tot[t];
+  for (uint64_t m = m0; m < m1; ++m) {
+    if (cnt[m] >= min) {
+      lid[m] = nl;
+      lmsg[nl] = (uint32_t)m;
+      soff[nl] = tot;
+      ++nl;
+      tot += cnt[m];
+    } else {
+      lid[m] = G1M_NONE;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_g1m_rank(uint64_t n, const uint32_t* __restrict__ msg_idx, uint64_t n_msgs,
+                                                  const uint32_t* __restrict__ lid, const uint32_t* __restrict__ soff,
+                                                  uint32_t* __restrict__ cursor, uint32_t* __restrict__ pos,
+                                                  uint32_t* __restrict__ slot_l) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i < n) g1m_rank_lane(i, msg_idx, n_msgs, lid, soff, cursor, pos, slot_l);
+}
+
+__global__ void __launch_bounds__(256) k_g1m_hist(uint64_t nslots, const uint32_t* __restrict__ meta,
+                                                  const uint32_t* __restrict__ gsc, const uint32_t* __restrict__ slot_l,
+                                                  uint32_t* __restrict__ bcnt) {
+  const uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (s < nslots) g1m_hist_lane(s, meta, gsc, slot_l, bcnt);
+}
+
+__global__ void __launch_bounds__(256) k_g1m_scatter(uint64_t nslots, const uint32_t* __restrict__ meta,
+                                                     const uint32_t* __restrict__ gsc,
+                                                     const uint32_t* __restrict__ slot_l, uint32_t* __restrict__ bcur,
+                                                     uint32_t* __restrict__ list) {
+  const uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (s < nslots) g1m_scatter_lane(s, meta, gsc, slot_l, bcur, list);
+}
+
+__global__ void __launch_bounds__(kBlock) k_g1m_bucket(uint64_t nb, const uint32_t* __restrict__ meta,
+                                                       const uint32_t* __restrict__ boff,
+                                                       const uint32_t* __restrict__ list,
+                                                       const uint32_t* __restrict__ gpts, uint64_t n,
+                                                       uint32_t* __restrict__ B) {
+  const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (b < nb) g1m_bucket_lane(b, meta, boff, list, gpts, n, B);
+}
+
+__global__ void __launch_bounds__(kBlock) k_g1m_fold(uint64_t nq, const uint32_t* __restrict__ meta,
+                                                     const uint32_t* __restrict__ B, uint32_t* __restrict__ Wv) {
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q < nq) g1m_fold_lane(q, meta, B, Wv);
+}
+
+// One lane pair per large message L < nl_max: R_L from the window sums (both lanes), the Miller value of (R_L, H(m_L))
+// split over the pair (lg2.h miller_loop_split, the same f as g1m_miller_lane's one-lane loop), the even lane writes
+// column col0 + L of F; the value 1 for L >= nl or an empty R.
+__global__ void __launch_bounds__(kBlock) k_g1m_miller(uint64_t nl_max, const uint32_t* __restrict__ meta,
+                                                       const uint32_t* __restrict__ lmsg, const uint32_t* __restrict__ Wv,
+                                                       const uint32_t* __restrict__ H, uint64_t hstride,
+                                                       const uint32_t* __restrict__ hslot, uint32_t* __restrict__ F,
+                                                       uint64_t col0, uint64_t fstride) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t L = t >> 1;
+  if (L >= nl_max) return;  // the same on both lanes of the pair
+  const uint32_t m = (t & 1) ? ~0u : 0u;
+  fp12 f;
+  fp12_set_one(f);
+  if (L < meta[0]) {
+    g1j R;
+    g1m_combine(R, Wv, L);
+    if (!jac_is_inf(R)) {  // the same on both lanes
+      g1a P;
+      g2a Q;
+      jac_to_aff(P, R);
+      soa_load<48>(&Q.x.c0.v[0], H, hstride, h_col(hslot, lmsg[L]));
+      fp6 h;
+      miller_loop_split(h, P, Q, m);
+      fp12h_gather(f, h, m);
+    }
+  }
+  if (!m) soa_store<144>(F, fstride, col0 + L, &f.c0.c0.c0.v[0]);
+}
+
+// ---- exclusive scan of n u32 counts (the G1 MSM's buckets): block sums, one-workgroup scan of them, block scans
+constexpr int kScanBlk = 1024;
+__global__ void __launch_bounds__(kScanBlk) k_scan_part(const uint32_t* __restrict__ in, uint64_t n,
+                                                        uint32_t* __restrict__ part) {
+  __shared__ uint32_t red[kScanBlk];
+  const uint64_t i = blockIdx.x * (uint64_t)kScanBlk + threadIdx.x;
+  red[threadIdx.x] = i < n ? in[i] : 0u;
+  __syncthreads();
+  for (int h = kScanBlk / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ void __launch_bounds__(kScanBlk) k_scan_top(uint32_t* __restrict__ part, uint64_t nparts) {
+  __shared__ uint32_t s[kScanBlk];
+  const uint64_t span = (nparts + kScanBlk - 1) / kScanBlk;
+  const uint64_t p0 = threadIdx.x * span, p1 = p0 + span < nparts ? p0 + span : nparts;
+  uint32_t sum = 0;
+  for (uint64_t p = p0; p < p1; ++p) sum += part[p];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    for (int k = 0; k < kScanBlk; ++k) {
+      const uint32_t x = s[k];
+      s[k] = a;
+      a += x;
+    }
+    part[nparts] = a;
+  }
+  __syncthreads();
+  uint32_t a = s[threadIdx.x];
+  for (uint64_t p = p0; p < p1; ++p) {
+    const uint32_t x = part[p];
+    part[p] = a;
+    a += x;
+  }
+}
+// out[i] = exclusive prefix (and cur[i] a copy); out[n] = the total
+__global__ void __launch_bounds__(kScanBlk) k_scan_apply(const uint32_t* __restrict__ in, uint64_t n,
+                                                         const uint32_t* __restrict__ part, uint64_t nparts,
+                                                         uint32_t* __restrict__ out, uint32_t* __restrict__ cur) {
+  __shared__ uint32_t s[kScanBlk];
+  const uint64_t i = blockIdx.x * (uint64_t)kScanBlk + threadIdx.x;
+  const uint32_t v = i < n ? in[i] : 0u;
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int d = 1; d < kScanBlk; d <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t x = (int)threadIdx.x >= d ? s[threadIdx.x - d] : 0u;
+    __syncthreads();
+    s[threadIdx.x] += x;
+    __syncthreads();
+  }
+  if (i < n) {
+    const uint32_t e = part[blockIdx.x] + s[threadIdx.x] - v;
+    out[i] = e;
+    cur[i] = e;
+  }
+  if (i == 0) out[n] = part[nparts];
 }
 
 __global__ void __launch_bounds__(256) k_msm_hist(uint64_t npts, const uint32_t* __restrict__ sc,
@@ -960,10 +1150,10 @@ __global__ void __launch_bounds__(kBlock) k_rlcb_chunks(uint64_t n, const int32_
                                                         const uint32_t* __restrict__ rpk,
                                                         const uint32_t* __restrict__ H, uint64_t hstride,
                                                         const uint32_t* __restrict__ hslot, uint32_t* __restrict__ F,
-                                                        uint64_t n_chunks) {
+                                                        uint64_t n_chunks, uint64_t fstride) {
   const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   BLS_LANE_F12(Lf);
-  if (c < n_chunks) rlcb_chunk_lane(Lf, c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks, n_chunks);
+  if (c < n_chunks) rlcb_chunk_lane(Lf, c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks, fstride);
 }
 
 __global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict__ Fin, uint64_t nin,
@@ -1022,9 +1212,12 @@ __global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restric
 
 __global__ void __launch_bounds__(kBlock) k_rlcb_mark(uint64_t n, const int32_t* __restrict__ flag,
                                                       int32_t* __restrict__ status, const uint32_t* __restrict__ pts,
-                                                      const uint32_t* __restrict__ sc, uint32_t* __restrict__ rsig) {
+                                                      const uint32_t* __restrict__ sc, uint32_t* __restrict__ rsig,
+                                                      const uint32_t* __restrict__ g1pos,
+                                                      const uint32_t* __restrict__ gpts,
+                                                      const uint32_t* __restrict__ gsc, uint32_t* __restrict__ rpk) {
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (i < n) rlcb_mark_lane(i, n, flag[0] != 0, status, pts, sc, rsig);
+  if (i < n) rlcb_mark_lane(i, n, flag[0] != 0, status, pts, sc, rsig, g1pos, gpts, gsc, rpk);
 }
 
 // ---------------------------------------------------------------- resident pubshare table

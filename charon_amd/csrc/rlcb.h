@@ -51,6 +51,9 @@ BLS_HD BLS_INLINE uint32_t bls_serial_add_u32(uint32_t* p, uint32_t v) {  // hos
 }
 #define BLS_ATOMIC_ADD_U32(p, v) bls_serial_add_u32((p), (v))
 #endif
+}  // namespace bls
+#include "g1msm.h"
+namespace bls {
 
 // ---- stage 1 ------------------------------------------------------------------------------------
 // pts: 2n affine G2 points, point-major (AoS, 48 contiguous words each: sig_i at i, psi(sig_i) at n + i), because
@@ -60,7 +63,9 @@ BLS_HD BLS_INLINE void rlcb_items_lane(uint64_t i, const uint8_t* pks, const uin
                                        uint64_t n, uint64_t n_msgs, const rlc_seed& seed, uint32_t* rpk,
                                        uint32_t* pts, uint32_t* sc, int32_t* status,
                                        const uint32_t* key_idx = nullptr, uint64_t T = 0,
-                                       const int32_t* tcode = nullptr, const uint32_t* tab = nullptr) {
+                                       const int32_t* tcode = nullptr, const uint32_t* tab = nullptr,
+                                       const uint32_t* g1pos = nullptr, uint32_t* gpts = nullptr,
+                                       uint32_t* gsc = nullptr) {
   g1j rp;
   jac_set_inf(rp);
   g2a sig, psig;
@@ -72,6 +77,8 @@ BLS_HD BLS_INLINE void rlcb_items_lane(uint64_t i, const uint8_t* pks, const uin
   if (msg_idx[i] >= n_msgs || (!pks && key_idx[i] >= T)) {
     st = HIPBLS_ERR_ARG;
   } else {
+    // items of a message with many items (g1msm.h): [r] pk comes from the message's G1 MSM, not from this lane
+    const uint32_t slot = g1pos ? g1pos[i] : G1M_NONE;
     g1a pk;
     g1j xpk;
     const int dp = pks ? g1_decompress_keep_x(pk, xpk, pks + 48 * i) : pubtab_get(pk, xpk, key_idx[i], T, tcode, tab);
@@ -86,9 +93,11 @@ BLS_HD BLS_INLINE void rlcb_items_lane(uint64_t i, const uint8_t* pks, const uin
     }
     if (st == RLC_PENDING) {
       rlc_scalars(a, b, seed, i);
-      g1j pj;
-      jac_from_aff(pj, pk);
-      jac_mul2_u32(rp, pj, xpk, a, b);
+      if (slot == G1M_NONE) {
+        g1j pj;
+        jac_from_aff(pj, pk);
+        jac_mul2_u32(rp, pj, xpk, a, b);
+      }
       g2j sj, psj;
       jac_from_aff(sj, sig);
       g2_psi(psj, sj);  // Z stays 1: psi of an affine point is affine
@@ -98,6 +107,7 @@ BLS_HD BLS_INLINE void rlcb_items_lane(uint64_t i, const uint8_t* pks, const uin
       fp2_set_zero(sig.x);
       fp2_set_zero(sig.y);
     }
+    if (slot != G1M_NONE) g1m_store_slot(gpts, gsc, n, slot, st == RLC_PENDING, pk, xpk, a, b);
   }
   soa_store<36>(rpk, n, i, &rp.x.v[0]);
   aos_store<48>(pts, i, &sig.x.c0.v[0]);
@@ -295,11 +305,18 @@ BLS_HD BLS_INLINE void fp12_prod_lane(uint64_t g, const uint32_t* Fin, uint64_t 
 // pass: every pending item is valid.  Otherwise [r_i] sig_i = [a_i] sig_i + [b_i] psi(sig_i) goes to rsig (Jacobian
 // SoA, 72 x n) for the window stages, which decide the pending items.
 BLS_HD BLS_INLINE void rlcb_mark_lane(uint64_t i, uint64_t n, bool pass, int32_t* status, const uint32_t* pts,
-                                      const uint32_t* sc, uint32_t* rsig) {
+                                      const uint32_t* sc, uint32_t* rsig, const uint32_t* g1pos = nullptr,
+                                      const uint32_t* gpts = nullptr, const uint32_t* gsc = nullptr,
+                                      uint32_t* rpk = nullptr) {
   if (status[i] != RLC_PENDING) return;
   if (pass) {
     status[i] = HIPBLS_OK;
     return;
+  }
+  if (g1pos && g1pos[i] != G1M_NONE) {  // stage 1 left [r] pk to the G1 MSM: the windows need it per item
+    g1j rp;
+    g1m_item_rpk(rp, gpts, n, gsc, g1pos[i]);
+    soa_store<36>(rpk, n, i, &rp.x.v[0]);
   }
   g2a s, ps;
   aos_load<48>(&s.x.c0.v[0], pts, i);

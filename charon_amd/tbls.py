@@ -72,6 +72,7 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_set_timing": ([ctypes.c_int], ctypes.c_int),
         "hipbls_set_pair_mode": ([ctypes.c_int], ctypes.c_int),
         "hipbls_rlc_set_mode": ([ctypes.c_int], ctypes.c_int),
+        "hipbls_rlc_set_g1_msm_min": ([ctypes.c_uint32], ctypes.c_int),
         "hipbls_threshold_aggregate_verify_batch": ([u8p, i64p, u64p, u64, u8p, u8p, u64p, u8p, i32p, i32p],
                                                     ctypes.c_int),
         "hipbls_threshold_aggregate_verify_batch_device": ([vp, vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, vp],
@@ -143,6 +144,7 @@ def exported_symbols() -> List[str]:
         "hipbls_rlc_set_mode", "hipbls_rlc_batch_stats", "hipbls_threshold_aggregate_verify_batch",
         "hipbls_threshold_aggregate_verify_batch_device", "hipbls_init_devices", "hipbls_device_slots",
         "hipbls_plan_ranges", "hipbls_queue_keyed_batches", "hipbls_deserialize_status", "hipbls_device_streams",
+        "hipbls_rlc_set_g1_msm_min",
     ]
 
 
@@ -617,6 +619,14 @@ class HipBLS:
         if rc not in (RLC_AUTO, RLC_WINDOWS, RLC_BATCH):
             _check(rc, self.lib)
         return rc
+
+    def set_rlc_g1_msm_min(self, min_items: int) -> int:
+        """Items per message from which the batch-wide check sums [r_i] pk_i by one Pippenger MSM per message
+        (g1msm.h; batches averaging >= 8 items per message); 0 = off.  Returns the previous value.  Statuses never
+        depend on it."""
+        if not 0 <= min_items < 1 << 31:
+            raise ValueError("min_items out of range")
+        return self.lib.hipbls_rlc_set_g1_msm_min(min_items)
 
     def rlc_batch_stats(self) -> Tuple[int, int, int]:
         """(batch-wide checks launched, passed, last verdict: -1 none / 0 failed / 1 passed)."""

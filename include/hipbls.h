@@ -218,6 +218,11 @@ int hipbls_rlc_stats(uint64_t* windows, uint64_t* windows_failed, uint64_t* item
  * only; HIPBLS_RLC_BATCH: batch-wide first always.  Returns the previous mode or HIPBLS_ERR_ARG. */
 enum { HIPBLS_RLC_AUTO = 0, HIPBLS_RLC_WINDOWS = 1, HIPBLS_RLC_BATCH = 2 };
 int hipbls_rlc_set_mode(int mode);
+/* The batch-wide check's G1 side for batches that average >= 8 items per message (committee roots): each message
+ * with >= `min` items gets one Pippenger sum of [r_i] pk_i (charon_amd/csrc/g1msm.h) and one Miller loop, instead of
+ * a scalar multiplication per item.  0 turns it off; default 64.  Statuses never depend on it.  Returns the previous
+ * value. */
+int hipbls_rlc_set_g1_msm_min(uint32_t min);
 /* Batch-wide checks launched and passed since load, and the last verdict (-1 none, 0 failed, 1 passed); waits for
  * the last one in flight. */
 int hipbls_rlc_batch_stats(uint64_t* attempted, uint64_t* passed, int32_t* last);

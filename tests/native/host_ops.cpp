@@ -7,6 +7,7 @@
 
 static uint64_t g_rlcb_slots = 0;   // device wave slots rlcb_chunk_count plans for (ht_rlcb_set_slots)
 static uint64_t g_rlcb_chunks = 0;  // test override of the chunk count (0: rlcb_chunk_count)
+static uint32_t g_g1m_min = 64;     // G1 MSM threshold (ht_rlcb_set_g1_min; the device's hipbls_rlc_set_g1_msm_min)
 namespace bls {
 thread_local uint64_t g_fp_mul_count = 0;
 thread_local uint64_t g_fp_sqr_count = 0;
@@ -532,8 +533,23 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
     seed.w[k] = (uint32_t)seed32[4 * k] << 24 | (uint32_t)seed32[4 * k + 1] << 16 | (uint32_t)seed32[4 * k + 2] << 8 |
                 (uint32_t)seed32[4 * k + 3];
   std::vector<uint32_t> rpk(n * 36), rsig(n * 72), pts(2 * n * 48), sc(2 * n), H((n_msgs ? n_msgs : 1) * 48);
+  // the G1 MSM per large message (g1msm.h) under the runtime's rule (hipbls.hip launch_rlc_batch)
+  const uint32_t g1min = g_g1m_min;
+  const bool g1 = g1min > 0 && n_msgs > 0 && n >= 8 * n_msgs && n >= g1min;
+  const uint64_t nl_max = g1 ? std::min<uint64_t>(n_msgs, n / g1min) : 0;
+  std::vector<uint32_t> gcnt(n_msgs + 1, 0), lid(n_msgs + 1), lmsg(nl_max + 1), soff(nl_max + 2), gcur(nl_max + 1, 0);
+  std::vector<uint32_t> meta(2, 0), pos(n + 1), slotl(n + 1), gpts(60 * n + 4), gsc(2 * n + 2);
+  if (g1) {
+    for (uint64_t i = 0; i < n; ++i)
+      if (msg_idx[i] < n_msgs) gcnt[msg_idx[i]] += 1;
+    g1m_plan_serial(gcnt.data(), n_msgs, g1min, lid.data(), lmsg.data(), soff.data(), meta.data());
+    for (uint64_t i = 0; i < n; ++i)
+      g1m_rank_lane(i, msg_idx, n_msgs, lid.data(), soff.data(), gcur.data(), pos.data(), slotl.data());
+  }
+  const uint32_t* gpos = g1 ? pos.data() : nullptr;
   for (uint64_t i = 0; i < n; ++i)
-    rlcb_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk.data(), pts.data(), sc.data(), status);
+    rlcb_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk.data(), pts.data(), sc.data(), status, nullptr, 0,
+                    nullptr, nullptr, gpos, gpts.data(), gsc.data());
   mark(0);
   for (uint64_t m = 0; m < n_msgs; ++m) rlc_hash_lane(m, msgs, offs, H.data(), n_msgs, nullptr);
   mark(1);
@@ -544,16 +560,36 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
     Wc[k] = (&W[0].x.c0.v[0])[k];
     Wc[72 + k] = (&W[1].x.c0.v[0])[k];
   }
+  const uint64_t nb = nl_max * G1M_NBL;
+  std::vector<uint32_t> bcnt(nb + 1, 0), boff(nb + 1), bcur(nb + 1), glist(2 * G1M_WIN * n + 1), B(36 * nb + 4);
+  std::vector<uint32_t> Wv(36 * nl_max * G1M_WIN + 4);
+  if (g1) {  // counted with the MSM (stage 2 of counts6)
+    for (uint64_t t = 0; t < n; ++t) g1m_hist_lane(t, meta.data(), gsc.data(), slotl.data(), bcnt.data());
+    uint32_t acc = 0;
+    for (uint64_t b = 0; b < nb; ++b) {
+      boff[b] = bcur[b] = acc;
+      acc += bcnt[b];
+    }
+    boff[nb] = acc;
+    for (uint64_t t = 0; t < n; ++t) g1m_scatter_lane(t, meta.data(), gsc.data(), slotl.data(), bcur.data(), glist.data());
+    for (uint64_t b = 0; b < nb; ++b) g1m_bucket_lane(b, meta.data(), boff.data(), glist.data(), gpts.data(), n, B.data());
+    for (uint64_t q = 0; q < nl_max * G1M_WIN; ++q) g1m_fold_lane(q, meta.data(), B.data(), Wv.data());
+  }
   mark(2);
   // stage 3 as the device runs it: the chunks, then the (-g1, S) lane as the last column
+  // (then the large messages' Miller values, as the device's k_g1m_miller columns)
   const uint64_t nch = g_rlcb_chunks ? g_rlcb_chunks : rlcb_chunk_count(n, g_rlcb_slots);
-  std::vector<uint32_t> F(144 * (nch + 1));
+  const uint64_t cols = nch + 1 + nl_max;
+  std::vector<uint32_t> F(144 * cols);
   for (uint64_t c = 0; c < nch; ++c)
     rlcb_chunk_lane(host_f12_slot(), c, n, status, msg_idx, rpk.data(), H.data(), n_msgs, nullptr, F.data(), nch,
-                    nch + 1);
+                    cols);
+  for (uint64_t L = 0; L < nl_max; ++L)
+    g1m_miller_lane(host_f12_slot(), L, meta.data(), lmsg.data(), Wv.data(), H.data(), n_msgs, nullptr, F.data(),
+                    nch + 1 + L, cols);
   mark(3);  // the (-g1, S) lane is counted with the product and the verdict (stage 4 of counts6)
-  rlcb_sfactor_lane(host_f12_slot(), Wc.data(), F.data(), nch + 1, nch);
-  uint64_t cur = nch + 1;
+  rlcb_sfactor_lane(host_f12_slot(), Wc.data(), F.data(), cols, nch);
+  uint64_t cur = cols;
   while (cur > 1) {
     const uint64_t nxt = (cur + RLCB_FAN - 1) / RLCB_FAN;
     std::vector<uint32_t> G(144 * nxt);
@@ -571,7 +607,8 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
     final_exponentiation(e, f);
     pass = fp12_is_one(e);
   }
-  for (uint64_t i = 0; i < n; ++i) rlcb_mark_lane(i, n, pass, status, pts.data(), sc.data(), rsig.data());
+  for (uint64_t i = 0; i < n; ++i)
+    rlcb_mark_lane(i, n, pass, status, pts.data(), sc.data(), rsig.data(), gpos, gpts.data(), gsc.data(), rpk.data());
   *passed = pass ? 1 : 0;
   mark(4);
   const uint64_t n_win = (n + RLC_W - 1) / RLC_W;
@@ -599,4 +636,9 @@ extern "C" void ht_fp_inv(const uint32_t* x12, int gcd, uint32_t* out12) {
 
 extern "C" void ht_rlcb_set_slots(uint64_t slots) { g_rlcb_slots = slots; }
 extern "C" void ht_rlcb_set_chunks(uint64_t nch) { g_rlcb_chunks = nch; }
+extern "C" uint32_t ht_rlcb_set_g1_min(uint32_t min) {
+  const uint32_t o = g_g1m_min;
+  g_g1m_min = min;
+  return o;
+}
 extern "C" uint64_t ht_rlcb_chunk_count(uint64_t n, uint64_t slots) { return rlcb_chunk_count(n, slots); }

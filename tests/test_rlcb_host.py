@@ -43,7 +43,7 @@ def test_msm_matches_naive_sum():
     assert out.raw == bls.g2_compress(want)
 
 
-def rlcb(L, pks, msgs, sigs, seed=SEED):
+def rlcb(L, pks, msgs, sigs, seed=SEED, counts=None):
     table, idx = message_table(msgs)
     n = len(pks)
     offs = (ctypes.c_uint64 * (len(table) + 1))()
@@ -56,7 +56,7 @@ def rlcb(L, pks, msgs, sigs, seed=SEED):
     passed = ctypes.c_int32(-1)
     arr = (ctypes.c_uint32 * max(n, 1))(*idx)
     rc = L.ht_rlcb_verify(b"".join(pks), b"".join(sigs), arr, ctypes.c_uint64(n), b"".join(table), offs,
-                          ctypes.c_uint64(len(table)), seed, st, ctypes.byref(passed), None)
+                          ctypes.c_uint64(len(table)), seed, st, ctypes.byref(passed), counts)
     assert rc == 0
     return [st[i] for i in range(n)], passed.value
 
@@ -127,3 +127,63 @@ def test_rlcb_uneven_chunks_same_verdicts():
         assert passed == 0 and got == [0] * 5 + [3, 3] + [0] * 63
     finally:
         L.ht_rlcb_set_chunks(ctypes.c_uint64(0))
+
+
+def committee_batch(L, sizes, seed, shuffle=False):
+    """Committee roots: sizes[m] partials (distinct keys) all signing root m; items grouped by root unless shuffled."""
+    rng = random.Random(seed)
+    sign, to_pk = host_sign(L), host_pk(L)
+    roots = [rng.randbytes(32) for _ in sizes]
+    items = [(m, rng.randrange(1, bls.R).to_bytes(32, "big")) for m, k in enumerate(sizes) for _ in range(k)]
+    if shuffle:
+        rng.shuffle(items)
+    pks = [to_pk(sk) for _, sk in items]
+    msgs = [roots[m] for m, _ in items]
+    sigs = [sign(sk, roots[m]) for m, sk in items]
+    return pks, msgs, sigs
+
+
+def _with_g1_min(L, k, fn):
+    L.ht_rlcb_set_g1_min.restype = ctypes.c_uint32
+    old = L.ht_rlcb_set_g1_min(ctypes.c_uint32(k))
+    try:
+        return fn()
+    finally:
+        L.ht_rlcb_set_g1_min(ctypes.c_uint32(old))
+
+
+def test_rlcb_g1_msm_committee_roots():
+    """g1msm.h: roots with >= min items get one bucket-method sum of [r_i] pk_i and one Miller loop (roots 0 and 1
+    here), the small root keeps the per-item path; the batch passes with and without it, items in any order."""
+    L = lib()
+    for shuffle in (False, True):
+        pks, msgs, sigs = committee_batch(L, [40, 24, 3], seed=31, shuffle=shuffle)
+        got, passed = _with_g1_min(L, 16, lambda: rlcb(L, pks, msgs, sigs))
+        assert got == [0] * 67 and passed == 1
+        got, passed = _with_g1_min(L, 0, lambda: rlcb(L, pks, msgs, sigs))
+        assert got == [0] * 67 and passed == 1
+    # the path is taken: stage 1 skips the 64 large-root items' Shamir multiplications (~600 products each), the
+    # chunks pair only the small root
+    on, off = (ctypes.c_uint64 * 6)(), (ctypes.c_uint64 * 6)()
+    _with_g1_min(L, 16, lambda: rlcb(L, pks, msgs, sigs, counts=on))
+    _with_g1_min(L, 0, lambda: rlcb(L, pks, msgs, sigs, counts=off))
+    assert off[0] - on[0] > 64 * 500 and on[3] < off[3]
+
+
+def test_rlcb_g1_msm_failures_fall_back_exactly():
+    """Invalid partials inside large roots: a swapped pair (only the scalars catch it), a wrong key, a flipped
+    signature bit (final status in stage 1, zero scalars in its slot).  The batch check fails, the windows take
+    [r_i] pk_i from the slots (rlcb_mark_lane) and decide each item exactly as with the G1 MSM off."""
+    L = lib()
+    pks, msgs, sigs = committee_batch(L, [40, 24, 3], seed=32)
+    sigs[5], sigs[6] = sigs[6], sigs[5]
+    pks[45] = pks[46]
+    b = bytearray(sigs[50])
+    b[40] ^= 0x04
+    sigs[50] = bytes(b)
+    got, passed = _with_g1_min(L, 16, lambda: rlcb(L, pks, msgs, sigs))
+    ref, ref_passed = _with_g1_min(L, 0, lambda: rlcb(L, pks, msgs, sigs))
+    assert passed == ref_passed == 0
+    assert got == ref
+    assert got[5] == got[6] == got[45] == 3 and got[50] in (2, 3)
+    assert [g for i, g in enumerate(got) if i not in (5, 6, 45, 50)] == [0] * 63
