@@ -21,22 +21,32 @@ TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 NT_AMDGPU_METADATA = 32
 
 
-def code_object(path: str, target: str = TARGET) -> bytes:
-    """The code object of `target` inside the library's offload bundle."""
+def code_objects(path: str, target: str = TARGET):
+    """The code objects of `target` inside the library's offload bundles (one per translation unit: hipbls.hip and
+    the eight-lane latency path verify_lat.hip)."""
     with open(path, "rb") as f:
         d = f.read()
+    out = []
     i = d.find(BUNDLE_MAGIC)
-    if i < 0:
-        raise ValueError("%s: no clang offload bundle (compressed bundles are not expected here)" % path)
-    (n,) = struct.unpack_from("<Q", d, i + 24)
-    p = i + 32
-    for _ in range(n):
-        off, size, idlen = struct.unpack_from("<QQQ", d, p)
-        tid = d[p + 24:p + 24 + idlen].decode()
-        p += 24 + idlen
-        if tid == target:
-            return d[i + off:i + off + size]
-    raise ValueError("%s: no %s code object" % (path, target))
+    while i >= 0:
+        (n,) = struct.unpack_from("<Q", d, i + 24)
+        p = i + 32
+        for _ in range(n):
+            off, size, idlen = struct.unpack_from("<QQQ", d, p)
+            tid = d[p + 24:p + 24 + idlen].decode()
+            p += 24 + idlen
+            if tid == target:
+                out.append(d[i + off:i + off + size])
+        i = d.find(BUNDLE_MAGIC, i + 32)
+    if not out:
+        raise ValueError("%s: no clang offload bundle with a %s code object (compressed bundles are not expected "
+                         "here)" % (path, target))
+    return out
+
+
+def code_object(path: str, target: str = TARGET) -> bytes:
+    """The first code object of `target` (the main translation unit's)."""
+    return code_objects(path, target)[0]
 
 
 def _notes(elf: bytes):
@@ -63,26 +73,34 @@ def _notes(elf: bytes):
 
 
 def kernels(path: str):
-    """{kernel symbol name: metadata dict} from the library's gfx950 code object."""
+    """{kernel symbol name: metadata dict} over every gfx950 code object of the library."""
     import msgpack
-    for name, ntype, desc in _notes(code_object(path)):
-        if name == "AMDGPU" and ntype == NT_AMDGPU_METADATA:
-            md = msgpack.unpackb(desc, raw=False)
-            return {k[".name"]: k for k in md["amdhsa.kernels"]}
-    raise ValueError("%s: no AMDGPU metadata note" % path)
+    out = {}
+    for co in code_objects(path):
+        found = False
+        for name, ntype, desc in _notes(co):
+            if name == "AMDGPU" and ntype == NT_AMDGPU_METADATA:
+                md = msgpack.unpackb(desc, raw=False)
+                out.update({k[".name"]: k for k in md["amdhsa.kernels"]})
+                found = True
+        if not found:
+            raise ValueError("%s: a code object without an AMDGPU metadata note" % path)
+    return out
 
 
 def short_name(mangled: str) -> str:
-    """k_verify_fused from _ZN12_GLOBAL__N_114k_verify_fusedEPKh... (anonymous-namespace kernels)."""
-    s = mangled
-    if s.startswith("_ZN12_GLOBAL__N_1"):
-        s = s[len("_ZN12_GLOBAL__N_1"):]
+    """The last component of a nested name: k_verify_fused from _ZN12_GLOBAL__N_114k_verify_fusedEPKh...
+    (anonymous-namespace kernels), k_verify_pair_lq8 from _ZN8bls_fp2p17k_verify_pair_lq8EPKjmPi."""
+    if not mangled.startswith("_ZN"):
+        return mangled
+    s, last = mangled[3:], None
+    while s and s[0].isdigit():
         j = 0
         while j < len(s) and s[j].isdigit():
             j += 1
-        if j:
-            return s[j:j + int(s[:j])]
-    return mangled
+        k = int(s[:j])
+        last, s = s[j:j + k], s[j + k:]
+    return last or mangled
 
 
 def resource_table(path: str):

@@ -255,6 +255,27 @@ __device__ __attribute__((used, noinline)) static void bls_fp_asm_routines() {
                ".p2align 6\n.type bls_fp2_sqr_rt,@function\nbls_fp2_sqr_rt:\n\t" BLS_FP2_SQR_ASM_BODY
                "\n\ts_setpc_b64 s[30:31]\n");
 }
+#if BLS_FP2_PAIR
+// The split-Fp2 build (verify_lat.hip): an Fp2 value is held in full on lanes l and l ^ 4, each computes one output
+// coefficient of a product or square (tools/gen_fp_asm.py gen_fp2_mul_half / gen_fp2_sqr_half), then they swap.
+__device__ __attribute__((used, noinline)) static void bls_fp2_half_routines() {
+  asm volatile("s_endpgm\n.p2align 6\n.type bls_fp2_mul_half_rt,@function\nbls_fp2_mul_half_rt:\n\t"
+               BLS_FP2_MUL_HALF_ASM_BODY "\n\ts_setpc_b64 s[30:31]\n"
+               ".p2align 6\n.type bls_fp2_sqr_half_rt,@function\nbls_fp2_sqr_half_rt:\n\t" BLS_FP2_SQR_HALF_ASM_BODY
+               "\n\ts_setpc_b64 s[30:31]\n");
+}
+// This lane's half: ~0 on lanes 4-7 of each group of eight (they form c1), 0 on lanes 0-3 (c0).
+__device__ __forceinline__ uint32_t fp2p_mask() {
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  return (lane & 4u) ? ~0u : 0u;
+}
+// The value of lane l ^ 4 (lanes 0-3 <-> 4-7 of each group of eight): row_shl:4 into banks 0 and 2 (lanes 0-3,
+// 8-11 read 4-7, 12-15), row_shr:4 into banks 1 and 3.  All eight lanes must be active.
+__device__ __forceinline__ uint32_t fp2p_xchg(uint32_t v) {
+  const int a = __builtin_amdgcn_update_dpp((int)v, (int)v, 0x104, 0xF, 0x5, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp(a, (int)v, 0x114, 0xF, 0xA, false);
+}
+#endif
 #define BLS_ASM_CALL(fn)                                                                           \
   "s_getpc_b64 s[16:17]\n\ts_add_u32 s16, s16, " fn "@rel32@lo+4\n\ts_addc_u32 s17, s17, " fn \
   "@rel32@hi+12\n\ts_swappc_b64 s[30:31], s[16:17]\n\t"

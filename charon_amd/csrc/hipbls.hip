@@ -42,6 +42,13 @@
 
 #include "kernels.h"
 
+// The eight-lane latency path (verify_lat.hip, its own translation unit: BLS_FP2_PAIR build in namespace bls_fp2p).
+namespace bls_fp2p {
+__global__ void k_verify_prep8(const uint8_t* pks, const uint8_t* msgs, const uint64_t* offs, const uint8_t* sigs,
+                               uint64_t n, uint32_t* ws, int32_t* status);
+__global__ void k_verify_pair_lq8(const uint32_t* ws, uint64_t n, int32_t* status);
+}  // namespace bls_fp2p
+
 namespace {
 
 // ============================================================================ device contexts
@@ -488,7 +495,7 @@ int timed(Context& c, const char* name, hipStream_t s, Launch launch) {
 // uses two lanes, so it wins while the batch leaves lanes idle: one wave per SIMD is 64 x 1024 lanes on MI355X.
 int initial_pair_mode() {
   const char* pm = getenv("HIPBLS_PAIR_MODE");
-  if (pm && pm[0] >= '0' && pm[0] <= '3' && pm[1] == 0) return pm[0] - '0';
+  if (pm && pm[0] >= '0' && pm[0] <= '4' && pm[1] == 0) return pm[0] - '0';
   return HIPBLS_PAIR_AUTO;
 }
 std::atomic<int> g_pair_mode{initial_pair_mode()};
@@ -502,16 +509,27 @@ constexpr uint64_t kLg2MaxWindows = 32768;   // auto: RLC sub-batches up to this
 #endif
 constexpr uint64_t kLq4MaxVerify = BLS_LQ4_MAX_VERIFY;  // auto: Verify-shaped batches up to this many take quads
 
+#ifndef BLS_LQ8_MAX_VERIFY
+#define BLS_LQ8_MAX_VERIFY 4096  // scripts/latency_sweep.py: octets 14.1 vs quads 17.7 ms at 4,096, 19.5 vs 18.8 at 8,192
+#endif
+constexpr uint64_t kLq8MaxVerify = BLS_LQ8_MAX_VERIFY;  // auto: Verify batches up to this many take octets
+
 bool use_pairs(uint64_t units, uint64_t auto_max) {
   const int mode = g_pair_mode.load();
   if (mode == HIPBLS_PAIR_SINGLE) return false;
-  if (mode == HIPBLS_PAIR_LANES || mode == HIPBLS_PAIR_QUADS) return true;
+  if (mode == HIPBLS_PAIR_LANES || mode == HIPBLS_PAIR_QUADS || mode == HIPBLS_PAIR_OCTETS) return true;
   return units <= auto_max;
 }
 bool use_quads(uint64_t n) {
   const int mode = g_pair_mode.load();
-  if (mode == HIPBLS_PAIR_QUADS) return true;
+  if (mode == HIPBLS_PAIR_QUADS || mode == HIPBLS_PAIR_OCTETS) return true;
   return mode == HIPBLS_PAIR_AUTO && n <= kLq4MaxVerify;
+}
+// Verify only (the drop-in latency path, verify_lat.hip); sigagg's check and the RLC stages keep quads / pairs.
+bool use_octets(uint64_t n) {
+  const int mode = g_pair_mode.load();
+  if (mode == HIPBLS_PAIR_OCTETS) return true;
+  return mode == HIPBLS_PAIR_AUTO && n <= kLq8MaxVerify;
 }
 
 // Verify: fused (one lane per item) or prep + lane-pair check; `ws` is the caller's SoA workspace for the latter
@@ -525,6 +543,17 @@ int launch_verify(Context& c, const uint8_t* d_pks, const uint8_t* d_msgs, const
                          d_sigs, n, d_status);
     });
   HIP_TRY(ws.ensure(n * 120 * 4));
+  if (use_octets(n)) {
+    const unsigned g8 = (unsigned)grid_for(8 * n);
+    int rc = timed(c, "verify_prep8", s, [&] {
+      hipLaunchKernelGGL(bls_fp2p::k_verify_prep8, dim3(2 * g8), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs, n,
+                         (uint32_t*)ws.p, d_status);
+    });
+    if (rc) return rc;
+    return timed(c, "verify_pair_lq8", s, [&] {
+      hipLaunchKernelGGL(bls_fp2p::k_verify_pair_lq8, dim3(g8), dim3(kBlock), 0, s, (const uint32_t*)ws.p, n, d_status);
+    });
+  }
   int rc = timed(c, "verify_prep", s, [&] {
     const int pair_hash = n <= kPairHashMaxVerify ? 1 : 0;
     hipLaunchKernelGGL(k_verify_prep, dim3((unsigned)((pair_hash ? 3 : 2) * grid_for(n))), dim3(kBlock), 0, s, d_pks,
@@ -1954,7 +1983,8 @@ int hipbls_rlc_batch_stats(uint64_t* attempted, uint64_t* passed, int32_t* last)
 }
 
 int hipbls_set_pair_mode(int mode) {
-  if (mode != HIPBLS_PAIR_AUTO && mode != HIPBLS_PAIR_SINGLE && mode != HIPBLS_PAIR_LANES && mode != HIPBLS_PAIR_QUADS)
+  if (mode != HIPBLS_PAIR_AUTO && mode != HIPBLS_PAIR_SINGLE && mode != HIPBLS_PAIR_LANES && mode != HIPBLS_PAIR_QUADS &&
+      mode != HIPBLS_PAIR_OCTETS)
     return arg_err("unknown pair mode");
   return g_pair_mode.exchange(mode);
 }

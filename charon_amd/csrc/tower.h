@@ -53,10 +53,22 @@ BLS_HD BLS_INLINE void fp2_conj(fp2& r, const fp2& a) {
   r.c0 = a.c0;
   fp_neg(r.c1, a.c1);
 }
+#if defined(__HIP_DEVICE_COMPILE__) && BLS_FP2_PAIR
+__device__ __forceinline__ void fp2p_join(fp2& r, const u32x12& c, uint32_t hm);
+BLS_HD BLS_INLINE void fp2_mul_fp(fp2& r, const fp2& a, const fp& b) {  // one Fp product per lane (split-Fp2 build)
+  const uint32_t hm = fp2p_mask();
+  fp x, y;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) x.v[j] = (hm & a.c1.v[j]) | (~hm & a.c0.v[j]);
+  fp_mul(y, x, b);
+  fp2p_join(r, fp_to_vec(y), hm);
+}
+#else
 BLS_HD BLS_INLINE void fp2_mul_fp(fp2& r, const fp2& a, const fp& b) {
   fp_mul(r.c0, a.c0, b);
   fp_mul(r.c1, a.c1, b);
 }
+#endif
 // (a0 + a1 u)(1 + u) = (a0 - a1) + (a0 + a1) u
 BLS_HD BLS_INLINE void fp2_mul_xi(fp2& r, const fp2& a) {
   fp t;
@@ -142,7 +154,42 @@ BLS_HD BLS_INLINE void fp12_conj(fp12& r, const fp12& a) {
 // Frobenius x -> x^(p^j), j in {1,2,3}
 // Granger-Scott squaring for elements of the cyclotomic subgroup
 
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && BLS_FP2_PAIR
+// Split-Fp2 build (field.h fp2p_*): this lane forms one coefficient (its half of gen_fp2_mul's two sums of products),
+// the partner lane l ^ 4 the other, and one exchange gives both lanes the full, canonical product.
+__device__ __forceinline__ void fp2p_join(fp2& r, const u32x12& c, uint32_t hm) {
+  fp mine, other;
+  fp_from_vec(mine, c);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) other.v[j] = fp2p_xchg(mine.v[j]);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    r.c0.v[j] = (hm & other.v[j]) | (~hm & mine.v[j]);
+    r.c1.v[j] = (hm & mine.v[j]) | (~hm & other.v[j]);
+  }
+}
+BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
+  u32x12 a0 = fp_to_vec(a.c0), a1 = fp_to_vec(a.c1), b0 = fp_to_vec(b.c0), b1 = fp_to_vec(b.c1), c;
+  uint32_t hm = fp2p_mask();
+  const uint32_t h = hm;
+  asm volatile(BLS_ASM_CALL("bls_fp2_mul_half_rt")
+               : "+{v[0:11]}"(a0), "+{v[12:23]}"(a1), "+{v[24:35]}"(b0), "+{v[36:47]}"(b1), "={v[52:63]}"(c),
+                 "+{v76}"(hm)
+               :
+               : BLS_FP2_MUL_HALF_ASM_CLOBBERS, "s30", "s31", "scc");
+  fp2p_join(r, c, h);
+}
+BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
+  u32x12 a0 = fp_to_vec(a.c0), a1 = fp_to_vec(a.c1), c;
+  uint32_t hm = fp2p_mask();
+  const uint32_t h = hm;
+  asm volatile(BLS_ASM_CALL("bls_fp2_sqr_half_rt")
+               : "+{v[0:11]}"(a0), "+{v[12:23]}"(a1), "={v[24:35]}"(c), "+{v76}"(hm)
+               :
+               : BLS_FP2_SQR_HALF_ASM_CLOBBERS, "s30", "s31", "scc");
+  fp2p_join(r, c, h);
+}
+#elif defined(__HIP_DEVICE_COMPILE__)
 // Device: one asm routine (tools/gen_fp_asm.py gen_fp2_mul): each coefficient is a single Montgomery reduction of
 // a sum of two products, c1 = (a0 b1 + a1 b0)/R and c0 = (a0 b0 + a1 (2p - b1))/R -- no Fp additions and two final
 // subtractions instead of Karatsuba's three reduced products, three subtractions and two sums.  Operands may be
@@ -181,7 +228,9 @@ BLS_HD BLS_INLINE void fp2_sqr_c(fp2& r, const fp2& a) {
   fp_mul(r.c0, s, d);
   fp_add(r.c1, m, m);
 }
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && BLS_FP2_PAIR
+// (split-Fp2 fp2_sqr above)
+#elif defined(__HIP_DEVICE_COMPILE__)
 // Device: one asm routine (tools/gen_fp_asm.py gen_fp2_sqr): c0 = (a0+a1)(a0+p-a1)/R, c1 = a0 (2 a1)/R with the three
 // operand sums unreduced inside it.
 BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
@@ -199,7 +248,11 @@ BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) { fp2_sqr_c(r, a); }
 // The cyclotomic squaring's Fp2 squarings use the three-product C form: inside the inlined exponentiation loop the
 // routine's 64 pinned registers cost more spills than it saves (op_probe: fp12_cyc_exp_xabs 5.86M -> 5.64M cycles).
 #ifndef BLS_CYC_FP2_SQR
+#if BLS_FP2_PAIR
+#define BLS_CYC_FP2_SQR fp2_sqr
+#else
 #define BLS_CYC_FP2_SQR fp2_sqr_c
+#endif
 #endif
 BLS_HD BLS_CALL void fp2_inv(fp2& r, const fp2& a_in) {
   const fp2 a = a_in;

@@ -23,7 +23,7 @@ R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 OK, ERR_PUBKEY, ERR_SIGNATURE, ERR_VERIFY, ERR_SECRET, ERR_COMBINE, ERR_ZERO_SIG = 0, 1, 2, 3, 4, 5, 6
 INFINITY_G2 = b"\xc0" + bytes(95)  # compressed point at infinity (the empty Aggregate, herumi.go:220-242)
 ERR_ARG, ERR_DEVICE = 16, 17
-PAIR_AUTO, PAIR_SINGLE, PAIR_LANES, PAIR_QUADS = 0, 1, 2, 3  # hipbls_set_pair_mode: pairing-check layout (hipbls.h)
+PAIR_AUTO, PAIR_SINGLE, PAIR_LANES, PAIR_QUADS, PAIR_OCTETS = 0, 1, 2, 3, 4  # hipbls_set_pair_mode (hipbls.h)
 RLC_AUTO, RLC_WINDOWS, RLC_BATCH = 0, 1, 2     # hipbls_rlc_set_mode: batch-wide check policy (include/hipbls.h)
 
 # tbls/herumi.go error strings by status code
@@ -605,10 +605,10 @@ class HipBLS:
     # ---------------------------------------------------------------- pairing-check layout
     def set_pair_mode(self, mode: int) -> int:
         """PAIR_AUTO / PAIR_SINGLE (one lane per check) / PAIR_LANES (a lane pair per check) / PAIR_QUADS (four
-        lanes per Verify-shaped check, each Miller loop split across a pair); returns the
-        previous mode.  Results are identical in every mode; only latency and lane use differ."""
+        lanes per Verify-shaped check, each Miller loop split across a pair) / PAIR_OCTETS (eight lanes per Verify:
+        quads with every Fp2 product split across twin lanes, the n = 1 latency path); returns the previous mode.  Results are identical in every mode; only latency and lane use differ."""
         rc = self.lib.hipbls_set_pair_mode(mode)
-        if rc not in (PAIR_AUTO, PAIR_SINGLE, PAIR_LANES, PAIR_QUADS):
+        if rc not in (PAIR_AUTO, PAIR_SINGLE, PAIR_LANES, PAIR_QUADS, PAIR_OCTETS):
             _check(rc, self.lib)
         return rc
 

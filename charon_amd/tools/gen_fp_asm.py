@@ -477,6 +477,90 @@ def gen_fp2_mul():
     return out
 
 
+# Lane-pair halves of the Fp2 product and square (the split-Fp2 build, BLS_FP2_PAIR: an Fp2 value is held in full on
+# two lanes and each lane computes ONE output coefficient, then the lanes swap; field.h / tower.h).  The lane's half
+# arrives as a mask in v76 (0: c0, ~0: c1); the operand choice is a v_bfi_b32 per word, so both lanes run the same
+# stream.  Same operand ranges and canonical output as gen_fp2_mul / gen_fp2_sqr.
+# Product half: a0 = v[0:11], a1 = v[12:23] (preserved), b0 = v[24:35], b1 = v[36:47] (clobbered); the half
+#   c0 = (a0 b0 + a1 (2p - b1))/R or c1 = (a0 b1 + a1 b0)/R -> v[52:63]; v48-v51, v64-v75, s16-s28, vcc clobbered.
+# Square half: a0 = v[0:11], a1 = v[12:23] (preserved); c0 = (a0 + a1)(a0 + p - a1)/R or c1 = a0 (2 a1)/R ->
+#   v[24:35]; v36-v75, s16-s28, vcc clobbered.
+FP2H_MASK, FP2H_OUT, FP2HS_OUT = 76, 52, 24
+
+
+def _final_sub(w, C, PR, T, mask):
+    """C <- C - p when that does not borrow (C < 2p -> canonical); PR holds p, T is scratch, mask a VGPR."""
+    w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), PR(0)))
+    for j in range(1, N32):
+        w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (T(j), C(j), PR(j)))
+    w("v_subb_co_u32_e64 %s, vcc, 0, 0, vcc" % mask)
+    for j in range(N32):
+        w("v_bfi_b32 %s, %s, %s, %s" % (C(j), mask, C(j), T(j)))
+
+
+def gen_fp2_mul_half():
+    PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
+    PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    P2L = [((2 * P) >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    V = lambda base: (lambda j: "v%d" % (base + j))
+    A0, A1, B0, B1, C, T = V(0), V(12), V(24), V(36), V(FP2H_OUT), V(64)
+    HM = "v%d" % FP2H_MASK
+    out = []
+    w = out.append
+    for j in range(N32):
+        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
+    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    for j in range(N32):                               # 2p staged in C (one constant-bus operand per carry step)
+        w("v_mov_b32 %s, 0x%08x" % (C(j), P2L[j]))
+    w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), B1(0)))
+    for j in range(1, N32):                            # T <- 2p - b1 in (0, 2p]
+        w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (T(j), C(j), B1(j)))
+    for j in range(N32):                               # W = c1 ? b0 : 2p - b1 (over T)
+        w("v_bfi_b32 %s, %s, %s, %s" % (T(j), HM, B0(j), T(j)))
+    for j in range(N32):                               # Y = c1 ? b1 : b0 (over b1)
+        w("v_bfi_b32 %s, %s, %s, %s" % (B1(j), HM, B1(j), B0(j)))
+    _gen_sop(w, A0, B1, A1, T, C)                      # (a0 Y + a1 W)/R, raw (< 2p), over C
+    for j in range(N32):                               # p over the dead b0
+        w("v_mov_b32 %s, s%d" % (B0(j), 16 + j))
+    _final_sub(w, C, B0, T, "v48")
+    return out
+
+
+def gen_fp2_sqr_half():
+    PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
+    PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    V = lambda base: (lambda j: "v%d" % (base + j))
+    A0, A1, X, Y, M, T = V(0), V(12), V(FP2HS_OUT), V(36), V(52), V(64)
+    HM = "v%d" % FP2H_MASK
+    out = []
+    w = out.append
+    for j in range(N32):
+        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
+    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    for j in range(N32):                               # p staged in X
+        w("v_mov_b32 %s, s%d" % (X(j), 16 + j))
+    w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (Y(0), X(0), A1(0)))
+    for j in range(1, N32):                            # Y <- p - a1
+        w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (Y(j), X(j), A1(j)))
+    w("v_add_co_u32_e32 %s, vcc, %s, %s" % (Y(0), Y(0), A0(0)))
+    for j in range(1, N32):                            # Y <- a0 + p - a1 (d)
+        w("v_addc_co_u32_e32 %s, vcc, %s, %s, vcc" % (Y(j), Y(j), A0(j)))
+    w("v_add_co_u32_e32 %s, vcc, %s, %s" % (X(0), A0(0), A1(0)))
+    for j in range(1, N32):                            # X <- a0 + a1 (s)
+        w("v_addc_co_u32_e32 %s, vcc, %s, %s, vcc" % (X(j), A0(j), A1(j)))
+    w("v_add_co_u32_e32 %s, vcc, %s, %s" % (T(0), A1(0), A1(0)))
+    for j in range(1, N32):                            # T <- 2 a1
+        w("v_addc_co_u32_e32 %s, vcc, %s, %s, vcc" % (T(j), A1(j), A1(j)))
+    for j in range(N32):                               # X = c1 ? a0 : s,  Y = c1 ? 2 a1 : d
+        w("v_bfi_b32 %s, %s, %s, %s" % (X(j), HM, A0(j), X(j)))
+        w("v_bfi_b32 %s, %s, %s, %s" % (Y(j), HM, T(j), Y(j)))
+    _gen_prod(w, X, Y, M, R=X)                         # X Y / R, raw (< 2p), over X
+    for j in range(N32):                               # p for the final subtraction
+        w("v_mov_b32 %s, s%d" % (T(j), 16 + j))
+    _final_sub(w, X, T, M, "v48")
+    return out
+
+
 # ---------------------------------------------------------------- modular add / sub / neg
 # One asm block each, operands allocated by the compiler (positional: outputs r = %0-%11, t = %12-%23,
 # m = %24; inputs a = %25-%36, then b = %37-%48 and p = %49-%60, or p = %37-%48 for neg).  One VCC carry chain
@@ -733,6 +817,11 @@ def emit_header(path, bodies, extra=()):
     lines.append("#define BLS_FP2_MUL_ASM_CLOBBERS %s" % clob2)
     clob3 = ", ".join('"v%d"' % r for r in range(48, 64)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
     lines.append("#define BLS_FP2_SQR_ASM_CLOBBERS %s" % clob3)
+    clob4 = ", ".join('"v%d"' % r for r in list(range(48, 52)) + list(range(64, 76))) + ', "vcc", ' + \
+        ", ".join('"s%d"' % r for r in range(16, 29))
+    lines.append("#define BLS_FP2_MUL_HALF_ASM_CLOBBERS %s" % clob4)
+    clob5 = ", ".join('"v%d"' % r for r in range(36, 76)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
+    lines.append("#define BLS_FP2_SQR_HALF_ASM_CLOBBERS %s" % clob5)
     for name, body in extra:
         lines.append("")
         lines.append("// %s: %d instructions, positional operands (see tools/gen_fp_asm.py)" % (name, len(body)))
@@ -751,7 +840,9 @@ def main():
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "fp_asm_gfx950.h")
     fp2 = gen_fp2_mul()
     fp2s = gen_fp2_sqr()
-    emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul), ("BLS_FP2_MUL_ASM_BODY", fp2), ("BLS_FP2_SQR_ASM_BODY", fp2s)],
+    emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul), ("BLS_FP2_MUL_ASM_BODY", fp2), ("BLS_FP2_SQR_ASM_BODY", fp2s),
+                       ("BLS_FP2_MUL_HALF_ASM_BODY", gen_fp2_mul_half()),
+                       ("BLS_FP2_SQR_HALF_ASM_BODY", gen_fp2_sqr_half())],
                 extra=[("BLS_FP_ADD_ASM", gen_add()), ("BLS_FP_SUB_ASM", gen_sub()), ("BLS_FP_NEG_ASM", gen_sub(neg=True)),
                        ("BLS_FP_ADD_LAZY_ASM", gen_add_lazy()), ("BLS_FP_SUB_LAZY_ASM", gen_sub_lazy())])
     print("wrote %s: %d instructions" % (path, len(mul)))

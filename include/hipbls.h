@@ -93,12 +93,15 @@ int hipbls_set_timing(int enabled);
 /* Pairing-check layout.  HIPBLS_PAIR_SINGLE: one lane per check.  HIPBLS_PAIR_LANES: a lane pair per check (the
  * two Miller loops side by side, the final exponentiation split across the pair; about half the latency, twice
  * the lanes).  HIPBLS_PAIR_QUADS: four lanes per Verify-shaped check (each Miller loop split across a lane pair,
- * the two pairs side by side; RLC windows keep lane pairs).  HIPBLS_PAIR_AUTO (default): the widest layout the
- * batch leaves lanes for (Verify: quads up to the quad limit, then pairs up to 32,768 items; RLC sub-batches up to
- * 32,768 windows, every RLC fallback list and FastAggregateVerify on pairs).  Results are identical in every mode.
- * Returns the previous mode, or HIPBLS_ERR_ARG for an unknown one.  The environment variable HIPBLS_PAIR_MODE
- * (0/1/2/3) sets the initial mode. */
-enum { HIPBLS_PAIR_AUTO = 0, HIPBLS_PAIR_SINGLE = 1, HIPBLS_PAIR_LANES = 2, HIPBLS_PAIR_QUADS = 3 };
+ * the two pairs side by side; RLC windows keep lane pairs).  HIPBLS_PAIR_OCTETS: eight lanes per Verify (the quad
+ * layout with every Fp2 product and square split across twin lanes, charon_amd/csrc/verify_lat.hip: the drop-in
+ * n = 1 latency path; other checks as QUADS).  HIPBLS_PAIR_AUTO (default): the widest layout the batch leaves
+ * lanes for (Verify: octets up to 4,096 items, quads up to the quad limit, then pairs up to 32,768 items; RLC
+ * sub-batches up to 32,768 windows, every RLC fallback list and FastAggregateVerify on pairs).  Results are
+ * identical in every mode.  Returns the previous mode, or HIPBLS_ERR_ARG for an unknown one.  The environment
+ * variable HIPBLS_PAIR_MODE (0-4) sets the initial mode. */
+enum { HIPBLS_PAIR_AUTO = 0, HIPBLS_PAIR_SINGLE = 1, HIPBLS_PAIR_LANES = 2, HIPBLS_PAIR_QUADS = 3,
+       HIPBLS_PAIR_OCTETS = 4 };
 int hipbls_set_pair_mode(int mode);
 
 /* ------------------------------------------------ single-item Verify through the submission queue ---- */

@@ -155,3 +155,46 @@ def test_fp2_square_routine():
         c1 = _val([regs[g.FP2S_C1 + j] for j in range(12)])
         assert c0 == (a0 * a0 - a1 * a1) * R_INV % g.P, (t, hex(a0), hex(a1))
         assert c1 == 2 * a0 * a1 * R_INV % g.P, (t, hex(a0), hex(a1))
+
+
+@pytest.mark.parametrize("half", [0, 1])
+def test_fp2_product_half_routine(half):
+    """The split-Fp2 build's product half (BLS_FP2_MUL_HALF_ASM_BODY, gen_fp2_mul_half): with the lane mask in v76
+    (0 or ~0) the interpreted stream gives c0 = (a0 b0 - a1 b1)/R or c1 = (a0 b1 + a1 b0)/R mod p, canonical, on
+    canonical and unreduced operands in [0, 2p); a0, a1 come back unchanged."""
+    body = _macro_body("BLS_FP2_MUL_HALF_ASM_BODY")
+    assert body == g.gen_fp2_mul_half(), "fp_asm_gfx950.h is stale: rerun charon_amd/tools/gen_fp_asm.py"
+    cases = _cases(60, 61) + [g.P, g.P + 1, 2 * g.P - 1, 2 * g.P - 2, g.P + (1 << 300)]
+    rnd = random.Random(62 + half)
+    for t in range(250):
+        a0, a1, b0, b1 = (rnd.choice(cases) for _ in range(4))
+        regs = {g.FP2H_MASK: 0xFFFFFFFF if half else 0}
+        for base, x in ((0, a0), (12, a1), (24, b0), (36, b1)):
+            regs.update({base + j: v for j, v in enumerate(_limbs(x))})
+        g.emulate(body, None, None, regs)
+        c = _val([regs[g.FP2H_OUT + j] for j in range(12)])
+        want = (a0 * b1 + a1 * b0) if half else (a0 * b0 - a1 * b1)
+        assert c == want * R_INV % g.P, (t, hex(a0), hex(a1), hex(b0), hex(b1))
+        for base, x in ((0, a0), (12, a1)):
+            assert _val([regs[base + j] for j in range(12)]) == x
+
+
+@pytest.mark.parametrize("half", [0, 1])
+def test_fp2_square_half_routine(half):
+    """The split-Fp2 build's square half (BLS_FP2_SQR_HALF_ASM_BODY): c0 = (a0^2 - a1^2)/R or c1 = 2 a0 a1/R mod p,
+    canonical, on canonical operands with edges; a0, a1 come back unchanged."""
+    body = _macro_body("BLS_FP2_SQR_HALF_ASM_BODY")
+    assert body == g.gen_fp2_sqr_half(), "fp_asm_gfx950.h is stale: rerun charon_amd/tools/gen_fp_asm.py"
+    cases = _cases(60, 71)
+    rnd = random.Random(72 + half)
+    for t in range(250):
+        a0, a1 = rnd.choice(cases), rnd.choice(cases)
+        regs = {g.FP2H_MASK: 0xFFFFFFFF if half else 0}
+        regs.update({j: v for j, v in enumerate(_limbs(a0))})
+        regs.update({12 + j: v for j, v in enumerate(_limbs(a1))})
+        g.emulate(body, None, None, regs)
+        c = _val([regs[g.FP2HS_OUT + j] for j in range(12)])
+        want = 2 * a0 * a1 if half else a0 * a0 - a1 * a1
+        assert c == want * R_INV % g.P, (t, hex(a0), hex(a1))
+        for base, x in ((0, a0), (12, a1)):
+            assert _val([regs[base + j] for j in range(12)]) == x

@@ -93,6 +93,24 @@ def test_bench_rlcb_stage_counts_match():
     assert abs(cnt[3] / 4 - want["chunk_1run"]) / want["chunk_1run"] < 0.02
 
 
+def test_bench_rlcb_g1_counts_match():
+    """bench.RLCB_FPMUL's G1 MSM units (g1msm.h) at one committee root of 512 partials, as C4(ii): stage 1 without
+    the per-item Shamir multiplication, the G1 bucket + fold work per item (MSM stage with minus without the G1 MSM:
+    the G2 MSM is the same in both), one Miller pair for the root."""
+    import bench
+    from tests.test_rlcb_host import _with_g1_min, committee_batch, rlcb
+    L = lib()
+    pks, msgs, sigs = committee_batch(L, [512], seed=41)
+    on, off = (ctypes.c_uint64 * 6)(), (ctypes.c_uint64 * 6)()
+    assert _with_g1_min(L, 64, lambda: rlcb(L, pks, msgs, sigs, counts=on)) == ([0] * 512, 1)
+    assert _with_g1_min(L, 0, lambda: rlcb(L, pks, msgs, sigs, counts=off)) == ([0] * 512, 1)
+    want = bench.RLCB_FPMUL
+    assert abs(on[0] / 512 - want["item_g1slot"]) / want["item_g1slot"] < 0.02
+    assert abs(off[0] / 512 - want["item"]) / want["item"] < 0.02
+    assert abs((on[2] - off[2]) / 512 - want["g1msm_per_item_512"]) / want["g1msm_per_item_512"] < 0.03
+    assert abs(on[3] - want["g1miller_per_root"]) / want["g1miller_per_root"] < 0.02
+
+
 def test_bench_tagg_counts_match():
     """bench.TAGG_FPMUL (the C3 roofline's per-aggregate unit) against the host build of the fused sigagg stages over
     seeded 7-of-10 groups on ids 1..10 (the small-integer Lagrange path the bench's groups take)."""
