@@ -16,9 +16,9 @@
 //     kind 1 = [x] pk with b's digits (full additions); each kind has 128 bucket indices of which 120 are used, so a
 //     wave of bucket lanes never mixes the two addition formulas (256 per large message);
 //   * counting sort of the slots by bucket (histogram, scan, scatter), one lane per bucket sums its entries, one lane
-//     per (L, w) folds sum_d d (B_{0,w,d} + B_{1,w,d}) with running sums, and one lane pair per L combines the
-//     windows (R = sum_w [16^w] W_w) and runs the split Miller loop of (R, H(m)) -> a column of the product tree
-//     (the value 1 for an empty R).
+//     per (L, kind, w) folds sum_d d B_{kind,w,d} with running sums, and one lane group per L combines the windows
+//     (R = sum_w [16^w] (W_{0,w} + W_{1,w})) and runs the split Miller loop of (R, H(m)) -> a column of the product
+//     tree (the value 1 for an empty R).
 #pragma once
 #include "rlc.h"
 // included by rlcb.h after BLS_ATOMIC_ADD_U32
@@ -145,23 +145,22 @@ BLS_HD BLS_INLINE void g1m_bucket_lane(uint64_t b, const uint32_t* meta, const u
   aos_store<36>(B, b, &acc.x.v[0]);
 }
 
-// (L, w): sum_{d=1..15} d (B_{L,0,w,d} + B_{L,1,w,d}) by running sums (top digit first): R = sum_{d' >= d} B_d',
-// T = sum_d R
+// q = (L, kind, w): W_q = sum_{d=1..15} d B_{L,kind,w,d} by running sums (top digit first): R = sum_{d' >= d} B_d',
+// T = sum_d R -- 30 additions of latency per lane (a lane per kind, not one for both: the fold is latency-bound)
+constexpr uint32_t G1M_NFOLD = 2 * G1M_WIN;  // fold lanes (window sums) per large message
 BLS_HD BLS_INLINE void g1m_fold_lane(uint64_t q, const uint32_t* meta, const uint32_t* B, uint32_t* Wv) {
-  if (q >= (uint64_t)meta[0] * G1M_WIN) return;
-  const uint32_t L = (uint32_t)(q / G1M_WIN);
-  const int w = (int)(q % G1M_WIN);
+  if (q >= (uint64_t)meta[0] * G1M_NFOLD) return;
+  const uint32_t L = (uint32_t)(q / G1M_NFOLD);
+  const int kind = (int)((q / G1M_WIN) & 1), w = (int)(q % G1M_WIN);
   g1j R, T;
   jac_set_inf(R);
   jac_set_inf(T);
   for (uint32_t d = G1M_ND; d >= 1; --d) {
-    for (int kind = 0; kind < 2; ++kind) {
-      g1j b;
-      aos_load<36>(&b.x.v[0], B, g1m_bucket(L, kind, w, d));
-      g1j x = R, y;
-      jac_add(y, x, b);
-      R = y;
-    }
+    g1j b;
+    aos_load<36>(&b.x.v[0], B, g1m_bucket(L, kind, w, d));
+    g1j x = R, y;
+    jac_add(y, x, b);
+    R = y;
     g1j u = T, v;
     jac_add(v, u, R);
     T = v;
@@ -169,9 +168,17 @@ BLS_HD BLS_INLINE void g1m_fold_lane(uint64_t q, const uint32_t* meta, const uin
   aos_store<36>(Wv, q, &T.x.v[0]);
 }
 
+// window w of message L: W_{L,0,w} + W_{L,1,w}
+BLS_HD BLS_INLINE void g1m_window(g1j& W, const uint32_t* Wv, uint64_t L, int w) {
+  g1j a, b;
+  aos_load<36>(&a.x.v[0], Wv, L * G1M_NFOLD + (uint64_t)w);
+  aos_load<36>(&b.x.v[0], Wv, L * G1M_NFOLD + G1M_WIN + (uint64_t)w);
+  jac_add(W, a, b);
+}
+
 // R_L = sum_w [16^w] W_{L,w} (Horner from the top window)
 BLS_HD BLS_INLINE void g1m_combine(g1j& R, const uint32_t* Wv, uint64_t L) {
-  aos_load<36>(&R.x.v[0], Wv, L * G1M_WIN + (G1M_WIN - 1));
+  g1m_window(R, Wv, L, G1M_WIN - 1);
   for (int w = G1M_WIN - 2; w >= 0; --w) {
     for (int k = 0; k < G1M_BITS; ++k) {
       g1j t;
@@ -179,7 +186,7 @@ BLS_HD BLS_INLINE void g1m_combine(g1j& R, const uint32_t* Wv, uint64_t L) {
       R = t;
     }
     g1j t;
-    aos_load<36>(&t.x.v[0], Wv, L * G1M_WIN + (uint64_t)w);
+    g1m_window(t, Wv, L, w);
     g1j x = R, y;
     jac_add(y, x, t);
     R = y;
@@ -197,7 +204,7 @@ BLS_HD BLS_INLINE void g1m_item_rpk(g1j& rp, const uint32_t* gpts, uint64_t n, c
 }
 
 // the Miller value of (R_L, H(m_L)) on one lane into column col of F (host build; the device splits it over a lane
-// pair, kernels.h k_g1m_miller); the value 1 for L >= nl or an empty R
+// pair, verify_lat.hip k_g1m_miller8); the value 1 for L >= nl or an empty R
 template <int S>
 BLS_HD BLS_INLINE void g1m_miller_lane(const f12l<S>& Lf, uint64_t L, const uint32_t* meta, const uint32_t* lmsg,
                                        const uint32_t* Wv, const uint32_t* H, uint64_t hstride, const uint32_t* hslot,

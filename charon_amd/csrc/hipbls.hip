@@ -47,6 +47,15 @@ namespace bls_fp2p {
 __global__ void k_verify_prep8(const uint8_t* pks, const uint8_t* msgs, const uint64_t* offs, const uint8_t* sigs,
                                uint64_t n, uint32_t* ws, int32_t* status);
 __global__ void k_verify_pair_lq8(const uint32_t* ws, uint64_t n, int32_t* status);
+__global__ void k_rlcb_sfactor8(const uint32_t* W, uint32_t* Fs);
+__global__ void k_rlcb_final8(const uint32_t* Ftot, const uint32_t* Fs, int32_t* flag);
+__global__ void k_g1m_miller8(uint64_t nl_max, const uint32_t* meta, const uint32_t* lmsg, const uint32_t* Wv,
+                              const uint32_t* H, uint64_t hstride, const uint32_t* hslot, uint32_t* F, uint64_t col0,
+                              uint64_t fstride);
+// LDS the S-factor workgroup reserves at launch and never touches: the chunk kernel's 36 KiB per workgroup (four per
+// CU), so a CU that hosts the S-factor wave takes at most three chunk waves and no SIMD runs two (a shared SIMD
+// stretched the 1,023-wave chunk kernel by the S factor's run time: 34.9 -> 40.5 ms).
+constexpr uint32_t kSfactorLds = 36 * 1024;
 }  // namespace bls_fp2p
 
 namespace {
@@ -763,7 +772,7 @@ struct G1mLayout {
     bcur = take(nb);
     list = take(2 * (uint64_t)G1M_WIN * n);
     B = take(36 * nb);
-    Wv = take(36 * nl * G1M_WIN);
+    Wv = take(36 * nl * G1M_NFOLD);
     part = take(nparts + 1);
   }
 };
@@ -934,13 +943,13 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
       hipLaunchKernelGGL(k_g1m_bucket, dim3((unsigned)grid_for(gl.nb)), dim3(kBlock), 0, s1, gl.nb,
                          (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.boff), (const uint32_t*)G(gl.list),
                          (const uint32_t*)G(gl.pts), n, G(gl.B));
-      hipLaunchKernelGGL(k_g1m_fold, dim3((unsigned)grid_for(nl_max * G1M_WIN)), dim3(kBlock), 0, s1,
-                         nl_max * G1M_WIN, (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.B), G(gl.Wv));
+      hipLaunchKernelGGL(k_g1m_fold, dim3((unsigned)grid_for(nl_max * G1M_NFOLD)), dim3(kBlock), 0, s1,
+                         nl_max * G1M_NFOLD, (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.B), G(gl.Wv));
     });
     if (rc) return rc;
     HIP_TRY(hipStreamWaitEvent(s1, c.ev_hash, 0));
     rc = timed(c, "rlcb_g1miller", s1, [&] {
-      hipLaunchKernelGGL(k_g1m_miller, dim3((unsigned)grid_for(2 * nl_max)), dim3(kBlock), 0, s1, nl_max,
+      hipLaunchKernelGGL(bls_fp2p::k_g1m_miller8, dim3((unsigned)grid_for(8 * nl_max)), dim3(kBlock), 0, s1, nl_max,
                          (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.lmsg), (const uint32_t*)G(gl.Wv),
                          (const uint32_t*)d_H, hstride, d_hslot, (uint32_t*)c.m_F.p, nch, cols);
     });
@@ -949,7 +958,8 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   HIP_TRY(hipStreamWaitEvent(s, c.rlcb_ev_msm, 0));
   // (-g1, S) on a lane pair on s (after the hash), beside the chunks on the SIMD rlcb_chunk_count leaves free
   rc = timed(c, "rlcb_sfactor", s, [&] {
-    hipLaunchKernelGGL(k_rlcb_sfactor, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)c.m_W.p, (uint32_t*)c.m_Fs.p);
+    hipLaunchKernelGGL(bls_fp2p::k_rlcb_sfactor8, dim3(1), dim3(kBlock), bls_fp2p::kSfactorLds, s,
+                       (const uint32_t*)c.m_W.p, (uint32_t*)c.m_Fs.p);
   });
   if (rc) return rc;
   HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_msm, 0));
@@ -978,7 +988,8 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));
   HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
   rc = timed(c, "rlcb_final", s, [&] {
-    hipLaunchKernelGGL(k_rlcb_final, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src, (const uint32_t*)c.m_Fs.p, flag);
+    hipLaunchKernelGGL(bls_fp2p::k_rlcb_final8, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src,
+                       (const uint32_t*)c.m_Fs.p, flag);
   });
   if (rc) return rc;
   rc = timed(c, "rlcb_mark", s, [&] {

@@ -971,35 +971,6 @@ __global__ void __launch_bounds__(kBlock) k_g1m_fold(uint64_t nq, const uint32_t
   if (q < nq) g1m_fold_lane(q, meta, B, Wv);
 }
 
-// One lane pair per large message L < nl_max: R_L from the window sums (both lanes), the Miller value of (R_L, H(m_L))
-// split over the pair (lg2.h miller_loop_split, the same f as g1m_miller_lane's one-lane loop), the even lane writes
-// column col0 + L of F; the value 1 for L >= nl or an empty R.
-__global__ void __launch_bounds__(kBlock) k_g1m_miller(uint64_t nl_max, const uint32_t* __restrict__ meta,
-                                                       const uint32_t* __restrict__ lmsg, const uint32_t* __restrict__ Wv,
-                                                       const uint32_t* __restrict__ H, uint64_t hstride,
-                                                       const uint32_t* __restrict__ hslot, uint32_t* __restrict__ F,
-                                                       uint64_t col0, uint64_t fstride) {
-  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  const uint64_t L = t >> 1;
-  if (L >= nl_max) return;  // the same on both lanes of the pair
-  const uint32_t m = (t & 1) ? ~0u : 0u;
-  fp12 f;
-  fp12_set_one(f);
-  if (L < meta[0]) {
-    g1j R;
-    g1m_combine(R, Wv, L);
-    if (!jac_is_inf(R)) {  // the same on both lanes
-      g1a P;
-      g2a Q;
-      jac_to_aff(P, R);
-      soa_load<48>(&Q.x.c0.v[0], H, hstride, h_col(hslot, lmsg[L]));
-      fp6 h;
-      miller_loop_split(h, P, Q, m);
-      fp12h_gather(f, h, m);
-    }
-  }
-  if (!m) soa_store<144>(F, fstride, col0 + L, &f.c0.c0.c0.v[0]);
-}
 
 // ---- exclusive scan of n u32 counts (the G1 MSM's buckets): block sums, one-workgroup scan of them, block scans
 constexpr int kScanBlk = 1024;
@@ -1144,7 +1115,7 @@ __global__ void __launch_bounds__(kSumBlock) k_msm_window(const uint32_t* __rest
 // Stage 3: one lane per chunk, n_chunks lanes exactly (rlcb.h rlcb_chunk_count).  The (-g1, S) Miller value is NOT an
 // extra lane here: at the bench's 1M items 65,536 chunks were exactly one wave per SIMD (four 36-KiB-LDS workgroups
 // per CU) and one lane more made a 1,025th workgroup -- a second round of waves (profiles/r04: 41 ms for 28 ms of
-// chunk work).  k_rlcb_sfactor computes it on the SIMD rlcb_chunk_count leaves free.
+// chunk work).  k_rlcb_sfactor8 (verify_lat.hip) computes it on the SIMD rlcb_chunk_count leaves free.
 __global__ void __launch_bounds__(kBlock) k_rlcb_chunks(uint64_t n, const int32_t* __restrict__ status,
                                                         const uint32_t* __restrict__ msg_idx,
                                                         const uint32_t* __restrict__ rpk,
@@ -1162,53 +1133,6 @@ __global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict
   if (g < nout) fp12_prod_lane(g, Fin, nin, Fout, nout, fan);
 }
 
-// The Miller value of (-g1, S), S = W0 + [2^16] W1 from the MSM's window sums (rlcb.h msm_combine): lanes 0, 1 as a
-// pair (lg2.h miller_loop_split, the same f as rlcb_sfactor_lane's one-lane loop), gathered, 144 words to Fs.  One
-// wave, beside the chunk kernel.
-__global__ void __launch_bounds__(kBlock) k_rlcb_sfactor(const uint32_t* __restrict__ W, uint32_t* __restrict__ Fs) {
-  const int t = threadIdx.x;
-  if (t >= 2) return;
-  const uint32_t m = t ? ~0u : 0u;
-  g2j W0, W1, S;
-  for (int k = 0; k < 72; ++k) {
-    (&W0.x.c0.v[0])[k] = W[k];
-    (&W1.x.c0.v[0])[k] = W[72 + k];
-  }
-  msm_combine(S, W0, W1);
-  fp12 f;
-  if (jac_is_inf(S)) {  // the same on both lanes
-    fp12_set_one(f);
-  } else {
-    g1a P;
-    P.x = G1_GEN_X;
-    P.y = G1_NEG_GEN_Y;
-    g2a Q;
-    jac_to_aff(Q, S);
-    fp6 h;
-    miller_loop_split(h, P, Q, m);
-    fp12h_gather(f, h, m);
-  }
-  if (t == 0)
-    for (int k = 0; k < 144; ++k) Fs[k] = (&f.c0.c0.c0.v[0])[k];
-}
-
-// The verdict on a lane quad (lg2.h): the chunks' product (Ftot, one column) times the (-g1, S) value (Fs), one
-// Fp6 product per lane, then the quad's final exponentiation; flag[0] = 1 when the result is 1.
-__global__ void __launch_bounds__(kBlock) k_rlcb_final(const uint32_t* __restrict__ Ftot, const uint32_t* __restrict__ Fs,
-                                                       int32_t* __restrict__ flag) {
-  const int t = threadIdx.x;
-  if (t >= 4) return;
-  fp12 a, b, r, e;
-  for (int k = 0; k < 144; ++k) {
-    (&a.c0.c0.c0.v[0])[k] = Fs[k];
-    (&b.c0.c0.c0.v[0])[k] = Ftot[k];
-  }
-  const quad_m qm(t);
-  fp12q_mul(r, a, b, qm);
-  final_exponentiation_quad(e, r, qm);
-  const bool ok = fp12_is_one(e);
-  if (t == 0) flag[0] = ok ? 1 : 0;
-}
 
 __global__ void __launch_bounds__(kBlock) k_rlcb_mark(uint64_t n, const int32_t* __restrict__ flag,
                                                       int32_t* __restrict__ status, const uint32_t* __restrict__ pts,

@@ -206,7 +206,7 @@ BLS_HD BLS_INLINE void msm_combine(g2j& S, const g2j& W0, const g2j& W1) {
 // ---- stage 3: per-chunk multi-Miller loop ----------------------------------------------------------
 // How many chunks for n items: ceil(n / RLCB_C), unless that fills whole rounds of waves exactly (`slots` = the waves
 // the device runs at once at one wave per SIMD): then one wave fewer, items spread over the lanes (16 or 17 each), so
-// a SIMD stays free for the (-g1, S) Miller value beside the chunks (k_rlcb_sfactor).  At the bench's 1M items:
+// a SIMD stays free for the (-g1, S) Miller value beside the chunks (verify_lat.hip k_rlcb_sfactor8).  At the bench's 1M items:
 // 65,536 chunks = 1,024 waves = every SIMD, so 65,472.
 BLS_HD BLS_INLINE uint64_t rlcb_chunk_count(uint64_t n, uint64_t slots) {
   const uint64_t nch = (n + RLCB_C - 1) / RLCB_C;

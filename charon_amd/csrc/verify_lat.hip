@@ -1,10 +1,14 @@
-// The drop-in latency path: tbls.Verify for batches far below one wave of work per SIMD (the unpatched callers'
-// n = 1 calls, /root/reference/core/parsigex/parsigex.go:86-91 and core/validatorapi/validatorapi.go:246-283), on
-// EIGHT lanes per item (VERDICT r03 "Next round" 8).  This translation unit is the lane-quad Verify of kernels.h
-// (k_verify_prep + k_verify_pair_lq4, lg2.h lq4_verify) compiled with BLS_FP2_PAIR: every Fp2 product and square is
-// split across lanes l and l ^ 4 (field.h fp2p_*, tower.h), so the quad's lanes 0-3 and their twins 4-7 hold the
-// same values and each does half of every Fp2 product.  Same formulas, same statuses; ~half the latency of the
-// Fp2-bound chains (hash to G2, the Miller loops, the final exponentiation).
+// Latency-bound kernels on twice the lanes, with every Fp2 product and square split across twin lanes:
+//   * the drop-in latency path: tbls.Verify for batches far below one wave of work per SIMD (the unpatched callers'
+//     n = 1 calls, /root/reference/core/parsigex/parsigex.go:86-91 and core/validatorapi/validatorapi.go:246-283), on
+//     EIGHT lanes per item (VERDICT r03 "Next round" 8): the lane-quad Verify of kernels.h (k_verify_prep +
+//     k_verify_pair_lq4, lg2.h lq4_verify) with every Fp2 product and square split across lanes l and l ^ 4
+//     (field.h fp2p_*, tower.h), so the quad's lanes 0-3 and their twins 4-7 hold the same values and each does half
+//     of every Fp2 product;
+//   * the batch-wide RLC check's serial tail (rlcb.h): the (-g1, S) Miller value, the verdict's final
+//     exponentiation, and the Miller value of each large message's G1 MSM sum (g1msm.h).
+// Same formulas, same results; ~0.7x the latency of the Fp2-bound chains (hash to G2, Miller loops, final
+// exponentiation: profiles/r04/latency_sweep_quads_octets.json).
 //
 // Everything here lives in namespace bls_fp2p (the kernel headers are included with `bls` renamed), so its inline
 // functions never meet the main translation unit's on the host side; hipbls.hip declares and launches the two kernels.
@@ -13,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "lg2.h"
+#include "rlcb.h"
 
 namespace bls {
 
@@ -77,6 +82,85 @@ __global__ void __launch_bounds__(kOctBlock) k_verify_pair_lq8(const uint32_t* _
   soa_load<48>(&sig.x.c0.v[0], ws + 72 * n, n, i);
   const int st = lq4_verify(pk, hm, sig, (int)(t & 3));
   if ((t & 7) == 0) status[i] = st;
+}
+
+// ---------------------------------------------------------------- the batch-wide RLC check's tail (rlcb.h)
+// The Miller value of (-g1, S), S = W0 + [2^16] W1 from the MSM's window sums (rlcb.h msm_combine): lanes 0/1 split
+// the loop (lg2.h miller_loop_split), lanes 4/5 are their Fp2 twins (2, 3, 6, 7 repeat them); 144 words to Fs.
+__global__ void __launch_bounds__(kOctBlock) k_rlcb_sfactor8(const uint32_t* __restrict__ W, uint32_t* __restrict__ Fs) {
+  const int t = threadIdx.x;
+  if (t >= 8) return;
+  const uint32_t m = (t & 1) ? ~0u : 0u;
+  g2j W0, W1, S;
+  for (int k = 0; k < 72; ++k) {
+    (&W0.x.c0.v[0])[k] = W[k];
+    (&W1.x.c0.v[0])[k] = W[72 + k];
+  }
+  msm_combine(S, W0, W1);
+  fp12 f;
+  if (jac_is_inf(S)) {  // the same on all eight lanes
+    fp12_set_one(f);
+  } else {
+    g1a P;
+    P.x = G1_GEN_X;
+    P.y = G1_NEG_GEN_Y;
+    g2a Q;
+    jac_to_aff(Q, S);
+    fp6 h;
+    miller_loop_split(h, P, Q, m);
+    fp12h_gather(f, h, m);
+  }
+  if (t == 0)
+    for (int k = 0; k < 144; ++k) Fs[k] = (&f.c0.c0.c0.v[0])[k];
+}
+
+// The verdict: the product tree's value (Ftot) times the (-g1, S) value (Fs) and the final exponentiation on a lane
+// quad (lanes 0-3, lg2.h fp12q_mul / final_exponentiation_quad) with Fp2 twins on 4-7; flag[0] = 1 when it is 1.
+__global__ void __launch_bounds__(kOctBlock) k_rlcb_final8(const uint32_t* __restrict__ Ftot,
+                                                           const uint32_t* __restrict__ Fs, int32_t* __restrict__ flag) {
+  const int t = threadIdx.x;
+  if (t >= 8) return;
+  fp12 a, b, r, e;
+  for (int k = 0; k < 144; ++k) {
+    (&a.c0.c0.c0.v[0])[k] = Fs[k];
+    (&b.c0.c0.c0.v[0])[k] = Ftot[k];
+  }
+  const quad_m qm(t & 3);
+  fp12q_mul(r, a, b, qm);
+  final_exponentiation_quad(e, r, qm);
+  const bool ok = fp12_is_one(e);
+  if (t == 0) flag[0] = ok ? 1 : 0;
+}
+
+// Eight lanes per large message L < nl_max (g1msm.h): R_L from the window sums, the Miller value of (R_L, H(m_L))
+// split over lanes 0/1 with Fp2 twins 4/5 (2, 3, 6, 7 repeat them); lane 0 writes column col0 + L of F.  The value 1
+// for L >= nl or an empty R.
+__global__ void __launch_bounds__(kOctBlock) k_g1m_miller8(uint64_t nl_max, const uint32_t* __restrict__ meta,
+                                                           const uint32_t* __restrict__ lmsg,
+                                                           const uint32_t* __restrict__ Wv,
+                                                           const uint32_t* __restrict__ H, uint64_t hstride,
+                                                           const uint32_t* __restrict__ hslot, uint32_t* __restrict__ F,
+                                                           uint64_t col0, uint64_t fstride) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t L = t >> 3;
+  if (L >= nl_max) return;  // the same on all eight lanes
+  const uint32_t m = (t & 1) ? ~0u : 0u;
+  fp12 f;
+  fp12_set_one(f);
+  if (L < meta[0]) {
+    g1j R;
+    g1m_combine(R, Wv, L);
+    if (!jac_is_inf(R)) {
+      g1a P;
+      g2a Q;
+      jac_to_aff(P, R);
+      soa_load<48>(&Q.x.c0.v[0], H, hstride, h_col(hslot, lmsg[L]));
+      fp6 h;
+      miller_loop_split(h, P, Q, m);
+      fp12h_gather(f, h, m);
+    }
+  }
+  if ((t & 7) == 0) soa_store<144>(F, fstride, col0 + L, &f.c0.c0.c0.v[0]);
 }
 
 }  // namespace bls

@@ -562,7 +562,7 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
   }
   const uint64_t nb = nl_max * G1M_NBL;
   std::vector<uint32_t> bcnt(nb + 1, 0), boff(nb + 1), bcur(nb + 1), glist(2 * G1M_WIN * n + 1), B(36 * nb + 4);
-  std::vector<uint32_t> Wv(36 * nl_max * G1M_WIN + 4);
+  std::vector<uint32_t> Wv(36 * nl_max * G1M_NFOLD + 4);
   if (g1) {  // counted with the MSM (stage 2 of counts6)
     for (uint64_t t = 0; t < n; ++t) g1m_hist_lane(t, meta.data(), gsc.data(), slotl.data(), bcnt.data());
     uint32_t acc = 0;
@@ -573,7 +573,7 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
     boff[nb] = acc;
     for (uint64_t t = 0; t < n; ++t) g1m_scatter_lane(t, meta.data(), gsc.data(), slotl.data(), bcur.data(), glist.data());
     for (uint64_t b = 0; b < nb; ++b) g1m_bucket_lane(b, meta.data(), boff.data(), glist.data(), gpts.data(), n, B.data());
-    for (uint64_t q = 0; q < nl_max * G1M_WIN; ++q) g1m_fold_lane(q, meta.data(), B.data(), Wv.data());
+    for (uint64_t q = 0; q < nl_max * G1M_NFOLD; ++q) g1m_fold_lane(q, meta.data(), B.data(), Wv.data());
   }
   mark(2);
   // stage 3 as the device runs it: the chunks, then the (-g1, S) lane as the last column
