@@ -179,6 +179,7 @@ struct Context {
   // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
   DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_flag, m_Fs;
   DevBuf g1_ws;  // the G1 MSM per large message (g1msm.h), carved by G1mLayout; its Miller values go to m_F
+  hipEvent_t rlcb_ev_sf = nullptr;  // the (-g1, S) Miller value is in m_Fs
   uint64_t slots = 0;               // waves in flight at one wave per SIMD: 4 x compute units (wave_slots)
   // Verdicts come back through a ring of pinned slots, one per batch check in flight, so a launch only waits
   // on the host when kRlcbSlots checks are still unread (never in the enqueue-only *_device paths otherwise).
@@ -838,6 +839,7 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
     for (int k = 0; k < Context::kRlcbSlots; ++k) HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_items, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_msm, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c.rlcb_ev_sf, hipEventDisableTiming));
   }
   int rc = ensure_rlc_streams(c);
   if (rc) return rc;
@@ -869,8 +871,8 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   // kernels; sub[1] runs the G1 MSM of the large messages beside the G2 MSM (both only need the items) and their
   // Miller values, then the chunk Miller loops and the product once the G2 MSM and the hash are done -- after the
   // MSM, because the chunk kernel holds every SIMD for its whole run and a short kernel queued behind it waits that
-  // long (round 2: k_msm_scan 33 ms beside k_rlcb_chunks 37.7 ms).  s, idle after the hash, runs the (-g1, S) lane
-  // pair once the G2 MSM is done (beside the chunks or the G1 Miller values), then the verdict and the windows.
+  // long (round 2: k_msm_scan 33 ms beside k_rlcb_chunks 37.7 ms).  sub[0] follows the G2 MSM with the (-g1, S)
+  // Miller value; s joins for the verdict and the windows.
   hipStream_t s0 = c.sub[0], s1 = c.sub[1];
   rc = ws_begin(c, s, WS_RLC);
   if (rc) return rc;
@@ -925,6 +927,15 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.rlcb_ev_msm, s0));
+  // (-g1, S) right behind the MSM on its own queue, beside the chunks on the SIMD rlcb_chunk_count leaves free.  (On
+  // the caller's stream, released by the same event as the chunks, it made the 1,023-wave chunk kernel 4.5 ms slower:
+  // scripts/ab_c4_chunks.sh.)
+  rc = timed(c, "rlcb_sfactor", s0, [&] {
+    hipLaunchKernelGGL(bls_fp2p::k_rlcb_sfactor8, dim3(1), dim3(kBlock), bls_fp2p::kSfactorLds, s0,
+                       (const uint32_t*)c.m_W.p, (uint32_t*)c.m_Fs.p);
+  });
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c.rlcb_ev_sf, s0));
   if (g1) {  // the large messages' sums R_L and their Miller values, beside the G2 MSM
     HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_items, 0));
     rc = timed(c, "rlcb_g1sort", s1, [&] {
@@ -955,13 +966,6 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
     });
     if (rc) return rc;
   }
-  HIP_TRY(hipStreamWaitEvent(s, c.rlcb_ev_msm, 0));
-  // (-g1, S) on a lane pair on s (after the hash), beside the chunks on the SIMD rlcb_chunk_count leaves free
-  rc = timed(c, "rlcb_sfactor", s, [&] {
-    hipLaunchKernelGGL(bls_fp2p::k_rlcb_sfactor8, dim3(1), dim3(kBlock), bls_fp2p::kSfactorLds, s,
-                       (const uint32_t*)c.m_W.p, (uint32_t*)c.m_Fs.p);
-  });
-  if (rc) return rc;
   HIP_TRY(hipStreamWaitEvent(s1, c.rlcb_ev_msm, 0));
   HIP_TRY(hipStreamWaitEvent(s1, c.ev_hash, 0));
   rc = timed(c, "rlcb_chunks", s1, [&] {
@@ -987,6 +991,7 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.ev_join[1], s1));
   HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
+  HIP_TRY(hipStreamWaitEvent(s, c.rlcb_ev_sf, 0));
   rc = timed(c, "rlcb_final", s, [&] {
     hipLaunchKernelGGL(bls_fp2p::k_rlcb_final8, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)src,
                        (const uint32_t*)c.m_Fs.p, flag);
