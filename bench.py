@@ -42,7 +42,10 @@ RLC_FPMUL = {"item": 5802, "hash": 4790, "window_2msg": 21906, "window_1msg": 17
 # (2 points x 2 windows of mixed additions; the bucket/segment folds add ~15 per item at 1M items and are left
 # out), and one multi-Miller loop per 16-item chunk with 4 message runs (one root per 4-partial validator) or with one
 # run (committee roots, C4(ii)).
-RLCB_FPMUL = {"item": 4306, "msm_per_item": 116, "chunk_4runs": 18948, "chunk_1run": 6909}
+RLCB_FPMUL = {"item": 4306, "msm_per_item": 116, "chunk_4runs": 18948, "chunk_1run": 6909,
+              # the G1 MSM per committee root (g1msm.h) at 512 items per root: stage 1 without the per-item Shamir
+              # multiplication, the bucket + fold work per item, one Miller pair per root
+              "item_g1slot": 3702, "g1msm_per_item_512": 207, "g1miller_per_root": 6977}
 # sigagg in one call (C3), per aggregate of 7 partials, same unit and source (tests/native/host_ops.cpp
 # ht_count_tagg_verify, tests/test_work_counts.py): the 7 partials' decode + subgroup test + c_k sig_k (k_tagg_scale),
 # the sum S (k_tagg_sum_s), [L^-1] S + compress (k_tagg_unscale), the root key's decode + subgroup test + [L] pk +
@@ -210,11 +213,12 @@ def c4_node_bad(tag, v_node, nk, shares=4, corrupt=True):
     return {v * shares + j for v in range(v_node) for j in range(shares) if c4_item(tag, v, j, nk, corrupt)[1]}
 
 
-def pmc_summary(path=os.path.join(ROOT, "profiles", "r03_pmc_verify.json")):
-    """k_verify_fused counters from the committed rocprofv3 --pmc passes over this build's bench (scripts/gpu_pmc.sh,
-    scripts/pmc_summary.py): HBM bytes per launch (FETCH_SIZE + WRITE_SIZE), their ratio to the 188 B/verify of
-    algorithmic input, VALU utilisation (SQ_ACTIVE_INST_VALU / SQ_BUSY_CYCLES per SIMD) and the fraction of wave
-    cycles spent waiting.  {} when absent."""
+def pmc_summary(path=os.path.join(ROOT, "profiles", "r04", "pmc_verify.json")):
+    """k_verify_fused counters from the committed rocprofv3 --pmc passes over this build's bench (scripts/gpu_pmc_r04.sh
+    WL=c2, scripts/pmc_commit_r04.py): HBM bytes per launch (FETCH_SIZE + WRITE_SIZE), their ratio to the 188 B/verify
+    of algorithmic input, VALU utilisation (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES at one wave per SIMD), the fraction
+    of wave cycles spent waiting, VALU and 64-bit integer VALU (the v_mad_u64_u32 stream) instructions per wave, and
+    the commit the counters were taken at.  {} when absent."""
     try:
         with open(path) as f:
             d = json.load(f)
@@ -222,7 +226,9 @@ def pmc_summary(path=os.path.join(ROOT, "profiles", "r03_pmc_verify.json")):
         return {}
     return {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch_raw"), "traffic_ratio": d.get("traffic_ratio"),
             "valu_util": d.get("valu_util"), "wait_any_frac": d.get("wait_any_frac"),
-            "source": os.path.relpath(path, ROOT)}
+            "valu_insts_per_wave": d.get("valu_insts_per_wave"),
+            "int64_valu_insts_per_wave": d.get("int64_valu_insts_per_wave"),
+            "taken_at": d.get("taken_at"), "source": os.path.relpath(path, ROOT)}
 
 
 def _cpu_model():
@@ -599,9 +605,16 @@ def main():
             per_win = RLC_FPMUL["window_1msg"] if n_roots else RLC_FPMUL["window_2msg"]
             fpmul = (RLC_FPMUL["item"] * n4 + RLC_FPMUL["hash"] * len(roots4) + per_win * w.value
                      + RLC_FPMUL["fallback"] * fb.value)
+            # committee roots take the G1 MSM path (hipbls.hip launch_rlc_batch: >= 8 items per root on average,
+            # roots of >= 64 items)
+            g1path = n_roots > 0 and n4 >= 8 * len(roots4) and n4 // len(roots4) >= 64
+            item_unit = RLCB_FPMUL["item_g1slot" if g1path else "item"]
+            chunk_work = 0 if g1path else RLCB_FPMUL["chunk_1run" if n_roots else "chunk_4runs"] * ((n4 + 15) // 16)
+            g1_work = (RLCB_FPMUL["g1msm_per_item_512"] * n4 + RLCB_FPMUL["g1miller_per_root"] * len(roots4)
+                       if g1path else 0)
             if b_pass1 > b_pass0:  # the batch-wide check decided alone: no window pairing work
-                fpmul = ((RLCB_FPMUL["item"] + RLCB_FPMUL["msm_per_item"]) * n4 + RLC_FPMUL["hash"] * len(roots4)
-                         + RLCB_FPMUL["chunk_1run" if n_roots else "chunk_4runs"] * ((n4 + 15) // 16))
+                fpmul = ((item_unit + RLCB_FPMUL["msm_per_item"]) * n4 + RLC_FPMUL["hash"] * len(roots4) + chunk_work
+                         + g1_work)
             ach = fpmul * MADS_PER_FPMUL * args.rlc_steps / tel / 1e12
             rlc[variant] = {"verified_partial_sigs_per_s": round(4 * V * args.rlc_steps / tel, 1),
                             "node_items": 4 * V, "items_this_gpu": n4, "distinct_roots_this_gpu": len(roots4),
@@ -624,9 +637,10 @@ def main():
                                 "rlc_window_lg2": 0 if b_pass1 > b_pass0 else per_win * w.value,
                                 "rlc_fallback": RLC_FPMUL["fallback"] * fb.value,
                                 "rlc_fallback_lg2": RLC_FPMUL["fallback"] * fb.value,
-                                "rlcb_items": RLCB_FPMUL["item"] * n4,
-                                "rlcb_chunks": RLCB_FPMUL["chunk_1run" if n_roots else "chunk_4runs"]
-                                * ((n4 + 15) // 16)}, args.rlc_steps)}
+                                "rlcb_items": item_unit * n4, "rlcb_chunks": chunk_work,
+                                "rlcb_g1msm": RLCB_FPMUL["g1msm_per_item_512"] * n4 if g1path else 0,
+                                "rlcb_g1miller": RLCB_FPMUL["g1miller_per_root"] * len(roots4) if g1path else 0},
+                                args.rlc_steps)}
             if corrupt and variant == "i_root_per_validator":
                 # the library's default policy (HIPBLS_RLC_AUTO) on the same stream: one failing batch-wide check,
                 # then windows while it backs off (rlc_mode comment above)
@@ -791,6 +805,9 @@ def main():
                 "valu_util": pmc.get("valu_util"),
                 "wait_any_frac": pmc.get("wait_any_frac"),
                 "pmc_source": pmc.get("source"),
+                "pmc_taken_at": pmc.get("taken_at"),
+                "valu_insts_per_wave": pmc.get("valu_insts_per_wave"),
+                "mad_insts_per_wave": pmc.get("int64_valu_insts_per_wave"),
                 "algorithmic_unit": "%d Fp-mul-equivalents x %d MADs per verify" % (FPMUL_PER_VERIFY, MADS_PER_FPMUL),
                 "kernel_avg_ms": round(k_ms, 3),
                 "kernel_launches": int(launches.value),

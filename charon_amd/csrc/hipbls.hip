@@ -856,7 +856,7 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   HIP_TRY(c.m_Sg.ensure((uint64_t)MSM_WINDOWS * MSM_NSEG * 72 * 4));
   HIP_TRY(c.m_W.ensure((uint64_t)MSM_WINDOWS * 72 * 4));
   HIP_TRY(c.m_F.ensure(cols * 144 * 4));
-  HIP_TRY(c.m_F2.ensure(((cols + RLCB_FAN - 1) / RLCB_FAN) * 144 * 4));
+  HIP_TRY(c.m_F2.ensure(((cols + kBlock - 1) / kBlock) * 144 * 4));
   if (g1) HIP_TRY(c.g1_ws.ensure(gl.words * 4));
   uint32_t* gw = (uint32_t*)c.g1_ws.p;
   auto G = [&](uint64_t off) { return g1 ? gw + off : nullptr; };
@@ -978,10 +978,9 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   uint32_t* dst = (uint32_t*)c.m_F2.p;
   uint64_t cur = cols;
   rc = timed(c, "rlcb_product", s1, [&] {
-    while (cur > 1) {
-      const uint64_t nxt = (cur + RLCB_FAN - 1) / RLCB_FAN;
-      hipLaunchKernelGGL(k_fp12_prod, dim3((unsigned)grid_for(nxt)), dim3(kBlock), 0, s1, (const uint32_t*)src, cur,
-                         dst, nxt, RLCB_FAN);
+    while (cur > 1) {  // 64 columns per wave (k_fp12_prod64)
+      const uint64_t nxt = (cur + kBlock - 1) / kBlock;
+      hipLaunchKernelGGL(k_fp12_prod64, dim3((unsigned)nxt), dim3(kBlock), 0, s1, (const uint32_t*)src, cur, dst, nxt);
       uint32_t* t = src;
       src = dst;
       dst = t;

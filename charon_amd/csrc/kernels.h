@@ -1127,11 +1127,35 @@ __global__ void __launch_bounds__(kBlock) k_rlcb_chunks(uint64_t n, const int32_
   if (c < n_chunks) rlcb_chunk_lane(Lf, c, n, status, msg_idx, rpk, H, hstride, hslot, F, n_chunks, fstride);
 }
 
-__global__ void __launch_bounds__(kBlock) k_fp12_prod(const uint32_t* __restrict__ Fin, uint64_t nin,
-                                                      uint32_t* __restrict__ Fout, uint64_t nout, int fan) {
-  const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (g < nout) fp12_prod_lane(g, Fin, nin, Fout, nout, fan);
+// Product of F's columns 64 at a time: workgroup g (one wave) multiplies columns [64 g, 64 g + 64) by a binary tree
+// through LDS -- one Fp12 product of latency per level, six levels -- and lane 0 writes column g of Fout (missing
+// columns count as 1).  65,472 chunk values take three launches and 16 products of latency, where fan-in-4 levels
+// took eight launches and 24 (profiles/r04: 8 x 0.36 ms).
+__global__ void __launch_bounds__(kBlock) k_fp12_prod64(const uint32_t* __restrict__ Fin, uint64_t nin,
+                                                        uint32_t* __restrict__ Fout, uint64_t nout) {
+  static_assert(kBlock == 64, "one wave per workgroup");
+  __shared__ uint32_t s_x[144 * kBlock];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t col = blockIdx.x * (uint64_t)kBlock + lane;
+  fp12 acc;
+  if (col < nin)
+    soa_load<144>(&acc.c0.c0.c0.v[0], Fin, nin, col);
+  else
+    fp12_set_one(acc);
+  for (uint32_t st = 1; st < (uint32_t)kBlock; st <<= 1) {
+    for (int k = 0; k < 144; ++k) s_x[k * kBlock + lane] = (&acc.c0.c0.c0.v[0])[k];
+    __syncthreads();
+    if ((lane & (2 * st - 1)) == 0) {
+      fp12 o;
+      for (int k = 0; k < 144; ++k) (&o.c0.c0.c0.v[0])[k] = s_x[k * kBlock + lane + st];
+      fp12 x = acc;
+      fp12_mul(acc, x, o);
+    }
+    __syncthreads();
+  }
+  if (lane == 0) soa_store<144>(Fout, nout, blockIdx.x, &acc.c0.c0.c0.v[0]);
 }
+
 
 
 __global__ void __launch_bounds__(kBlock) k_rlcb_mark(uint64_t n, const int32_t* __restrict__ flag,

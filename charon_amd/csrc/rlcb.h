@@ -15,12 +15,15 @@
 //                 2n points by digit (histogram, scan, scatter), one lane per bucket sums its points, one lane
 //                 per 16-bucket segment folds sum_j j B_j by running sums, two workgroups tree-sum the
 //                 segments in LDS, and S = W0 + [2^16] W1;
-//   3. chunks   : one lane per 16 consecutive items: runs of equal message among pending items are summed in G1
-//                 and paired with H(m) in one multi-Miller loop (no final exponentiation) -> f_chunk; one more
-//                 lane forms S from the window sums and computes the Miller value of (-g1, S) as the last column;
-//   4. product  : the chunks' Miller values multiplied together (fan-in RLCB_FAN per level);
-//   5. final    : a lane pair runs the split final exponentiation of the product (lg2.h); the verdict goes to
-//                 a device flag;
+//   3. chunks   : one lane per ~16 consecutive items: runs of equal message among pending items are summed in G1
+//                 and paired with H(m) in one multi-Miller loop (no final exponentiation) -> f_chunk; beside them
+//                 the S factor: S from the window sums and the Miller value of (-g1, S) (rlcb_sfactor_lane; on the
+//                 device a split-Fp2 lane group, verify_lat.hip k_rlcb_sfactor8); committee roots add one Miller
+//                 value per large message (g1msm.h);
+//   4. product  : the Miller values multiplied together (host: fan-in RLCB_FAN per level; device: 64 per wave,
+//                 kernels.h k_fp12_prod64);
+//   5. final    : the product times the S factor and the final exponentiation (device: a lane quad with Fp2
+//                 twins, verify_lat.hip k_rlcb_final8); the verdict goes to a device flag;
 //   6. mark     : pass -> every pending item is valid; fail -> each pending item gets [r_i] sig_i for the window
 //                 stages of rlc.h, which then decide item by item.
 // Soundness is the windows' argument over the whole batch: a batch with an invalid item passes with
