@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 case $WL in
   c2) ARGS="--steps 1 --warmup 0 --tagg-groups 0 --cpu-sample 0 --rlc-node-validators 0 --c5 0 --keys 0 --latency-calls 0";;
   c3) ARGS="--c2-items 40960 --steps 1 --warmup 0 --tagg-steps 1 --cpu-sample 0 --rlc-node-validators 0 --c5 0 --keys 0 --latency-calls 0";;
-  c4) ARGS="--c2-items 40960 --steps 1 --warmup 0 --tagg-groups 0 --rlc-steps 1 --rlc-variants i,all_valid --c5 0 --keys 0 --latency-calls 0 --cpu-sample 0";;
+  c4) ARGS="--c2-items 40960 --steps 1 --warmup 0 --tagg-groups 0 --rlc-steps 1 --rlc-variants i,all_valid,ii_all_valid --c5 0 --keys 0 --latency-calls 0 --cpu-sample 0";;
 esac
 if [ ! -s $R/gpurun_out/counters_avail.txt ]; then
   timeout -s KILL 90 rocprofv3 --list-avail > $R/gpurun_out/counters_avail.txt 2>&1 || true
