@@ -106,9 +106,11 @@ BLS_HD BLS_CALL void jac_dbl(jac<F>& r, const jac<F>& p_in) {
   r = t;
 }
 
-// add-2007-bl with the exceptional cases handled (P = Q doubles, P = -Q gives infinity)
+// add-2007-bl with the exceptional cases handled (P = Q doubles, P = -Q gives infinity).  The _body form inlines into
+// a loop (the MSM bucket and fold lanes, where a call would save and restore the live accumulators through scratch
+// on every addition); jac_add is the out-of-line call everything else uses.
 template <class F>
-BLS_HD BLS_CALL void jac_add(jac<F>& r, const jac<F>& p_in, const jac<F>& q_in) {
+BLS_HD BLS_INLINE void jac_add_body(jac<F>& r, const jac<F>& p_in, const jac<F>& q_in) {
   const jac<F> p = p_in;
   const jac<F> q = q_in;
   if (jac_is_inf(p)) {
@@ -163,9 +165,14 @@ BLS_HD BLS_CALL void jac_add(jac<F>& r, const jac<F>& p_in, const jac<F>& q_in) 
   r.z = z3;
 }
 
-// mixed addition r = p + q with q affine (madd-2007-bl), exceptional cases handled
 template <class F>
-BLS_HD BLS_CALL void jac_add_aff(jac<F>& r, const jac<F>& p_in, const aff<F>& q_in) {
+BLS_HD BLS_CALL void jac_add(jac<F>& r, const jac<F>& p_in, const jac<F>& q_in) {
+  jac_add_body(r, p_in, q_in);
+}
+
+// mixed addition r = p + q with q affine (madd-2007-bl), exceptional cases handled (_body: inlined, as jac_add_body)
+template <class F>
+BLS_HD BLS_INLINE void jac_add_aff_body(jac<F>& r, const jac<F>& p_in, const aff<F>& q_in) {
   const jac<F> p = p_in;
   const aff<F> q = q_in;
   if (jac_is_inf(p)) {
@@ -210,6 +217,10 @@ BLS_HD BLS_CALL void jac_add_aff(jac<F>& r, const jac<F>& p_in, const aff<F>& q_
   r.x = x3;
   r.y = y3;
   r.z = z3;
+}
+template <class F>
+BLS_HD BLS_CALL void jac_add_aff(jac<F>& r, const jac<F>& p_in, const aff<F>& q_in) {
+  jac_add_aff_body(r, p_in, q_in);
 }
 
 // r = [k] p for a 64-bit scalar k (uniform across lanes when k is a constant)

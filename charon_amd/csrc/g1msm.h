@@ -128,7 +128,7 @@ BLS_HD BLS_INLINE void g1m_bucket_lane(uint64_t b, const uint32_t* meta, const u
       const g1j cur = q;
       if (k + 1 < k1) aos_load<36>(&q.x.v[0], gxp, list[k + 1]);
       g1j x = acc, y;
-      jac_add(y, x, cur);
+      jac_add_body(y, x, cur);
       acc = y;
     }
   } else {  // pk, affine
@@ -138,7 +138,7 @@ BLS_HD BLS_INLINE void g1m_bucket_lane(uint64_t b, const uint32_t* meta, const u
       const g1a cur = q;
       if (k + 1 < k1) aos_load<24>(&q.x.v[0], gpts, list[k + 1]);
       g1j x = acc, y;
-      jac_add_aff(y, x, cur);
+      jac_add_aff_body(y, x, cur);
       acc = y;
     }
   }
@@ -159,10 +159,10 @@ BLS_HD BLS_INLINE void g1m_fold_lane(uint64_t q, const uint32_t* meta, const uin
     g1j b;
     aos_load<36>(&b.x.v[0], B, g1m_bucket(L, kind, w, d));
     g1j x = R, y;
-    jac_add(y, x, b);
+    jac_add_body(y, x, b);
     R = y;
     g1j u = T, v;
-    jac_add(v, u, R);
+    jac_add_body(v, u, R);
     T = v;
   }
   aos_store<36>(Wv, q, &T.x.v[0]);

@@ -147,7 +147,8 @@ BLS_HD BLS_INLINE void msm_scatter_lane(uint64_t p, const uint32_t* sc, uint32_t
 
 // bucket (w, j): the sum of its points.  off: MSM_WINDOWS x (MSM_NB + 1) exclusive offsets.  B: Jacobian SoA,
 // 72 words x (MSM_WINDOWS * MSM_NB).  Software-pipelined: the next point's gather is issued before the current
-// addition (a call the loads cannot move across), so its latency hides behind ~30 products of work.
+// addition, so its latency hides behind ~30 products of work; the addition is inlined (jac_add_aff_body), so the
+// accumulator and the prefetched point stay in registers instead of going through scratch around a call.
 BLS_HD BLS_INLINE void msm_bucket_lane(uint32_t w, uint32_t j, const uint32_t* off, const uint32_t* list,
                                        uint64_t npts, const uint32_t* pts, uint32_t* B) {
   g2j acc;
@@ -159,7 +160,7 @@ BLS_HD BLS_INLINE void msm_bucket_lane(uint32_t w, uint32_t j, const uint32_t* o
     const g2a cur = q;
     if (k + 1 < k1) aos_load<48>(&q.x.c0.v[0], pts, list[(uint64_t)w * npts + k + 1]);
     g2j x = acc, y;
-    jac_add_aff(y, x, cur);
+    jac_add_aff_body(y, x, cur);
     acc = y;
   }
   soa_store<72>(B, (uint64_t)MSM_WINDOWS * MSM_NB, (uint64_t)w * MSM_NB + j, &acc.x.c0.v[0]);
@@ -179,10 +180,10 @@ BLS_HD BLS_INLINE void msm_segment_lane(uint32_t w, uint32_t s, const uint32_t* 
     const g2j cur = b;
     if (k > 0) soa_load<72>(&b.x.c0.v[0], B, nb, base + k - 1);
     g2j x = R, y;
-    jac_add(y, x, cur);
+    jac_add_body(y, x, cur);
     R = y;
     g2j u = T, v;
-    jac_add(v, u, R);
+    jac_add_body(v, u, R);
     T = v;
   }
   g2j m, out;
