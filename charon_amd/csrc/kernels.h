@@ -1104,7 +1104,7 @@ __global__ void __launch_bounds__(kSumBlock) k_msm_window(const uint32_t* __rest
     g2j p;
     soa_load<72>(&p.x.c0.v[0], Sg, (uint64_t)MSM_WINDOWS * MSM_NSEG, (uint64_t)w * MSM_NSEG + s);
     g2j x = acc, y;
-    jac_add(y, x, p);
+    jac_add_body(y, x, p);
     acc = y;
   }
   g2_block_tree_sum(acc, red);
