@@ -552,11 +552,11 @@ int launch_verify(Context& c, const uint8_t* d_pks, const uint8_t* d_msgs, const
       hipLaunchKernelGGL(k_verify_fused, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs,
                          d_sigs, n, d_status);
     });
-  HIP_TRY(ws.ensure(n * 120 * 4));
+  HIP_TRY(ws.ensure(n * 122 * 4));  // + two decode codes per item for the octet path
   if (use_octets(n)) {
     const unsigned g8 = (unsigned)grid_for(8 * n);
-    int rc = timed(c, "verify_prep8", s, [&] {
-      hipLaunchKernelGGL(bls_fp2p::k_verify_prep8, dim3(2 * g8), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs, n,
+    int rc = timed(c, "verify_prep8", s, [&] {  // three roles: key, signature, hash (verify_lat.hip)
+      hipLaunchKernelGGL(bls_fp2p::k_verify_prep8, dim3(3 * g8), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs, n,
                          (uint32_t*)ws.p, d_status);
     });
     if (rc) return rc;

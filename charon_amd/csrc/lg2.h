@@ -861,8 +861,9 @@ __device__ bool rlc_window_lg2(uint64_t i0, uint64_t i1, const int32_t* status, 
 // (same data, same branches); the even lane maps u0 and the odd lane u1 (SSWU + isogeny, the square-root powers
 // run side by side), the pair swaps the two points after the maps have reconverged, and both lanes form
 // q0 + q1 in hash_to_g2's order and clear the cofactor.  Same Jacobian result as hash_to_g2, on both lanes.
-BLS_CALL __device__ void hash_to_g2_pair(g2j& out, const uint8_t* msg, uint32_t msg_len, const uint8_t* dst,
-                                         uint32_t dst_len, uint32_t m) {
+// q0 + q1 before the cofactor clearing (hash_to_g2_pair's first part; verify_lat.hip clears it on a lane quad)
+BLS_CALL __device__ void hash_to_g2_pair_sum(g2j& s, const uint8_t* msg, uint32_t msg_len, const uint8_t* dst,
+                                             uint32_t dst_len, uint32_t m) {
   uint32_t uni[64];
   expand_message_xmd_256(uni, msg, msg_len, dst, dst_len);
   fp2 u0, u1;
@@ -885,12 +886,17 @@ BLS_CALL __device__ void hash_to_g2_pair(g2j& out, const uint8_t* msg, uint32_t 
   const fp2 u = sel(m, u1, u0), zu = sel(m, zu1, zu0), t = sel(m, t1, t0);
   g2a qa;
   map_to_curve_sswu_tv(qa, u, zu, t);
-  g2j q, qo, q0, q1, s;
+  g2j q, qo, q0, q1;
   iso_map_g2(q, qa);
   pair_swap_words<72>(&qo.x.c0.v[0], &q.x.c0.v[0]);
   sel_words<72>(&q0.x.c0.v[0], m, &qo.x.c0.v[0], &q.x.c0.v[0]);  // the even lane's point (u0)
   sel_words<72>(&q1.x.c0.v[0], m, &q.x.c0.v[0], &qo.x.c0.v[0]);  // the odd lane's point (u1)
   jac_add(s, q0, q1);
+}
+BLS_CALL __device__ void hash_to_g2_pair(g2j& out, const uint8_t* msg, uint32_t msg_len, const uint8_t* dst,
+                                         uint32_t dst_len, uint32_t m) {
+  g2j s;
+  hash_to_g2_pair_sum(s, msg, msg_len, dst, dst_len, m);
   g2_clear_cofactor(out, s);
 }
 

@@ -23,65 +23,153 @@ namespace bls {
 
 constexpr int kOctBlock = 64;
 
-// Stage 1, eight lanes per item (t >> 3): the first ceil(8n / 64) workgroups decode + check pk and sig (herumi's
-// order, k_verify_prep's statuses), the rest hash the messages (lanes 0/1 of each quad split the two SSWU maps,
-// lg2.h hash_to_g2_pair; lanes 2/3 repeat them).  ws: pk (24 x n), H(m) (48 x n), sig (48 x n), SoA.
+// ---------------------------------------------------------------- the hash's cofactor clearing on a lane quad
+// G2 doubling (curve.h jac_dbl_body, dbl-2009-l) with its seven Fp2 products dealt out over the quad's lanes
+// (q = lane & 3): level 1 X^2 | Y^2 | Y Z, level 2 B^2 | (X + B)^2 | E^2, level 3 E (D - X3) on every lane; each level's
+// products are broadcast to the quad (lg2.h quad_bcast).  Three products of latency instead of seven; every lane
+// ends with the same point.  All four lanes (and, here, their Fp2 twins) must be active.
+__device__ __forceinline__ void g2_dbl_quad(g2j& r, const g2j& p, int q) {
+  const uint32_t q1 = q == 1 ? ~0u : 0u, q2 = q == 2 ? ~0u : 0u;
+  fp2 x, y, o;
+  x = sel(q2, p.y, sel(q1, p.y, p.x));
+  y = sel(q2, p.z, sel(q1, p.y, p.x));
+  fp2_mul(o, x, y);  // X^2 | Y^2 | Y Z
+  const fp2 A = quad_bcast<0>(o), B = quad_bcast<1>(o), YZ = quad_bcast<2>(o);
+  fp2 XB, E;
+  fp2_add(XB, p.x, B);
+  fp2_add(E, A, A);
+  fp2_add(E, E, A);
+  x = sel(q2, E, sel(q1, XB, B));
+  fp2_mul(o, x, x);  // C = B^2 | (X + B)^2 | F = E^2
+  const fp2 C = quad_bcast<0>(o), T = quad_bcast<1>(o), Fv = quad_bcast<2>(o);
+  fp2 t, D, x3, c8;
+  fp2_sub(t, T, A);
+  fp2_sub(t, t, C);
+  fp2_add(D, t, t);
+  fp2_sub(x3, Fv, D);
+  fp2_sub(x3, x3, D);
+  fp2_sub(t, D, x3);
+  fp2_mul(t, E, t);
+  fp2_add(c8, C, C);
+  fp2_add(c8, c8, c8);
+  fp2_add(c8, c8, c8);
+  fp2_sub(r.y, t, c8);
+  fp2_add(r.z, YZ, YZ);
+  r.x = x3;
+}
+
+// [|x|] p with the doublings on the quad (the additions, at |x|'s six set bits, on every lane)
+__device__ void g2_mul_xabs_quad(g2j& r, const g2j& p_in, int q) {
+  const g2j p = p_in;
+  g2j acc = p;
+  for (int i = 62; i >= 0; --i) {
+    g2j t;
+    g2_dbl_quad(t, acc, q);
+    acc = t;
+    if ((X_ABS >> i) & 1ull) {
+      g2j u = acc;
+      jac_add(acc, u, p);
+    }
+  }
+  r = acc;
+}
+
+// curve.h g2_clear_cofactor (Budroni-Pintore) with its two [x] multiplications on the quad
+__device__ void g2_clear_cofactor_quad(g2j& r, const g2j& p_in, int q) {
+  const g2j p = p_in;
+  g2j t1, t2, t3, np, nt1, nt2;
+  g2_mul_xabs_quad(t1, p, q);
+  jac_neg(t1, t1);  // [x] P
+  g2_psi(t2, p);
+  jac_dbl(t3, p);
+  g2_psi2(t3, t3);
+  jac_neg(nt2, t2);
+  jac_add(t3, t3, nt2);  // psi^2(2P) - psi(P)
+  jac_add(t2, t1, t2);   // [x] P + psi(P)
+  g2_mul_xabs_quad(t2, t2, q);
+  jac_neg(t2, t2);
+  jac_add(t3, t3, t2);
+  jac_neg(nt1, t1);
+  jac_add(t3, t3, nt1);
+  jac_neg(np, p);
+  jac_add(r, t3, np);
+}
+
+// Stage 1, eight lanes per item (t >> 3), three roles per set of workgroups (uniform per workgroup, so they run side
+// by side on different SIMDs): decode + check the key, decode the signature, hash the message (lanes 0/1 of each
+// quad split the two SSWU maps, lg2.h hash_to_g2_pair_sum, and the quad clears the cofactor).  The decode codes go
+// to ws + 120 n (two words per item); k_verify_pair_lq8 composes the status in herumi's order.  ws: pk (24 x n),
+// H(m) (48 x n), sig (48 x n), SoA.
 __global__ void __launch_bounds__(kOctBlock) k_verify_prep8(const uint8_t* __restrict__ pks,
                                                             const uint8_t* __restrict__ msgs,
                                                             const uint64_t* __restrict__ offs,
                                                             const uint8_t* __restrict__ sigs, uint64_t n,
                                                             uint32_t* __restrict__ ws, int32_t* __restrict__ status) {
+  (void)status;  // k_verify_pair_lq8 writes every status
   const uint64_t nb = (8 * n + kOctBlock - 1) / kOctBlock;
-  const bool hash_role = blockIdx.x >= nb;  // uniform per workgroup
-  const uint64_t t = (blockIdx.x - (hash_role ? nb : 0)) * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t role = blockIdx.x / nb;  // 0 key, 1 signature, 2 hash: uniform per workgroup
+  const uint64_t t = (blockIdx.x - role * nb) * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t i = t >> 3;
   if (i >= n) return;  // the same on all eight lanes
   const bool lead = (t & 7) == 0;
-  if (hash_role) {
+  int32_t* codes = (int32_t*)(ws + 120 * n);
+  if (role == 2) {
     const uint32_t m = (t & 1) ? ~0u : 0u;
     const uint64_t o0 = offs[i], o1 = offs[i + 1];
-    g2j hj;
-    hash_to_g2_pair(hj, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43, m);
+    g2j sum, hj;
+    hash_to_g2_pair_sum(sum, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43, m);
+    g2_clear_cofactor_quad(hj, sum, (int)(t & 3));
     g2a hm;
     jac_to_aff(hm, hj);
     if (lead) soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);
     return;
   }
-  g1a pk;
-  g2a sig;
-  int st = RLC_PENDING;
-  const int dp = g1_decompress(pk, pks + 48 * i, true);
-  if (dp == DEC_BAD) {
-    st = HIPBLS_ERR_PUBKEY;
-  } else {
-    const int ds = g2_decompress(sig, sigs + 96 * i, false);  // G2 membership: from the signature's Miller loop
-    if (ds == DEC_BAD)
-      st = HIPBLS_ERR_SIGNATURE;
-    else if (dp == DEC_INF || ds == DEC_INF)
-      st = verify_inf_status(ds, sig);
-  }
-  if (lead) {
-    if (st == RLC_PENDING) {
-      soa_store<24>(ws, n, i, &pk.x.v[0]);
-      soa_store<48>(ws + 72 * n, n, i, &sig.x.c0.v[0]);
+  if (role == 0) {
+    g1a pk;
+    const int dp = g1_decompress(pk, pks + 48 * i, true);
+    if (lead) {
+      codes[2 * i] = dp;
+      if (dp == DEC_OK) soa_store<24>(ws, n, i, &pk.x.v[0]);
     }
-    status[i] = st;
+    return;
+  }
+  g2a sig;
+  const int ds = g2_decompress(sig, sigs + 96 * i, false);  // G2 membership: from the signature's Miller loop
+  if (lead) {
+    codes[2 * i + 1] = ds;
+    if (ds == DEC_OK) soa_store<48>(ws + 72 * n, n, i, &sig.x.c0.v[0]);
   }
 }
 
-// Stage 2, eight lanes per item: lq4_verify on lanes 0-3 (q = t & 3) and, as their Fp2 twins, on 4-7.
+// Stage 2, eight lanes per item: the status from the decode codes in herumi's order (key, then signature, then the
+// infinity cases), then lq4_verify on lanes 0-3 (q = t & 3) and, as their Fp2 twins, on 4-7.
 __global__ void __launch_bounds__(kOctBlock) k_verify_pair_lq8(const uint32_t* __restrict__ ws, uint64_t n,
                                                                int32_t* __restrict__ status) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t i = t >> 3;
-  if (i >= n || status[i] != RLC_PENDING) return;  // the same on all eight lanes
+  if (i >= n) return;  // the same on all eight lanes
+  const int32_t* codes = (const int32_t*)(ws + 120 * n);
+  const int dp = codes[2 * i], ds = codes[2 * i + 1];
+  const bool lead = (t & 7) == 0;
+  g2a sig;
+  if (ds == DEC_OK) soa_load<48>(&sig.x.c0.v[0], ws + 72 * n, n, i);
+  int st = RLC_PENDING;
+  if (dp == DEC_BAD)
+    st = HIPBLS_ERR_PUBKEY;
+  else if (ds == DEC_BAD)
+    st = HIPBLS_ERR_SIGNATURE;
+  else if (dp == DEC_INF || ds == DEC_INF)
+    st = verify_inf_status(ds, sig);  // KeyValidate / e(pk, H) != 1
+  if (st != RLC_PENDING) {
+    if (lead) status[i] = st;
+    return;
+  }
   g1a pk;
-  g2a hm, sig;
+  g2a hm;
   soa_load<24>(&pk.x.v[0], ws, n, i);
   soa_load<48>(&hm.x.c0.v[0], ws + 24 * n, n, i);
-  soa_load<48>(&sig.x.c0.v[0], ws + 72 * n, n, i);
-  const int st = lq4_verify(pk, hm, sig, (int)(t & 3));
-  if ((t & 7) == 0) status[i] = st;
+  st = lq4_verify(pk, hm, sig, (int)(t & 3));
+  if (lead) status[i] = st;
 }
 
 // ---------------------------------------------------------------- the batch-wide RLC check's tail (rlcb.h)
