@@ -459,7 +459,8 @@ def main():
         latency = {"calls": k, "p50_ms": round(1000 * lat[k // 2], 3), "p90_ms": round(1000 * lat[(9 * k) // 10], 3),
                    "min_ms": round(1000 * lat[0], 3), "serial_verifies_per_s": round(k / tot, 1),
                    "seconds_per_1000_serial": round(1000 * tot / k, 2),
-                   "path": "hipbls_verify (submission queue, n = 1 batch: prep + lane-quad pairing check)"}
+                   "path": "hipbls_verify (submission queue, n = 1 batch: eight-lane prep + pairing check, "
+                           "verify_lat.hip)"}
 
     # ---- C2 with the resident pubshare table (extra field): same items, keys by index
     keys_rate = None
@@ -785,9 +786,10 @@ def main():
             out["rlc_batch_verify"] = dict(rlc, workload="C4 (BASELINE configs[3]): the %d-validator x 4-partial node "
                                                         "batch sliced over %d GPU(s) by validator index (strong "
                                                         "scaling), items grouped by validator, ~1%% corrupted (i, ii) "
-                                                        "or all valid (i_all_valid: decided by the batch-wide "
-                                                        "Pippenger check of rlcb.h alone), windows of 8 items for the "
-                                                        "rest, per-item bitmap == tbls.Verify, node bitmap "
+                                                        "or all valid (i_all_valid, ii_all_valid: decided by the "
+                                                        "batch-wide Pippenger check of rlcb.h alone; ii with one G1 "
+                                                        "MSM per committee root, g1msm.h), windows of 8 items for "
+                                                        "the rest, per-item bitmap == tbls.Verify, node bitmap "
                                                         "all-gathered" % (args.rlc_node_validators, world))
         k_ms = avg_ms.value
         if k_ms > 0:
