@@ -152,3 +152,45 @@ def test_verdict_ring_wraps(impl, keys):
     a1, p1, last = impl.rlc_batch_stats()
     assert got[0] == 3 and got[1:] == [0] * (len(P) - 1)
     assert (a1 - a0, p1 - p0, last) == (12, 11, 0)
+
+
+def test_g1_msm_edges(impl, keys):
+    """The G1 MSM per committee root (g1msm.h) at its edges, against per-item Verify and the batch verdict:
+    a large root whose every item fails to decode (zero scalars: an empty sum, Miller value 1), the G1 path taken
+    with no root large enough (40 roots x 12 items: the kernels run with nl = 0), every root large (threshold 1),
+    and the resident key table with committee roots (keys from the table into the slots)."""
+    from charon_amd.tbls import RLC_BATCH
+    sks, pks = keys
+    # (a) root 0's 80 items all broken, root 1's 80 honest
+    idx, P, M, S = _batch(impl, keys, 40, 4, 41, n_roots=2)
+    for i in range(80):
+        b = bytearray(S[i])
+        b[0] &= 0x7F  # compression flag cleared: ERR_SIGNATURE in stage 1
+        S[i] = bytes(b)
+    want = impl.batch_verify_status(P, M, S)
+    assert want == [2] * 80 + [0] * 80
+    got, att, passed, last = _run(impl, RLC_BATCH, P, M, S)
+    assert got == want and (att, passed, last) == (1, 1, 1)
+    # (b) G1 path on, no large root
+    _, P, M, S = _batch(impl, keys, 120, 4, 42, n_roots=40)
+    got, att, passed, last = _run(impl, RLC_BATCH, P, M, S)
+    assert got == [0] * 480 and (att, passed, last) == (1, 1, 1)
+    # (c) every root large; one swapped pair inside a root still caught
+    old = impl.set_rlc_g1_msm_min(1)
+    try:
+        _, P, M, S = _batch(impl, keys, 128, 4, 43, n_roots=8)
+        got, att, passed, last = _run(impl, RLC_BATCH, P, M, S)
+        assert got == [0] * 512 and (att, passed, last) == (1, 1, 1)
+        S[20], S[21] = S[21], S[20]
+        got, att, passed, last = _run(impl, RLC_BATCH, P, M, S)
+        assert (att, passed, last) == (1, 0, 0) and got == [0] * 20 + [3, 3] + [0] * 490
+    finally:
+        impl.set_rlc_g1_msm_min(old)
+    # (d) resident key table, committee roots
+    assert set(impl.load_pubshares(pks)) == {0}
+    idx, P, M, S = _batch(impl, keys, 512, 4, 44, n_roots=4)
+    impl.set_rlc_mode(RLC_BATCH)
+    a0, p0, _ = impl.rlc_batch_stats()
+    got = impl.batch_verify_rlc_keys_status(idx, M, S, seed=bytes(32))
+    a1, p1, last = impl.rlc_batch_stats()
+    assert got == [0] * len(idx) and (a1 - a0, p1 - p0, last) == (1, 1, 1)
