@@ -537,7 +537,8 @@ __device__ __forceinline__ uint32_t quad_swap(uint32_t v) {
 //     the pairs combine theirs into c0 = a0 b0 + v a1 b1 (lanes 0, 1) and c1 = a0 b1 + a1 b0 (lanes 2, 3), and one
 //     exchange across the pairs gives every lane both halves: one Fp6 product per lane instead of two on a pair;
 //   * Karabina's compressed squaring: its six Fp2 squarings as two rounds of four (z2 | z3 | z4 | z5, then
-//     z2 + z3 | z4 + z5 on lanes 0, 1), each result broadcast to the quad: two squarings of latency instead of three.
+//     z2 + z3 | z4 + z5 on lanes 0, 1): two squarings of latency instead of three; then each lane forms one of the
+//     four new coordinates and the quad broadcasts them (half the additions per lane).
 // Everything else (decompression, the easy part's inversion, Frobenius maps) runs redundantly on all lanes on the
 // same data, so every branch is quad-uniform (DPP needs all four lanes).
 template <int SRC>
@@ -584,8 +585,23 @@ BLS_CALL __device__ void fp12q_mul(fp12& r, const fp12& a_in, const fp12& b_in, 
   r.c1 = sel(qm.hi, mine, other);
 }
 
+// Arbitrary permutation within each quad: lane i takes lane CTRL's 2-bit field i (quad_perm [p0, p1, p2, p3]).
+template <int CTRL>
+__device__ __forceinline__ fp2 quad_perm(const fp2& s) {
+  fp2 d;
+#pragma unroll
+  for (int i = 0; i < 24; ++i)
+    (&d.c0.v[0])[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(&s.c0.v[0])[i], CTRL, 0xF, 0xF, false);
+  return d;
+}
+
+// The six Fp2 squarings as two rounds of four, then each lane forms ONE new coordinate (z2' | z3' | z4' | z5') from the
+// squares it needs (three DPP permutations bring them) and the quad broadcasts the four: the additions after the
+// squarings are ~11 Fp2 operations per lane instead of every lane forming all four coordinates (22).
+//   lane 0: z2' = 2 z2 + 3 xi ((z4 + z5)^2 - z4^2 - z5^2)     lane 1: z3' = 3 (z4^2 + xi z5^2) - 2 z3
+//   lane 2: z4' = 3 (z2^2 + xi z3^2) - 2 z4                    lane 3: z5' = 2 z5 + 3 ((z2 + z3)^2 - z2^2 - z3^2)
 __device__ __forceinline__ void cyc_sqr_compressed_quad(cyc_c& c, const quad_m& qm) {
-  // round 1: z2 | z3 | z4 | z5
+  // round 1: z2 | z3 | z4 | z5 (also this lane's own coordinate)
   const fp2 xa = sel(qm.hi, sel(qm.odd, c.z5, c.z4), sel(qm.odd, c.z3, c.z2));
   // round 2: z2 + z3 | z4 + z5 (lanes 2, 3 repeat lanes 0, 1)
   fp2 s23, s45;  // canonical: the squaring routine forms a0 + p - a1
@@ -595,32 +611,25 @@ __device__ __forceinline__ void cyc_sqr_compressed_quad(cyc_c& c, const quad_m& 
   fp2 ra, rb;
   BLS_KAR_FP2_SQR(ra, xa);
   BLS_KAR_FP2_SQR(rb, xb);
-  const fp2 s2 = quad_bcast<0>(ra), s3 = quad_bcast<1>(ra), s4 = quad_bcast<2>(ra), s5 = quad_bcast<3>(ra);
-  fp2 u = quad_bcast<0>(rb), t = quad_bcast<1>(rb);
-  fp2 v;
-  fp2_sub(t, t, s4);
-  fp2_sub(t, t, s5);  // 2 z4 z5
-  fp2_sub(u, u, s2);
-  fp2_sub(u, u, s3);  // 2 z2 z3
-  // the new state as cyc_sqr_compressed (pairing.h)
-  fp2 q45, q23;
-  fp2_mul_xi(t, t);
-  fp2_add(v, c.z2, t);
-  fp2_add(v, v, v);
-  fp2_add(c.z2, v, t);
-  fp2_mul_xi(q45, s5);
-  fp2_add(q45, q45, s4);
-  fp2_sub(v, q45, c.z3);
-  fp2_add(v, v, v);
-  fp2_add(c.z3, v, q45);
-  fp2_mul_xi(q23, s3);
-  fp2_add(q23, q23, s2);
-  fp2_sub(v, q23, c.z4);
-  fp2_add(v, v, v);
-  fp2_add(c.z4, v, q23);
-  fp2_add(v, c.z5, u);
-  fp2_add(v, v, v);
-  fp2_add(c.z5, v, u);
+  const fp2 X = quad_perm<0x0A>(ra);  // [2, 2, 0, 0]: z4^2 | z4^2 | z2^2 | z2^2
+  const fp2 Y = quad_perm<0x5F>(ra);  // [3, 3, 1, 1]: z5^2 | z5^2 | z3^2 | z3^2
+  const fp2 W = quad_perm<0x05>(rb);  // [1, 1, 0, 0]: (z4 + z5)^2 on lane 0, (z2 + z3)^2 on lane 3
+  fp2 A, B, xiA, xiY, zz, nzz, V3, out;
+  fp2_sub(A, W, X);
+  fp2_sub(A, A, Y);  // 2 z4 z5 (lane 0) | 2 z2 z3 (lane 3)
+  fp2_mul_xi(xiY, Y);
+  fp2_add(B, xiY, X);  // z4^2 + xi z5^2 (lane 1) | z2^2 + xi z3^2 (lane 2)
+  fp2_mul_xi(xiA, A);
+  const fp2 V = sel(qm.cross, B, sel(qm.odd, A, xiA));
+  fp2_add(V3, V, V);
+  fp2_add(V3, V3, V);
+  fp2_add(zz, xa, xa);
+  fp2_neg(nzz, zz);
+  fp2_add(out, V3, sel(qm.cross, nzz, zz));  // 3 V + 2 z (lanes 0, 3) | 3 V - 2 z (lanes 1, 2)
+  c.z2 = quad_bcast<0>(out);
+  c.z3 = quad_bcast<1>(out);
+  c.z4 = quad_bcast<2>(out);
+  c.z5 = quad_bcast<3>(out);
 }
 
 // r = a^|x| on a quad (a in the cyclotomic subgroup, in full on every lane), pairing.h fp12_cyc_exp_xabs_karabina's

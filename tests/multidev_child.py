@@ -47,6 +47,12 @@ def main():
     _check(impl.lib.hipbls_batch_verify_rlc_keys(kidx, b"".join(rs), idx, n, blob, offs, len(roots), os.urandom(32),
                                                  st2), impl.lib)
     out["rlc_keys"] = np.array(list(st2), dtype=np.int32)
+    # committee roots in the batch-wide mode: each context's range takes the G1 MSM per root
+    from charon_amd.tbls import RLC_AUTO, RLC_BATCH
+    cp, cs, cm, croots = rows(d["c_pk"], 48), rows(d["c_sig"], 96), d["c_midx"].tolist(), rows(d["c_roots"], 32)
+    impl.set_rlc_mode(RLC_BATCH)
+    out["rlc_committee"] = np.array(impl.batch_verify_rlc_status(cp, [croots[m] for m in cm], cs), dtype=np.int32)
+    impl.set_rlc_mode(RLC_AUTO)
     m12 = [roots[m] for m in rm[:12288].tolist()]
     out["verify_keys"] = np.array(impl.batch_verify_keys_status([pos[p] for p in rp[:12288]], m12, rs[:12288]),
                                   dtype=np.int32)

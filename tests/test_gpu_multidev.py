@@ -47,6 +47,9 @@ def test_three_contexts_equal_unsplit(impl, tmp_path):
     # RLC: 12,288 validators x 4 partials (3 ranges of 16,384), ~1% corrupted
     keys4 = bench.share_keys(impl, 512, "md4")
     rp, rs, rm, rroots, rbad = bench.make_c4(impl, keys4, "md4", 0, 12288, 12288)
+    # RLC with committee roots (the batch-wide check's G1 MSM per root in every range): 2,048 validators x 4 over
+    # 24 roots, ~1% corrupted, in the batch-wide mode
+    cp, cs, cm, croots, cbad = bench.make_c4(impl, keys4, "md4c", 0, 2048, 2048, 24)
     # ThresholdAggregate: 3,072 validators x 3-of-5, with a few failing groups
     t_sig, t_ids, t_off, t_dvpk, t_root = [], [], [0], [], []
     for g in range(3072):
@@ -91,6 +94,7 @@ def test_three_contexts_equal_unsplit(impl, tmp_path):
     a_sig = (good * 17)[:196608]
     np.savez(tmp_path / "in.npz", v_pk=_u8(pks), v_msg=_u8(roots), v_sig=_u8(sigs), v_obj=_u8(objs), v_dom=_u8(doms),
              r_pk=_u8(rp), r_sig=_u8(rs), r_midx=np.array(rm, dtype=np.uint32), r_roots=_u8(rroots),
+             c_pk=_u8(cp), c_sig=_u8(cs), c_midx=np.array(cm, dtype=np.uint32), c_roots=_u8(croots),
              t_sig=_u8(flat_sig), t_ids=np.array(t_ids, dtype=np.int64), t_off=np.array(t_off, dtype=np.int64),
              t_dvpk=_u8(dvpks), t_root=_u8(t_root), s_sk=_u8(s_sk), s_msg=_u8(s_msg), f_pk=_u8(fpk),
              f_off=np.arange(0, 769, 4, dtype=np.int64), f_sig=_u8(f_sig), f_msg=_u8(f_msg_used), a_sig=_u8(a_sig))
@@ -106,6 +110,13 @@ def test_three_contexts_equal_unsplit(impl, tmp_path):
     want["rlc"] = list(st)
     assert {i for i, s in enumerate(want["rlc"]) if s} == rbad
     want["rlc_keys"] = want["rlc"]
+    from charon_amd.tbls import RLC_AUTO, RLC_BATCH
+    impl.set_rlc_mode(RLC_BATCH)
+    try:
+        want["rlc_committee"] = impl.batch_verify_rlc_status(cp, [croots[m] for m in cm], cs)
+    finally:
+        impl.set_rlc_mode(RLC_AUTO)
+    assert {i for i, s in enumerate(want["rlc_committee"]) if s} == cbad
     want["verify_keys"] = want["rlc"][:12288]
     groups = [dict(zip(t_ids[t_off[g]:t_off[g + 1]], flat_sig[t_off[g]:t_off[g + 1]])) for g in range(3072)]
     res = impl.batch_threshold_aggregate(groups)
@@ -130,7 +141,7 @@ def test_three_contexts_equal_unsplit(impl, tmp_path):
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     got = np.load(tmp_path / "out.npz", allow_pickle=False)
-    for key in ("verify", "rlc", "rlc_keys", "verify_keys", "tagg_vst", "fav", "signed", "queue"):
+    for key in ("verify", "rlc", "rlc_keys", "rlc_committee", "verify_keys", "tagg_vst", "fav", "signed", "queue"):
         assert got[key].tolist() == list(want[key]), key
     for key in ("tagg", "tagg_v", "sign", "pk", "agg"):
         assert got[key].tobytes() == want[key], key
