@@ -391,7 +391,11 @@ def main():
     impl = HipBLS(device=local_dev)
     lib = load_library()
     lib.hipbls_set_timing(1)  # per-kernel HIP events for the roofline (off by default in the library)
-    stream = torch.cuda.current_stream(dev)
+    # A stream of our own, made current: the library's *_device calls enqueue on it, and the bitmap packing and the
+    # collectives that read their results run after them on the same stream.  (The default stream's handle is 0,
+    # which the library reads as "my own stream": nothing would order the gathers behind its kernels.)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     sp = ctypes.c_void_p(stream.cuda_stream)
 
     def barrier():
@@ -526,7 +530,9 @@ def main():
         assert bytes(d_agg.cpu().numpy().tobytes()) == b"".join(want_aggs), "C3 aggregate bytes != Sign(secret)"
         if world > 1:
             assert torch.equal(node_aggs[0][96 * g_lo:96 * g_hi], d_agg), "gathered aggregates differ from local"
-            assert bool(node_aggs[1].all()), "an aggregate of the node batch failed Verify"
+            bad_g = (~node_aggs[1]).nonzero().flatten().tolist()
+            assert not bad_g, "an aggregate of the node batch failed Verify: %d groups, first %s (this rank's slice " \
+                              "[%d, %d))" % (len(bad_g), bad_g[:8], g_lo, g_hi)
         tagg = G_node * args.tagg_steps / tel
         # C3 roofline: the counted per-aggregate unit over the whole call's wall time (the pipeline), and per stage over
         # its kernel's average launch time (HIP events on the launch stream)
