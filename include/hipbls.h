@@ -238,7 +238,9 @@ int hipbls_hcache_stats(uint64_t* hits, uint64_t* misses, uint64_t* entries);
 
 /* ------------------------------------------- device-resident variants (inputs already in HBM) ---- */
 /* Same semantics; every pointer is a device pointer; work is enqueued on `stream` (a hipStream_t,
- * NULL = the library's stream of that device) and the call returns without synchronizing.  The call runs on the
+ * NULL = the library's own non-blocking stream of that device, which is NOT ordered with the caller's default
+ * stream: a caller that reads the results with other work must pass that work's stream) and the call returns
+ * without synchronizing.  The call runs on the
  * device that owns the status array. */
 int hipbls_verify_batch_device(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
                                const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream);
