@@ -325,10 +325,8 @@ BLS_HD BLS_INLINE void rlcb_mark_lane(uint64_t i, uint64_t n, bool pass, int32_t
   g2a s, ps;
   aos_load<48>(&s.x.c0.v[0], pts, i);
   aos_load<48>(&ps.x.c0.v[0], pts, n + i);
-  g2j sj, psj, rs;
-  jac_from_aff(sj, s);
-  jac_from_aff(psj, ps);
-  jac_mul2_u32(rs, sj, psj, sc[i], sc[n + i]);
+  g2j rs;
+  jac_mul2_u32_aff(rs, s, ps, sc[i], sc[n + i]);
   soa_store<72>(rsig, n, i, &rs.x.c0.v[0]);
 }
 
