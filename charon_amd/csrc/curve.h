@@ -240,7 +240,7 @@ BLS_HD BLS_CALL void jac_mul_u64(jac<F>& r, const jac<F>& p_in, uint64_t k) {
       acc = t;
       if ((k >> i) & 1ull) {
         jac<F> x = acc, y;
-        jac_add(y, x, p_in);
+        jac_add_body(y, x, p_in);  // inlined (one copy per field type): no scratch round trip per addition
         acc = y;
       }
     }
@@ -259,7 +259,7 @@ BLS_HD BLS_CALL void jac_mul_limbs(jac<F>& r, const jac<F>& p_in, const uint32_t
     acc = t;
     if ((k[i >> 5] >> (i & 31)) & 1u) {
       jac<F> x = acc, y;
-      jac_add(y, x, p_in);
+      jac_add_body(y, x, p_in);
       acc = y;
     }
   }

@@ -188,13 +188,13 @@ BLS_HD BLS_CALL bool g2_subgroup_and_mul_i64(g2j& out, const g2j& sj, int64_t c)
   jac_set_inf(ax);
   jac_set_inf(ac);
   for (int i = 0; i < 64; ++i) {
-    if ((X_ABS >> i) & 1ull) {
+    if ((X_ABS >> i) & 1ull) {  // wave-uniform, six times: the called addition
       g2j t = ax;
       jac_add(ax, t, pw);
     }
-    if ((k >> i) & 1ull) {
+    if ((k >> i) & 1ull) {  // per lane, up to 64 times: inlined
       g2j t = ac;
-      jac_add(ac, t, pw);
+      jac_add_body(ac, t, pw);
     }
     if (i < 63 && ((X_ABS | k) >> (i + 1)) != 0) {
       g2j t;
