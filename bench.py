@@ -77,7 +77,7 @@ def parse():
                          "invalid partial), ii_all_valid (ii, no invalid partial)")
     ap.add_argument("--c5", type=int, default=1, help="time the C5 full-slot mix (0 = skip)")
     ap.add_argument("--keys", type=int, default=1, help="also time C2 / C4 with the resident pubshare table (0 = skip)")
-    ap.add_argument("--latency-calls", type=int, default=200,
+    ap.add_argument("--latency-calls", type=int, default=1000,
                     help="synchronous n = 1 tbls.Verify calls (hipbls_verify on an idle queue) timed one after another, "
                          "the unpatched parsigex loop's shape (0 = skip; rank 0 only)")
     return ap.parse_args()
