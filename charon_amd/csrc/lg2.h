@@ -305,7 +305,8 @@ __device__ __forceinline__ void fp12h_exp(fp6& r, const fp6& a_in, uint32_t m) {
 #endif
 }
 
-// final_exponentiation (pairing.h) on a split value: same formula, split operations.
+// final_exponentiation (pairing.h) on a split value: same formula, split operations; the products inlined (as the
+// quad's fp12q_mul: a call sends its operands through the stack).
 BLS_CALL __device__ void final_exponentiation_split(fp6& r, const fp6& f_in, uint32_t m) {
   // temporaries scoped so their frame slots can be shared (pairing_lds.h final_exponentiation_l); r may alias f_in
   fp6 mm;
@@ -319,24 +320,24 @@ BLS_CALL __device__ void final_exponentiation_split(fp6& r, const fp6& f_in, uin
       fi = sel(m, inv.c1, inv.c0);
     }
     fp12h_conj(t, f_in, m);
-    fp12h_mul(mm, t, fi, m);
+    fp12h_mul_inl(mm, t, fi, m);
     fp12h_frobenius(t, mm, 2, m);
-    fp12h_mul(mm, t, mm, m);
+    fp12h_mul_inl(mm, t, mm, m);
   }
   // hard part
   fp6 t1;
   {
     fp6 t0, u;
     fp12h_exp(t0, mm, m);
-    fp12h_mul(t0, t0, mm, m);
+    fp12h_mul_inl(t0, t0, mm, m);
     fp12h_conj(t0, t0, m);
     fp12h_exp(u, t0, m);
-    fp12h_mul(u, u, t0, m);
+    fp12h_mul_inl(u, u, t0, m);
     fp12h_conj(t0, u, m);
     fp12h_exp(u, t0, m);
     fp12h_conj(u, u, m);
     fp12h_frobenius(t1, t0, 1, m);
-    fp12h_mul(t1, t1, u, m);
+    fp12h_mul_inl(t1, t1, u, m);
   }
   fp6 t2;
   {
@@ -344,15 +345,15 @@ BLS_CALL __device__ void final_exponentiation_split(fp6& r, const fp6& f_in, uin
     fp12h_exp(u, t1, m);
     fp12h_exp(u, u, m);
     fp12h_frobenius(t2, t1, 2, m);
-    fp12h_mul(t2, t2, u, m);
+    fp12h_mul_inl(t2, t2, u, m);
     fp12h_conj(u, t1, m);
-    fp12h_mul(t2, t2, u, m);
+    fp12h_mul_inl(t2, t2, u, m);
   }
   {
     fp6 u;
     fp12h_cyc_sqr(u, mm, m);
-    fp12h_mul(u, u, mm, m);
-    fp12h_mul(r, t2, u, m);
+    fp12h_mul_inl(u, u, mm, m);
+    fp12h_mul_inl(r, t2, u, m);
   }
 }
 
@@ -566,7 +567,12 @@ struct quad_m {  // lane masks within the quad (q = lane & 3)
       : odd((q & 1) ? ~0u : 0u), hi((q & 2) ? ~0u : 0u), cross(((q ^ (q >> 1)) & 1) ? ~0u : 0u) {}
 };
 
-BLS_CALL __device__ void fp12q_mul(fp12& r, const fp12& a_in, const fp12& b_in, const quad_m& qm) {
+// Inlined into its callers: as a call, its two 576-byte operands and result go through the stack around every product
+// (profiles/r04/oct_probe*.txt: fp12q_mul 55.8k -> 41.3k cycles, the quad final exponentiation 13.3M -> 10.2M).
+#ifndef BLS_FP12Q_MUL_ATTR
+#define BLS_FP12Q_MUL_ATTR static __forceinline__
+#endif
+BLS_FP12Q_MUL_ATTR __device__ void fp12q_mul(fp12& r, const fp12& a_in, const fp12& b_in, const quad_m& qm) {
   const fp12 a = a_in, b = b_in;
   const fp6 x = sel(qm.odd, a.c1, a.c0);    // a0 | a1 | a0 | a1
   const fp6 y = sel(qm.cross, b.c1, b.c0);  // b0 | b1 | b1 | b0
