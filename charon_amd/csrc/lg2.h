@@ -638,6 +638,18 @@ __device__ __forceinline__ void cyc_sqr_compressed_quad(cyc_c& c, const quad_m& 
   c.z5 = quad_bcast<3>(out);
 }
 
+template <int SRC>
+__device__ __forceinline__ void quad_bcast12(fp12& d, const fp12& s) {
+#pragma unroll
+  for (int i = 0; i < 144; ++i) (&d.c0.c0.c0.v[0])[i] = quad_bcast<SRC>((&s.c0.c0.c0.v[0])[i]);
+}
+__device__ __forceinline__ void cyc_sel(cyc_c& r, uint32_t m, const cyc_c& if_set, const cyc_c& if_clear) {
+  r.z2 = sel(m, if_set.z2, if_clear.z2);
+  r.z3 = sel(m, if_set.z3, if_clear.z3);
+  r.z4 = sel(m, if_set.z4, if_clear.z4);
+  r.z5 = sel(m, if_set.z5, if_clear.z5);
+}
+
 // r = a^|x| on a quad (a in the cyclotomic subgroup, in full on every lane), pairing.h fp12_cyc_exp_xabs_karabina's
 // steps; the degenerate case (a saved power with z2 = z3 = 0) takes the one-lane Granger-Scott exponentiation on
 // every lane.
@@ -657,35 +669,68 @@ BLS_CALL __device__ bool fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, cons
     cyc_sqr_compressed_quad(c, qm);
     if (k == 16 || k == 48 || k == 57 || k == 60 || k == 62 || k == 63) st[s++] = c;
   }
-  fp2 num[6], den[6], pre[6];
-#pragma unroll 1
-  for (s = 0; s < 6; ++s) cyc_z1_parts(num[s], den[s], st[s]);
+  // The six powers' z1 parts and decompressions are dealt out over the quad (lane q takes powers q and, on lanes 0
+  // and 1, q + 4: two rounds instead of six), then broadcast; the batch inversion and the products stay shared.
+  cyc_c cA, cB;
+  cyc_sel(cA, qm.odd, st[1], st[0]);
+  {
+    cyc_c hi;
+    cyc_sel(hi, qm.odd, st[3], st[2]);
+    cyc_sel(cA, qm.hi, hi, cA);
+  }
+  cyc_sel(cB, qm.odd, st[5], st[4]);
+  fp2 nA, dA, nB, dB;
+  cyc_z1_parts(nA, dA, cA);
+  cyc_z1_parts(nB, dB, cB);
+  const fp2 den[6] = {quad_bcast<0>(dA), quad_bcast<1>(dA), quad_bcast<2>(dA), quad_bcast<3>(dA), quad_bcast<0>(dB),
+                      quad_bcast<1>(dB)};
+  fp2 pre[6];
   pre[0] = den[0];
-#pragma unroll 1
+#pragma unroll
   for (s = 1; s < 6; ++s) fp2_mul(pre[s], pre[s - 1], den[s]);
   if (fp2_is_zero(pre[5])) return true;  // the same on all four lanes
   fp2 inv;
   fp2_inv(inv, pre[5]);
-  fp12 acc;
-#pragma unroll 1
-  for (s = 5; s >= 0; --s) {
-    fp2 is, z1;
-    if (s > 0) {
-      fp2_mul(is, inv, pre[s - 1]);  // 1 / den[s]
-      fp2_mul(inv, inv, den[s]);
-    } else {
-      is = inv;
-    }
-    fp2_mul(z1, num[s], is);
-    fp12 d;
-    cyc_decompress(d, st[s], z1);
-    if (s == 5) {
-      acc = d;
-    } else {
-      fp12 x = acc, y;
-      fp12q_mul(y, x, d, qm);
-      acc = y;
-    }
+  fp2 is[6];  // 1 / den[s] by back-substitution
+#pragma unroll
+  for (s = 5; s > 0; --s) {
+    fp2_mul(is[s], inv, pre[s - 1]);
+    fp2_mul(inv, inv, den[s]);
+  }
+  is[0] = inv;
+  fp2 z1A, z1B;
+  fp2_mul(z1A, nA, sel(qm.hi, sel(qm.odd, is[3], is[2]), sel(qm.odd, is[1], is[0])));
+  fp2_mul(z1B, nB, sel(qm.odd, is[5], is[4]));
+  fp12 xA, xB;
+  cyc_decompress(xA, cA, z1A);
+  cyc_decompress(xB, cB, z1B);
+  // acc = d5 d4 d3 d2 d1 d0 (pairing.h's order)
+  fp12 acc, d;
+  quad_bcast12<1>(acc, xB);
+  quad_bcast12<0>(d, xB);
+  {
+    fp12 x = acc;
+    fp12q_mul(acc, x, d, qm);
+  }
+  quad_bcast12<3>(d, xA);
+  {
+    fp12 x = acc;
+    fp12q_mul(acc, x, d, qm);
+  }
+  quad_bcast12<2>(d, xA);
+  {
+    fp12 x = acc;
+    fp12q_mul(acc, x, d, qm);
+  }
+  quad_bcast12<1>(d, xA);
+  {
+    fp12 x = acc;
+    fp12q_mul(acc, x, d, qm);
+  }
+  quad_bcast12<0>(d, xA);
+  {
+    fp12 x = acc;
+    fp12q_mul(acc, x, d, qm);
   }
   r = acc;
   return false;
