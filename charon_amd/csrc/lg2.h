@@ -259,36 +259,66 @@ BLS_CALL __device__ bool fp12h_exp_xabs_karabina(fp6& r, const fp6& a_in, uint32
     cyc_sqr_compressed_pair(c, m);
     if (k == 16 || k == 48 || k == 57 || k == 60 || k == 62 || k == 63) st[s++] = c;
   }
-  fp2 num[6], den[6], pre[6];
-#pragma unroll 1
-  for (s = 0; s < 6; ++s) cyc_z1_parts(num[s], den[s], st[s]);
+  // The six powers' z1 parts and decompressions are dealt out over the pair (even lane: powers 0, 2, 4; odd lane:
+  // 1, 3, 5 -- three rounds instead of six); the batch inversion stays shared, and each lane hands its partner the
+  // partner's half of the power it decompressed.  The back-substitution runs from power 5 down, so each round's two
+  // inverses are ready just before its decompression, and only the running product stays live.
+  fp2 nm[3], den[6];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    cyc_c cp;
+    cp.z2 = sel(m, st[2 * k + 1].z2, st[2 * k].z2);
+    cp.z3 = sel(m, st[2 * k + 1].z3, st[2 * k].z3);
+    cp.z4 = sel(m, st[2 * k + 1].z4, st[2 * k].z4);
+    cp.z5 = sel(m, st[2 * k + 1].z5, st[2 * k].z5);
+    fp2 dm, o;
+    cyc_z1_parts(nm[k], dm, cp);
+    pair_swap_words<24>(&o.c0.v[0], &dm.c0.v[0]);
+    den[2 * k] = sel(m, o, dm);
+    den[2 * k + 1] = sel(m, dm, o);
+  }
+  fp2 pre[6];
   pre[0] = den[0];
-#pragma unroll 1
+#pragma unroll
   for (s = 1; s < 6; ++s) fp2_mul(pre[s], pre[s - 1], den[s]);
   if (fp2_is_zero(pre[5])) return true;  // same on both lanes
   fp2 inv;
   fp2_inv(inv, pre[5]);
   fp6 acc;
-#pragma unroll 1
-  for (s = 5; s >= 0; --s) {
-    fp2 is, z1;
-    if (s > 0) {
-      fp2_mul(is, inv, pre[s - 1]);  // 1 / den[s]
-      fp2_mul(inv, inv, den[s]);
+#pragma unroll
+  for (int k = 2; k >= 0; --k) {
+    fp2 is_odd, is_even;  // 1 / den[2k + 1], 1 / den[2k]
+    fp2_mul(is_odd, inv, pre[2 * k]);
+    fp2_mul(inv, inv, den[2 * k + 1]);
+    if (k > 0) {
+      fp2_mul(is_even, inv, pre[2 * k - 1]);
+      fp2_mul(inv, inv, den[2 * k]);
     } else {
-      is = inv;
+      is_even = inv;
     }
-    fp2_mul(z1, num[s], is);
+    cyc_c cp;
+    cp.z2 = sel(m, st[2 * k + 1].z2, st[2 * k].z2);
+    cp.z3 = sel(m, st[2 * k + 1].z3, st[2 * k].z3);
+    cp.z4 = sel(m, st[2 * k + 1].z4, st[2 * k].z4);
+    cp.z5 = sel(m, st[2 * k + 1].z5, st[2 * k].z5);
+    fp2 z1;
+    fp2_mul(z1, nm[k], sel(m, is_odd, is_even));
     fp12 d;
-    cyc_decompress(d, st[s], z1);
-    const fp6 dh = sel(m, d.c1, d.c0);
-    if (s == 5) {
-      acc = dh;
+    cyc_decompress(d, cp, z1);
+    const fp6 own = sel(m, d.c1, d.c0), theirs = sel(m, d.c0, d.c1);
+    fp6 got;
+    pair_swap(got, theirs);
+    const fp6 h_odd = sel(m, own, got), h_even = sel(m, got, own);  // this lane's halves of d_{2k+1}, d_{2k}
+    if (k == 2) {
+      acc = h_odd;
     } else {
       fp6 x = acc, y;
-      BLS_LG2_KAR_MUL(y, x, dh, m);
+      BLS_LG2_KAR_MUL(y, x, h_odd, m);
       acc = y;
     }
+    fp6 x = acc, y;
+    BLS_LG2_KAR_MUL(y, x, h_even, m);
+    acc = y;
   }
   r = acc;
   return false;
