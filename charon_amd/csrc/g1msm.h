@@ -112,35 +112,103 @@ BLS_HD BLS_INLINE void g1m_scatter_lane(uint64_t s, const uint32_t* meta, const 
   }
 }
 
-// bucket b: the sum of its entries, gathered by slot (the next one loaded before the current addition, as
-// rlcb.h msm_bucket_lane); B: Jacobian, 36 words, AoS.  boff: exclusive offsets over all nl * G1M_NBL indices.
-BLS_HD BLS_INLINE void g1m_bucket_lane(uint64_t b, const uint32_t* meta, const uint32_t* boff, const uint32_t* list,
-                                       const uint32_t* gpts, uint64_t n, uint32_t* B) {
-  if (b >= (uint64_t)meta[0] * G1M_NBL) return;
+// Bucket sums, load-balanced as the G2 MSM's (rlcb.h msm_run_lane): run lane r adds the G1M_RUN consecutive entries
+// [r RUN, (r + 1) RUN) of the bucket-sorted list, bucket run by bucket run (kind 1 = [x] pk, Jacobian, full additions;
+// kind 0 = pk, affine, mixed additions); a bucket wholly inside the range goes to B, a bucket cut by the range's
+// start or end leaves a partial in P (slot 0 = the lane's first run, 1 = its last) for g1m_fix_lane.  B, P: Jacobian,
+// 36 words, AoS.  boff: exclusive offsets over all nl_max * G1M_NBL indices (entries = boff[meta[0] * G1M_NBL]).
+// Launched for g1m_run_lanes(n) lanes, the bound for 16 entries per slot.
+constexpr int G1M_RUN = 32;
+BLS_HD BLS_INLINE uint64_t g1m_run_lanes(uint64_t n) { return (2 * (uint64_t)G1M_WIN * n + G1M_RUN - 1) / G1M_RUN; }
+
+BLS_HD BLS_INLINE void g1m_run_lane(uint64_t r, const uint32_t* meta, const uint32_t* boff, const uint32_t* list,
+                                    const uint32_t* gpts, uint64_t n, uint32_t* B, uint32_t* P) {
+  const uint64_t nbk = (uint64_t)meta[0] * G1M_NBL;
+  if (nbk == 0) return;
+  const uint64_t total = boff[nbk], k0 = r * G1M_RUN;
+  if (k0 >= total) return;
+  const uint64_t k1 = k0 + G1M_RUN < total ? k0 + G1M_RUN : total;
+  uint64_t lo = 0, hi = nbk;  // the bucket of entry k0: boff[lo] <= k0 < boff[hi]
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (boff[mid] <= k0)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  // One addition per iteration on every lane (a loop per bucket run made the wave wait for each lane's longest run
+  // in turn): the point of entry k + 1 is prefetched in its bucket's kind before entry k's addition; the kind is the
+  // same across a wave except where its 2,048 entries straddle a kind boundary.
+  uint64_t b = lo, end = boff[b + 1];
+  bool kind = ((b / G1M_KSTR) & 1) != 0;
+  int slot = 0;
+  const uint32_t* gxp = gpts + 24 * n;
+  g1j q;
+  if (kind)
+    aos_load<36>(&q.x.v[0], gxp, list[k0]);
+  else
+    aos_load<24>(&q.x.v[0], gpts, list[k0]);
   g1j acc;
   jac_set_inf(acc);
-  const uint32_t k0 = boff[b], k1 = boff[b + 1];
-  if ((b / G1M_KSTR) & 1) {  // [x] pk, Jacobian
-    const uint32_t* gxp = gpts + 24 * n;
-    g1j q;
-    if (k0 < k1) aos_load<36>(&q.x.v[0], gxp, list[k0]);
-    for (uint32_t k = k0; k < k1; ++k) {
-      const g1j cur = q;
-      if (k + 1 < k1) aos_load<36>(&q.x.v[0], gxp, list[k + 1]);
-      g1j x = acc, y;
+  for (uint64_t k = k0; k < k1; ++k) {
+    const g1j cur = q;
+    const bool kc = kind;
+    uint64_t nb = b;
+    if (k + 1 < k1) {
+      if (k + 1 == end) {
+        ++nb;
+        while (boff[nb + 1] <= k + 1) ++nb;  // the next non-empty bucket
+      }
+      const bool kn = ((nb / G1M_KSTR) & 1) != 0;
+      if (kn)
+        aos_load<36>(&q.x.v[0], gxp, list[k + 1]);
+      else
+        aos_load<24>(&q.x.v[0], gpts, list[k + 1]);
+    }
+    g1j x = acc, y;
+    if (kc) {
       jac_add_body(y, x, cur);
-      acc = y;
+    } else {
+      g1a ca;
+      ca.x = cur.x;
+      ca.y = cur.y;
+      jac_add_aff_body(y, x, ca);
     }
-  } else {  // pk, affine
-    g1a q;
-    if (k0 < k1) aos_load<24>(&q.x.v[0], gpts, list[k0]);
-    for (uint32_t k = k0; k < k1; ++k) {
-      const g1a cur = q;
-      if (k + 1 < k1) aos_load<24>(&q.x.v[0], gpts, list[k + 1]);
-      g1j x = acc, y;
-      jac_add_aff_body(y, x, cur);
-      acc = y;
+    acc = y;
+    if (k + 1 == end || k + 1 == k1) {  // bucket b's run in this range ends here
+      if (boff[b] >= k0 && end <= k1)
+        aos_store<36>(B, b, &acc.x.v[0]);
+      else
+        aos_store<36>(P, 2 * r + slot, &acc.x.v[0]);
+      slot = 1;
+      jac_set_inf(acc);
+      b = nb;
+      end = boff[b + 1];
+      kind = ((b / G1M_KSTR) & 1) != 0;
     }
+  }
+}
+
+// bucket b after the run lanes (as rlcb.h msm_fix_lane): infinity when empty, written already when one run lane holds
+// all its entries, otherwise the sum of its partials.
+BLS_HD BLS_INLINE void g1m_fix_lane(uint64_t b, const uint32_t* meta, const uint32_t* boff, uint32_t* B,
+                                    const uint32_t* P) {
+  if (b >= (uint64_t)meta[0] * G1M_NBL) return;
+  const uint64_t k0 = boff[b], k1 = boff[b + 1];
+  g1j acc;
+  if (k0 == k1) {
+    jac_set_inf(acc);
+    aos_store<36>(B, b, &acc.x.v[0]);
+    return;
+  }
+  const uint64_t a = k0 / G1M_RUN, e = (k1 - 1) / G1M_RUN;
+  if (a == e) return;
+  aos_load<36>(&acc.x.v[0], P, 2 * a + (k0 == a * G1M_RUN ? 0 : 1));
+  for (uint64_t l = a + 1; l <= e; ++l) {
+    g1j p, x = acc, y;
+    aos_load<36>(&p.x.v[0], P, 2 * l);
+    jac_add_body(y, x, p);
+    acc = y;
   }
   aos_store<36>(B, b, &acc.x.v[0]);
 }

@@ -177,7 +177,7 @@ struct Context {
   uint64_t r_windows = 0;        // window count of this context's last RLC call (hipbls_rlc_stats)
   uint64_t r_call = 0;           // entry-point call that call belonged to
   // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
-  DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_Sg, m_W, m_F, m_F2, m_flag, m_Fs;
+  DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_P, m_Sg, m_Wp, m_W, m_F, m_F2, m_flag, m_Fs;
   DevBuf g1_ws;  // the G1 MSM per large message (g1msm.h), carved by G1mLayout; its Miller values go to m_F
   hipEvent_t rlcb_ev_sf = nullptr;  // the (-g1, S) Miller value is in m_Fs
   uint64_t slots = 0;               // waves in flight at one wave per SIMD: 4 x compute units (wave_slots)
@@ -749,10 +749,12 @@ constexpr uint64_t kG1mAvg = 8;
 // buffer (each region 64-word aligned).
 struct G1mLayout {
   uint64_t nl_max = 0, nb = 0, nparts = 0;
-  uint64_t cnt, lid, lmsg, soff, cur, meta, pos, slotl, pts, sc, bcnt, boff, bcur, list, B, Wv, part, words = 0;
+  uint64_t nrun = 0;
+  uint64_t cnt, lid, lmsg, soff, cur, meta, pos, slotl, pts, sc, bcnt, boff, bcur, list, B, P, Wv, part, words = 0;
   G1mLayout(uint64_t n, uint64_t n_msgs, uint64_t nl) : nl_max(nl) {
     nb = nl * G1M_NBL;
     nparts = (nb + kScanBlk - 1) / kScanBlk;
+    nrun = nl ? g1m_run_lanes(n) : 0;
     auto take = [&](uint64_t w) {
       const uint64_t at = words;
       words += (w + 63) & ~(uint64_t)63;
@@ -773,6 +775,7 @@ struct G1mLayout {
     bcur = take(nb);
     list = take(2 * (uint64_t)G1M_WIN * n);
     B = take(36 * nb);
+    P = take(2 * 36 * nrun);
     Wv = take(36 * nl * G1M_NFOLD);
     part = take(nparts + 1);
   }
@@ -853,7 +856,10 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
   HIP_TRY(c.m_cur.ensure((uint64_t)MSM_WINDOWS * MSM_NB * 4));
   HIP_TRY(c.m_list.ensure((uint64_t)MSM_WINDOWS * npts * 4));
   HIP_TRY(c.m_B.ensure((uint64_t)MSM_WINDOWS * MSM_NB * 72 * 4));
+  const uint64_t lpw = msm_run_lanes(npts);  // bucket-run lanes per window
+  HIP_TRY(c.m_P.ensure(2 * MSM_WINDOWS * lpw * 72 * 4));
   HIP_TRY(c.m_Sg.ensure((uint64_t)MSM_WINDOWS * MSM_NSEG * 72 * 4));
+  HIP_TRY(c.m_Wp.ensure((uint64_t)MSM_WINDOWS * MSM_WG * 72 * 4));
   HIP_TRY(c.m_W.ensure((uint64_t)MSM_WINDOWS * 72 * 4));
   HIP_TRY(c.m_F.ensure(cols * 144 * 4));
   HIP_TRY(c.m_F2.ensure(((cols + kBlock - 1) / kBlock) * 144 * 4));
@@ -917,13 +923,16 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
                        (uint32_t*)c.m_cur.p);
     hipLaunchKernelGGL(k_msm_scatter, dim3(g256), dim3(256), 0, s, npts, (const uint32_t*)sc, (uint32_t*)c.m_cur.p,
                        (uint32_t*)c.m_list.p);
-    hipLaunchKernelGGL(k_msm_bucket, dim3((unsigned)grid_for((uint64_t)MSM_WINDOWS * MSM_NB)), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(k_msm_run, dim3((unsigned)grid_for((uint64_t)MSM_WINDOWS * lpw)), dim3(kBlock), 0, s,
                        (const uint32_t*)c.m_off.p, (const uint32_t*)c.m_list.p, npts, (const uint32_t*)pts,
-                       (uint32_t*)c.m_B.p);
+                       (uint32_t*)c.m_B.p, (uint32_t*)c.m_P.p, lpw);
+    hipLaunchKernelGGL(k_msm_fix, dim3((unsigned)grid_for((uint64_t)MSM_WINDOWS * MSM_NB)), dim3(kBlock), 0, s,
+                       (const uint32_t*)c.m_off.p, (uint32_t*)c.m_B.p, (const uint32_t*)c.m_P.p, lpw);
     hipLaunchKernelGGL(k_msm_segment, dim3((unsigned)grid_for((uint64_t)MSM_WINDOWS * MSM_NSEG)), dim3(kBlock), 0, s,
                        (const uint32_t*)c.m_B.p, (uint32_t*)c.m_Sg.p);
-    hipLaunchKernelGGL(k_msm_window, dim3(MSM_WINDOWS), dim3(kSumBlock), 0, s, (const uint32_t*)c.m_Sg.p,
-                       (uint32_t*)c.m_W.p);
+    hipLaunchKernelGGL(k_msm_window, dim3(MSM_WINDOWS * MSM_WG), dim3(kSumBlock), 0, s, (const uint32_t*)c.m_Sg.p,
+                       (uint32_t*)c.m_Wp.p);
+    hipLaunchKernelGGL(k_msm_wsum, dim3(MSM_WINDOWS), dim3(64), 0, s, (const uint32_t*)c.m_Wp.p, (uint32_t*)c.m_W.p);
   });
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c.rlcb_ev_msm, s0));
@@ -951,9 +960,11 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
     });
     if (rc) return rc;
     rc = timed(c, "rlcb_g1msm", s1, [&] {
-      hipLaunchKernelGGL(k_g1m_bucket, dim3((unsigned)grid_for(gl.nb)), dim3(kBlock), 0, s1, gl.nb,
+      hipLaunchKernelGGL(k_g1m_run, dim3((unsigned)grid_for(gl.nrun)), dim3(kBlock), 0, s1, gl.nrun,
                          (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.boff), (const uint32_t*)G(gl.list),
-                         (const uint32_t*)G(gl.pts), n, G(gl.B));
+                         (const uint32_t*)G(gl.pts), n, G(gl.B), G(gl.P));
+      hipLaunchKernelGGL(k_g1m_fix, dim3((unsigned)grid_for(gl.nb)), dim3(kBlock), 0, s1, gl.nb,
+                         (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.boff), G(gl.B), (const uint32_t*)G(gl.P));
       hipLaunchKernelGGL(k_g1m_fold, dim3((unsigned)grid_for(nl_max * G1M_NFOLD)), dim3(kBlock), 0, s1,
                          nl_max * G1M_NFOLD, (const uint32_t*)G(gl.meta), (const uint32_t*)G(gl.B), G(gl.Wv));
     });

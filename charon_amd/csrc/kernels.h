@@ -956,13 +956,19 @@ __global__ void __launch_bounds__(256) k_g1m_scatter(uint64_t nslots, const uint
   if (s < nslots) g1m_scatter_lane(s, meta, gsc, slot_l, bcur, list);
 }
 
-__global__ void __launch_bounds__(kBlock) k_g1m_bucket(uint64_t nb, const uint32_t* __restrict__ meta,
-                                                       const uint32_t* __restrict__ boff,
-                                                       const uint32_t* __restrict__ list,
-                                                       const uint32_t* __restrict__ gpts, uint64_t n,
-                                                       uint32_t* __restrict__ B) {
+__global__ void __launch_bounds__(kBlock) k_g1m_run(uint64_t nrun, const uint32_t* __restrict__ meta,
+                                                    const uint32_t* __restrict__ boff, const uint32_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ gpts, uint64_t n,
+                                                    uint32_t* __restrict__ B, uint32_t* __restrict__ P) {
+  const uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (r < nrun) g1m_run_lane(r, meta, boff, list, gpts, n, B, P);
+}
+
+__global__ void __launch_bounds__(kBlock) k_g1m_fix(uint64_t nb, const uint32_t* __restrict__ meta,
+                                                    const uint32_t* __restrict__ boff, uint32_t* __restrict__ B,
+                                                    const uint32_t* __restrict__ P) {
   const uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (b < nb) g1m_bucket_lane(b, meta, boff, list, gpts, n, B);
+  if (b < nb) g1m_fix_lane(b, meta, boff, B, P);
 }
 
 __global__ void __launch_bounds__(kBlock) k_g1m_fold(uint64_t nq, const uint32_t* __restrict__ meta,
@@ -1080,12 +1086,19 @@ __global__ void __launch_bounds__(256) k_msm_scatter(uint64_t npts, const uint32
   if (p < npts) msm_scatter_lane(p, sc, cursor, list, npts);
 }
 
-__global__ void __launch_bounds__(kBlock) k_msm_bucket(const uint32_t* __restrict__ off,
-                                                       const uint32_t* __restrict__ list, uint64_t npts,
-                                                       const uint32_t* __restrict__ pts, uint32_t* __restrict__ B) {
+// Bucket sums: run lanes (MSM_RUN list entries each, rlcb.h msm_run_lane), then one lane per bucket for the buckets
+// the runs cut (msm_fix_lane).
+__global__ void __launch_bounds__(kBlock) k_msm_run(const uint32_t* __restrict__ off, const uint32_t* __restrict__ list,
+                                                    uint64_t npts, const uint32_t* __restrict__ pts,
+                                                    uint32_t* __restrict__ B, uint32_t* __restrict__ P, uint64_t lpw) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (t < (uint64_t)MSM_WINDOWS * MSM_NB) msm_bucket_lane((uint32_t)(t / MSM_NB), (uint32_t)(t % MSM_NB), off, list,
-                                                          npts, pts, B);
+  if (t < (uint64_t)MSM_WINDOWS * lpw) msm_run_lane((uint32_t)(t / lpw), t % lpw, off, list, npts, pts, B, P, lpw);
+}
+
+__global__ void __launch_bounds__(kBlock) k_msm_fix(const uint32_t* __restrict__ off, uint32_t* __restrict__ B,
+                                                    const uint32_t* __restrict__ P, uint64_t lpw) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t < (uint64_t)MSM_WINDOWS * MSM_NB) msm_fix_lane((uint32_t)(t / MSM_NB), (uint32_t)(t % MSM_NB), off, B, P, lpw);
 }
 
 __global__ void __launch_bounds__(kBlock) k_msm_segment(const uint32_t* __restrict__ B, uint32_t* __restrict__ Sg) {
@@ -1093,14 +1106,15 @@ __global__ void __launch_bounds__(kBlock) k_msm_segment(const uint32_t* __restri
   if (t < (uint64_t)MSM_WINDOWS * MSM_NSEG) msm_segment_lane((uint32_t)(t / MSM_NSEG), (uint32_t)(t % MSM_NSEG), B, Sg);
 }
 
-// Window sums: workgroup w folds its window's MSM_NSEG segment results (strided, then the LDS tree of
-// g2_block_tree_sum) into W[w] (72 contiguous words).
-__global__ void __launch_bounds__(kSumBlock) k_msm_window(const uint32_t* __restrict__ Sg, uint32_t* __restrict__ W) {
+// Window sums in two steps, both latency-bound: MSM_WG workgroups per window each fold a strided share of the window's
+// MSM_NSEG segment results (MSM_NSEG / (MSM_WG kSumBlock) additions per thread, then the LDS tree of g2_block_tree_sum)
+// into Wp[w MSM_WG + b]; k_msm_wsum adds each window's MSM_WG partials into W[w] (72 contiguous words).
+__global__ void __launch_bounds__(kSumBlock) k_msm_window(const uint32_t* __restrict__ Sg, uint32_t* __restrict__ Wp) {
   __shared__ uint32_t red[72 * kSumBlock];
-  const uint32_t w = blockIdx.x;
+  const uint32_t w = blockIdx.x / MSM_WG, b = blockIdx.x % MSM_WG;
   g2j acc;
   jac_set_inf(acc);
-  for (uint32_t s = threadIdx.x; s < MSM_NSEG; s += kSumBlock) {
+  for (uint32_t s = b * kSumBlock + threadIdx.x; s < MSM_NSEG; s += MSM_WG * kSumBlock) {
     g2j p;
     soa_load<72>(&p.x.c0.v[0], Sg, (uint64_t)MSM_WINDOWS * MSM_NSEG, (uint64_t)w * MSM_NSEG + s);
     g2j x = acc, y;
@@ -1109,7 +1123,30 @@ __global__ void __launch_bounds__(kSumBlock) k_msm_window(const uint32_t* __rest
   }
   g2_block_tree_sum(acc, red);
   if (threadIdx.x == 0)
-    for (int k = 0; k < 72; ++k) W[72 * w + k] = (&acc.x.c0.v[0])[k];
+    for (int k = 0; k < 72; ++k) Wp[72 * blockIdx.x + k] = (&acc.x.c0.v[0])[k];
+}
+
+// One wave per window: lanes 0..MSM_WG-1 hold the partials, a log2(MSM_WG)-level tree through LDS.
+__global__ void __launch_bounds__(64) k_msm_wsum(const uint32_t* __restrict__ Wp, uint32_t* __restrict__ W) {
+  __shared__ uint32_t red[72 * MSM_WG];
+  const uint32_t w = blockIdx.x, t = threadIdx.x;
+  if (t < MSM_WG)
+    for (int k = 0; k < 72; ++k) red[k * MSM_WG + t] = Wp[72 * (w * MSM_WG + t) + k];
+  __syncthreads();
+  for (int half = MSM_WG / 2; half >= 1; half >>= 1) {
+    if (t < (uint32_t)half) {
+      g2j x, y, z;
+      for (int k = 0; k < 72; ++k) {
+        (&x.x.c0.v[0])[k] = red[k * MSM_WG + t];
+        (&y.x.c0.v[0])[k] = red[k * MSM_WG + t + half];
+      }
+      jac_add(z, x, y);
+      for (int k = 0; k < 72; ++k) red[k * MSM_WG + t] = (&z.x.c0.v[0])[k];
+    }
+    __syncthreads();
+  }
+  if (t == 0)
+    for (int k = 0; k < 72; ++k) W[72 * w + k] = red[k * MSM_WG];
 }
 
 // Stage 3: one lane per chunk, n_chunks lanes exactly (rlcb.h rlcb_chunk_count).  The (-g1, S) Miller value is NOT an

@@ -38,8 +38,10 @@ constexpr int RLCB_CMAX = 18;                  // most items a chunk lane may ge
 constexpr int MSM_BITS = 16;                   // Pippenger window width
 constexpr int MSM_WINDOWS = 2;                 // 32-bit scalars
 constexpr uint32_t MSM_NB = 1u << MSM_BITS;    // buckets per window (bucket 0 unused)
-constexpr int MSM_SEG = 16;                    // buckets folded per segment lane
+constexpr int MSM_SEG = 8;                     // buckets folded per segment lane
 constexpr uint32_t MSM_NSEG = MSM_NB / MSM_SEG;
+constexpr int MSM_RUN = 32;                    // bucket-sorted list entries per bucket-run lane
+constexpr int MSM_WG = 8;                      // workgroups folding one window's segment results
 // Fan-in of the Miller-value product tree: a level costs `fan` serial Fp12 products, so f * log_f(chunks) products
 // of latency in all -- 32 at fan 4 for 65,536 chunks, 64 at fan 16.
 constexpr int RLCB_FAN = 4;
@@ -145,30 +147,92 @@ BLS_HD BLS_INLINE void msm_scatter_lane(uint64_t p, const uint32_t* sc, uint32_t
   }
 }
 
-// bucket (w, j): the sum of its points.  off: MSM_WINDOWS x (MSM_NB + 1) exclusive offsets.  B: Jacobian SoA,
-// 72 words x (MSM_WINDOWS * MSM_NB).  Software-pipelined: the next point's gather is issued before the current
-// addition, so its latency hides behind ~30 products of work; the addition is inlined (jac_add_aff_body), so the
-// accumulator and the prefetched point stay in registers instead of going through scratch around a call.
-BLS_HD BLS_INLINE void msm_bucket_lane(uint32_t w, uint32_t j, const uint32_t* off, const uint32_t* list,
-                                       uint64_t npts, const uint32_t* pts, uint32_t* B) {
+// Bucket sums, load-balanced: bucket-run lane r of window w adds the MSM_RUN consecutive entries [r RUN, (r + 1) RUN)
+// of the window's bucket-sorted list, whatever buckets they belong to, so every lane does the same number of mixed
+// additions (one lane per bucket made each wave as long as its largest bucket: Poisson(32) sizes, ~1.7x the mean).
+// A bucket whose entries all lie in the lane's range is written to B directly; a bucket cut by the range's start or
+// end leaves a partial sum in P (slot 0 = the lane's first run, slot 1 = its last), which msm_fix_lane adds up.
+// off: MSM_WINDOWS x (MSM_NB + 1) exclusive offsets.  B: Jacobian SoA, 72 words x (MSM_WINDOWS * MSM_NB).  P: Jacobian
+// SoA, 72 words x (2 * MSM_WINDOWS * lpw), lpw = msm_run_lanes(npts) lanes per window.  Software-pipelined: the next
+// point's gather is issued before the current addition; the addition is inlined (jac_add_aff_body), so the
+// accumulator and the prefetched point stay in registers.
+BLS_HD BLS_INLINE uint64_t msm_run_lanes(uint64_t npts) { return (npts + MSM_RUN - 1) / MSM_RUN; }
+
+BLS_HD BLS_INLINE void msm_run_lane(uint32_t w, uint64_t r, const uint32_t* off, const uint32_t* list, uint64_t npts,
+                                    const uint32_t* pts, uint32_t* B, uint32_t* P, uint64_t lpw) {
+  const uint32_t* o = off + (uint64_t)w * (MSM_NB + 1);
+  const uint64_t total = o[MSM_NB];
+  const uint64_t k0 = r * MSM_RUN;
+  if (k0 >= total) return;
+  const uint64_t k1 = k0 + MSM_RUN < total ? k0 + MSM_RUN : total;
+  uint32_t lo = 0, hi = MSM_NB;  // the bucket of entry k0: o[lo] <= k0 < o[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (o[mid] <= k0)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  uint32_t j = lo;
+  uint64_t end = o[j + 1];
+  const uint64_t lane = (uint64_t)w * lpw + r, nb = (uint64_t)MSM_WINDOWS * MSM_NB, ps = 2 * MSM_WINDOWS * lpw;
+  const uint32_t* lw = list + (uint64_t)w * npts;
+  int slot = 0;
   g2j acc;
   jac_set_inf(acc);
-  const uint32_t k0 = off[w * (MSM_NB + 1) + j], k1 = off[w * (MSM_NB + 1) + j + 1];
   g2a q;
-  if (k0 < k1) aos_load<48>(&q.x.c0.v[0], pts, list[(uint64_t)w * npts + k0]);
-  for (uint32_t k = k0; k < k1; ++k) {
+  aos_load<48>(&q.x.c0.v[0], pts, lw[k0]);
+  for (uint64_t k = k0; k < k1; ++k) {
     const g2a cur = q;
-    if (k + 1 < k1) aos_load<48>(&q.x.c0.v[0], pts, list[(uint64_t)w * npts + k + 1]);
+    if (k + 1 < k1) aos_load<48>(&q.x.c0.v[0], pts, lw[k + 1]);
     g2j x = acc, y;
     jac_add_aff_body(y, x, cur);
     acc = y;
+    if (k + 1 == end || k + 1 == k1) {  // bucket j's run in this range ends here
+      if (o[j] >= k0 && end <= k1)
+        soa_store<72>(B, nb, (uint64_t)w * MSM_NB + j, &acc.x.c0.v[0]);
+      else
+        soa_store<72>(P, ps, 2 * lane + slot, &acc.x.c0.v[0]);
+      slot = 1;
+      jac_set_inf(acc);
+      if (k + 1 < k1) {
+        ++j;
+        while (o[j + 1] <= k + 1) ++j;  // the next non-empty bucket
+        end = o[j + 1];
+      }
+    }
   }
-  soa_store<72>(B, (uint64_t)MSM_WINDOWS * MSM_NB, (uint64_t)w * MSM_NB + j, &acc.x.c0.v[0]);
+}
+
+// Bucket (w, j) after the run lanes: infinity when empty; written already when its entries fall in one run lane's
+// range; otherwise the sum of its partials -- slot 0 of every lane whose range starts inside the bucket, and the first
+// lane's slot 0 or 1 depending on whether the bucket starts that lane's range.
+BLS_HD BLS_INLINE void msm_fix_lane(uint32_t w, uint32_t j, const uint32_t* off, uint32_t* B, const uint32_t* P,
+                                    uint64_t lpw) {
+  const uint32_t* o = off + (uint64_t)w * (MSM_NB + 1);
+  const uint64_t k0 = o[j], k1 = o[j + 1], nb = (uint64_t)MSM_WINDOWS * MSM_NB, ps = 2 * MSM_WINDOWS * lpw;
+  g2j acc;
+  if (k0 == k1) {
+    jac_set_inf(acc);
+    soa_store<72>(B, nb, (uint64_t)w * MSM_NB + j, &acc.x.c0.v[0]);
+    return;
+  }
+  const uint64_t a = k0 / MSM_RUN, b = (k1 - 1) / MSM_RUN;
+  if (a == b) return;
+  const uint64_t base = 2 * ((uint64_t)w * lpw);
+  soa_load<72>(&acc.x.c0.v[0], P, ps, base + 2 * a + (k0 == a * MSM_RUN ? 0 : 1));
+  for (uint64_t l = a + 1; l <= b; ++l) {
+    g2j p, x = acc, y;
+    soa_load<72>(&p.x.c0.v[0], P, ps, base + 2 * l);
+    jac_add_body(y, x, p);
+    acc = y;
+  }
+  soa_store<72>(B, nb, (uint64_t)w * MSM_NB + j, &acc.x.c0.v[0]);
 }
 
 // segment (w, s): sum_{j in [16 s, 16 s + 16)} j B_j = T + (16 s - 1) R with R = sum B_j and T = sum (j - 16 s + 1) B_j
 // from running sums (top bucket first).  Sg: Jacobian SoA, 72 words x (MSM_WINDOWS * MSM_NSEG).  The next bucket is
-// loaded before the current one's two additions (as msm_bucket_lane).
+// loaded before the current one's two additions (as msm_run_lane).
 BLS_HD BLS_INLINE void msm_segment_lane(uint32_t w, uint32_t s, const uint32_t* B, uint32_t* Sg) {
   g2j R, T;
   jac_set_inf(R);

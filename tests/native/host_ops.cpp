@@ -483,9 +483,13 @@ void host_msm(g2j* W, const uint32_t* pts, const uint32_t* sc, uint64_t npts) {
     off[w * (MSM_NB + 1) + MSM_NB] = acc;
   }
   for (uint64_t p = 0; p < npts; ++p) msm_scatter_lane(p, sc, cur.data(), list.data(), npts);
+  const uint64_t lpw = msm_run_lanes(npts);
   std::vector<uint32_t> B((uint64_t)MSM_WINDOWS * MSM_NB * 72), Sg((uint64_t)MSM_WINDOWS * MSM_NSEG * 72);
+  std::vector<uint32_t> P(2 * MSM_WINDOWS * (lpw ? lpw : 1) * 72);
   for (int w = 0; w < MSM_WINDOWS; ++w)
-    for (uint32_t j = 0; j < MSM_NB; ++j) msm_bucket_lane(w, j, off.data(), list.data(), npts, pts, B.data());
+    for (uint64_t r = 0; r < lpw; ++r) msm_run_lane(w, r, off.data(), list.data(), npts, pts, B.data(), P.data(), lpw);
+  for (int w = 0; w < MSM_WINDOWS; ++w)
+    for (uint32_t j = 0; j < MSM_NB; ++j) msm_fix_lane(w, j, off.data(), B.data(), P.data(), lpw);
   for (int w = 0; w < MSM_WINDOWS; ++w)
     for (uint32_t s = 0; s < MSM_NSEG; ++s) msm_segment_lane(w, s, B.data(), Sg.data());
   for (int w = 0; w < MSM_WINDOWS; ++w) {
@@ -572,7 +576,10 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
     }
     boff[nb] = acc;
     for (uint64_t t = 0; t < n; ++t) g1m_scatter_lane(t, meta.data(), gsc.data(), slotl.data(), bcur.data(), glist.data());
-    for (uint64_t b = 0; b < nb; ++b) g1m_bucket_lane(b, meta.data(), boff.data(), glist.data(), gpts.data(), n, B.data());
+    const uint64_t nrun = g1m_run_lanes(n);
+    std::vector<uint32_t> P(2 * 36 * nrun + 4);
+    for (uint64_t r = 0; r < nrun; ++r) g1m_run_lane(r, meta.data(), boff.data(), glist.data(), gpts.data(), n, B.data(), P.data());
+    for (uint64_t b = 0; b < nb; ++b) g1m_fix_lane(b, meta.data(), boff.data(), B.data(), P.data());
     for (uint64_t q = 0; q < nl_max * G1M_NFOLD; ++q) g1m_fold_lane(q, meta.data(), B.data(), Wv.data());
   }
   mark(2);

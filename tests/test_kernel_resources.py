@@ -21,7 +21,7 @@ def test_every_kernel_within_scratch_budget():
     rows = codeobj.check_budget(LIB)
     assert len(rows) >= 30
     names = {r[0] for r in rows}
-    for k in ("k_verify_fused", "k_verify_pair_lq4", "k_rlcb_items", "k_tagg_scale", "k_msm_bucket"):
+    for k in ("k_verify_fused", "k_verify_pair_lq4", "k_rlcb_items", "k_tagg_scale", "k_msm_run"):
         assert k in names, k
     assert max(r[1] for r in rows) <= codeobj.PRIVATE_SEGMENT_BUDGET
 
