@@ -118,7 +118,7 @@ BLS_HD BLS_INLINE void g1m_scatter_lane(uint64_t s, const uint32_t* meta, const 
 // start or end leaves a partial in P (slot 0 = the lane's first run, 1 = its last) for g1m_fix_lane.  B, P: Jacobian,
 // 36 words, AoS.  boff: exclusive offsets over all nl_max * G1M_NBL indices (entries = boff[meta[0] * G1M_NBL]).
 // Launched for g1m_run_lanes(n) lanes, the bound for 16 entries per slot.
-constexpr int G1M_RUN = 32;
+constexpr int G1M_RUN = 64;
 BLS_HD BLS_INLINE uint64_t g1m_run_lanes(uint64_t n) { return (2 * (uint64_t)G1M_WIN * n + G1M_RUN - 1) / G1M_RUN; }
 
 BLS_HD BLS_INLINE void g1m_run_lane(uint64_t r, const uint32_t* meta, const uint32_t* boff, const uint32_t* list,

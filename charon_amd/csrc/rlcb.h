@@ -40,7 +40,7 @@ constexpr int MSM_WINDOWS = 2;                 // 32-bit scalars
 constexpr uint32_t MSM_NB = 1u << MSM_BITS;    // buckets per window (bucket 0 unused)
 constexpr int MSM_SEG = 8;                     // buckets folded per segment lane
 constexpr uint32_t MSM_NSEG = MSM_NB / MSM_SEG;
-constexpr int MSM_RUN = 32;                    // bucket-sorted list entries per bucket-run lane
+constexpr int MSM_RUN = 64;                    // bucket-sorted list entries per bucket-run lane
 constexpr int MSM_WG = 8;                      // workgroups folding one window's segment results
 // Fan-in of the Miller-value product tree: a level costs `fan` serial Fp12 products, so f * log_f(chunks) products
 // of latency in all -- 32 at fan 4 for 65,536 chunks, 64 at fan 16.
