@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--tagg-groups", type=int, default=10000,
                     help="C3 validators per GPU (0 = skip); node batch = groups x world")
     ap.add_argument("--tagg-steps", type=int, default=2)
+    ap.add_argument("--tagg-two-streams", type=int, default=1,
+                    help="also time C3 with consecutive calls alternating between two streams (0 = skip)")
     ap.add_argument("--cpu-sample", type=int, default=4096,
                     help="C2 items verified by the C++ CPU baseline, one thread per core (0 = skip)")
     ap.add_argument("--rlc-node-validators", type=int, default=262144,
@@ -488,6 +490,7 @@ def main():
     # ---- C3: threshold aggregation + Verify of each aggregate; node batch = groups x world validators, this rank's
     # slice; the 96-byte aggregates and the verify bitmap are all-gathered inside the timed step
     tagg = None
+    tagg2 = None
     tagg_kms = {}
     tagg_roofline = None
     if args.tagg_groups > 0:
@@ -520,8 +523,8 @@ def main():
         torch.cuda.synchronize(dev)
         lib.hipbls_kernel_timing_reset()
         tel = timed_loop(tstep, args.tagg_steps, dev, barrier, world)
-        tagg_kms = kernel_ms(lib, ("tagg_scale", "tagg_sum", "tagg_unscale", "tv_prep_pk",
-                                         "verify_pair_lq4", "verify_pair_lg2", "verify_pair_single"))
+        tagg_kms = kernel_ms(lib, ("tv_phase_a", "tagg_sum", "tv_check_unscale", "tagg_scale", "tagg_unscale",
+                                   "tv_prep_pk", "verify_pair_lg2", "verify_pair_single"))
         assert set(d_gst.cpu().tolist()) == {0} and set(d_vst.cpu().tolist()) == {0}, "aggregate mismatch"
         # the 96-byte aggregates themselves (herumi.go:244-283 returns exactly these bytes, sigagg.go:149-154 injects
         # them): each equals Sign(secret) made by the separate sign kernel
@@ -534,6 +537,34 @@ def main():
             assert not bad_g, "an aggregate of the node batch failed Verify: %d groups, first %s (this rank's slice " \
                               "[%d, %d))" % (len(bad_g), bad_g[:8], g_lo, g_hi)
         tagg = G_node * args.tagg_steps / tel
+        # The same calls with two in flight: consecutive calls alternate between this stream and a second one (each
+        # with its own outputs), as consecutive sigagg duties would; the library starts a call's phase A once the
+        # previous call's is done, so it runs in the SIMDs the previous call's quad check leaves idle.  No gathers in
+        # this measurement (two streams' collectives on one communicator are not ordered); outputs checked after.
+        if args.tagg_two_streams:
+            stream_b = torch.cuda.Stream(device=dev)
+            sp_b = ctypes.c_void_p(stream_b.cuda_stream)
+            d_agg_b = torch.zeros_like(d_agg)
+            d_gst_b = torch.full_like(d_gst, -1)
+            d_vst_b = torch.full_like(d_vst, -1)
+
+            def tcall(spx, agg, gst, vst):
+                rc = lib.hipbls_threshold_aggregate_verify_batch_device(
+                    d_psig.data_ptr(), d_pid.data_ptr(), d_poff.data_ptr(), G, len(pids), d_dpk.data_ptr(),
+                    d_dmsg.data_ptr(), d_doff.data_ptr(), agg.data_ptr(), gst.data_ptr(), vst.data_ptr(), spx)
+                assert rc == 0
+
+            def tstep2():  # two calls, one per stream
+                tcall(sp, d_agg, d_gst, d_vst)
+                tcall(sp_b, d_agg_b, d_gst_b, d_vst_b)
+
+            tstep2()
+            torch.cuda.synchronize(dev)
+            tel2 = timed_loop(tstep2, args.tagg_steps, dev, barrier, world)
+            for agg, gst, vst in ((d_agg, d_gst, d_vst), (d_agg_b, d_gst_b, d_vst_b)):
+                assert set(gst.cpu().tolist()) == {0} and set(vst.cpu().tolist()) == {0}, "two-stream C3 statuses"
+                assert bytes(agg.cpu().numpy().tobytes()) == b"".join(want_aggs), "two-stream C3 aggregate bytes"
+            tagg2 = 2 * G_node * args.tagg_steps / tel2
         # C3 roofline: the counted per-aggregate unit over the whole call's wall time (the pipeline), and per stage over
         # its kernel's average launch time (HIP events on the launch stream)
         unit = sum(TAGG_FPMUL.values())
@@ -547,11 +578,12 @@ def main():
             "algorithmic_unit": "%d Fp-mul-equivalents x %d MADs per aggregate (7 partials + Verify)" % (unit,
                                                                                                      MADS_PER_FPMUL),
             "achieved": round(ach, 3), "peak": MAD_PEAK_T, "unit": "Tmad/s", "frac": round(ach / MAD_PEAK_T, 4),
-            "note": "whole sigagg call (5 kernels on 3 streams) over wall time",
-            "stage_frac": {"tagg_scale": kfrac("tagg_scale", TAGG_FPMUL["scale_7"] * G),
-                           "tv_prep_pk": kfrac("tv_prep_pk", TAGG_FPMUL["key_prep"] * G),
-                           "tagg_unscale": kfrac("tagg_unscale", TAGG_FPMUL["unscale"] * G),
-                           "verify_pair_lq4": kfrac("verify_pair_lq4", TAGG_FPMUL["pairing"] * G)}}
+            "note": "whole sigagg call (4 kernels on the caller's stream) over wall time, one call in flight",
+            "stage_frac": {"tv_phase_a": kfrac("tv_phase_a", (TAGG_FPMUL["scale_7"] + TAGG_FPMUL["key_prep"]) * G),
+                           "tv_check_unscale": kfrac("tv_check_unscale",
+                                                     (TAGG_FPMUL["pairing"] + TAGG_FPMUL["unscale"]) * G)}}
+        if tagg2:
+            tagg_roofline["frac_two_streams"] = round(unit * MADS_PER_FPMUL * (tagg2 / world) / 1e12 / MAD_PEAK_T, 4)
 
     # ---- C4: RLC BatchVerify of the 1M-partial node batch, validator-index slices over the ranks (strong scaling:
     # the node batch is fixed); node bitmap all-gathered inside the timed step
@@ -779,6 +811,7 @@ def main():
             "drop_in_latency": latency,
             "verified_partial_sigs_per_s_pubshare_table": round(keys_rate, 1) if keys_rate else None,
             "threshold_aggregates_per_s": round(tagg, 1) if tagg else None,
+            "threshold_aggregates_per_s_two_streams": round(tagg2, 1) if tagg2 else None,
             "threshold_aggregate_kernel_avg_ms": tagg_kms or None,
             "threshold_aggregate_roofline": tagg_roofline,
             "threshold_aggregate_workload": "C3: %d validators per GPU x 7-of-10 Lagrange in G2 + Verify of each "

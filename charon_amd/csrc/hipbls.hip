@@ -157,6 +157,11 @@ struct Context {
   DevBuf r_pk, r_sig, r_h, r_win, r_midx, r_list, r_cnt, r_slot, r_mlist;  // RLC BatchVerify workspaces
   DevBuf t_code, t_tab, b_kidx;                                            // resident pubshare table + key indices
   DevBuf v_ws;                                                             // lane-pair Verify points (SoA)
+  // sigagg in one call (launch_tagg_verify): two workspace sets used alternately, each with the completion event of
+  // the call that last used it
+  DevBuf tv_pts[2], tv_pst[2], tv_ws[2], tv_aux[2];
+  hipEvent_t tv_done[2] = {}, tv_phase = nullptr;  // tv_phase: the last call's phase A (and S, statuses) done
+  uint64_t tv_seq = 0;
   uint64_t t_size = 0;
   // pubshare bytes -> table index (host side), for the submission queue's keyed path
   std::unordered_map<std::string, uint32_t> t_index;
@@ -170,9 +175,9 @@ struct Context {
   // Last workspace user's completion (cross-stream ordering), per workspace group: the general buffers (b_*, v_ws) and
   // the RLC ones (r_*, m_*, the H(m) cache), so an RLC batch and, say, a FastAggregateVerify on another stream (the C5
   // slot mix) overlap instead of queueing behind each other.  The two groups still SHARE the fork sub-streams
-  // (sub[0], sub[1], the device's) and the fork/join events (ev_fork, ev_hash, ev_join): launch_rlc,
-  // launch_rlc_batch and launch_tagg_verify issue every record/wait pair on those within one call under c.mu, which
-  // is what makes the sharing safe; a sigagg call queued behind an RLC batch's sub-stream work waits for it there.
+  // (sub[0], sub[1], the device's) and the fork/join events (ev_fork, ev_hash, ev_join): launch_rlc and
+  // launch_rlc_batch issue every record/wait pair on those within one call under c.mu, which
+  // is what makes the sharing safe.  sigagg in one call uses neither: its workspace sets (tv_*) carry their own events.
   hipEvent_t ws_done = nullptr, ws_done_rlc = nullptr;
   uint64_t r_windows = 0;        // window count of this context's last RLC call (hipbls_rlc_stats)
   uint64_t r_call = 0;           // entry-point call that call belonged to
@@ -1064,86 +1069,90 @@ int launch_tagg(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, const u
   return ws_end(c, s);
 }
 
-// sigagg in one call: ThresholdAggregate on sub[0] while sub[1] decodes and scales the validators' root keys and
-// hashes their messages; the caller's stream joins both and runs the pairing checks on S (kernels.h, k_tagg_sum_s)
-// while sub[0] goes on to [L^-1] S and the 96-byte aggregates (k_tagg_unscale).
+// sigagg in one call, three kernels on the caller's stream (kernels.h): phase A (the root keys' decode, [L] pk and
+// message hashes, beside the partials' decode + subgroup test + c_k sig_k: one launch, prep workgroups first), the
+// sums S (k_tagg_sum_s) and the status join, then the pairing checks on S against [L] pk beside [L^-1] S and the
+// 96-byte aggregates (k_tv_check_unscale).  No sub-streams: the workspace comes from one of two sets used
+// alternately (each waits for the call two back that used it), so calls enqueued on different streams overlap --
+// the next call's phase A runs in the SIMDs the quad check leaves idle.  Same statuses and bytes as before.
+#ifndef BLS_TV_PAIR_HASH
+#define BLS_TV_PAIR_HASH 1
+#endif
 int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, const uint64_t* d_goffs,
                        uint64_t n_groups, uint64_t n_parts, const uint8_t* d_dvpks, const uint8_t* d_msgs,
                        const uint64_t* d_moffs, uint8_t* d_out, int32_t* d_astatus, int32_t* d_vstatus, hipStream_t s) {
   if (n_groups == 0) return HIPBLS_OK;
-  int rc = ensure_rlc_streams(c);
-  if (rc) return rc;
-  HIP_TRY(c.b_pts.ensure((n_parts ? n_parts : 1) * 72 * 4));
-  HIP_TRY(c.b_pst.ensure((n_parts ? n_parts : 1) * 4));
-  HIP_TRY(c.v_ws.ensure(n_groups * 120 * 4));
-  HIP_TRY(c.b_aux.ensure(n_groups * 4));
-  uint32_t* ws = (uint32_t*)c.v_ws.p;
-  int32_t* agg_inf = (int32_t*)c.b_aux.p;
-  hipStream_t s0 = c.sub[0], s1 = c.sub[1];
-  rc = ws_begin(c, s);
-  if (rc) return rc;
-  HIP_TRY(hipEventRecord(c.ev_fork, s));
-  HIP_TRY(hipStreamWaitEvent(s0, c.ev_fork, 0));
-  HIP_TRY(hipStreamWaitEvent(s1, c.ev_fork, 0));
-  // The key side first: its lane-pair hashes are the longest lanes of phase A, so they take their wave slots before
-  // the scaling's 1,094 waves fill the rest (kernel trace: phase A 9.1 ms with the prep dispatched first, 9.8-10.4 ms
-  // when the scaling went first and the prep waited for a second round of slots).
-#ifndef BLS_TV_PAIR_HASH
-#define BLS_TV_PAIR_HASH 1
-#endif
-  rc = timed(c, "tv_prep_pk", s1, [&] {
-    if (BLS_TV_PAIR_HASH && n_groups <= kPairHashMaxVerify)
-      hipLaunchKernelGGL(k_tv_prep_pk2, dim3((unsigned)(3 * grid_for(n_groups))), dim3(kBlock), 0, s1, d_dvpks, d_msgs,
+  const int p = (int)(c.tv_seq & 1);
+  if (!c.tv_done[p]) HIP_TRY(hipEventCreateWithFlags(&c.tv_done[p], hipEventDisableTiming));
+  HIP_TRY(c.tv_pts[p].ensure((n_parts ? n_parts : 1) * 72 * 4));
+  HIP_TRY(c.tv_pst[p].ensure((n_parts ? n_parts : 1) * 4));
+  HIP_TRY(c.tv_ws[p].ensure(n_groups * 120 * 4));
+  HIP_TRY(c.tv_aux[p].ensure(n_groups * 4));
+  ++c.tv_seq;
+  uint32_t* ws = (uint32_t*)c.tv_ws[p].p;
+  int32_t* agg_inf = (int32_t*)c.tv_aux[p].p;
+  uint32_t* pts = (uint32_t*)c.tv_pts[p].p;
+  int32_t* pst = (int32_t*)c.tv_pst[p].p;
+  HIP_TRY(hipStreamWaitEvent(s, c.tv_done[p], 0));
+  // Phase A after the previous call's phase A, whatever its stream: two calls' phase A would only share the same
+  // wave slots, while this call's phase A beside the previous call's check fills the SIMDs that check leaves idle.
+  if (!c.tv_phase) HIP_TRY(hipEventCreateWithFlags(&c.tv_phase, hipEventDisableTiming));
+  HIP_TRY(hipStreamWaitEvent(s, c.tv_phase, 0));
+  int rc = HIPBLS_OK;
+  if (BLS_TV_PAIR_HASH && n_groups <= kPairHashMaxVerify) {
+    const uint64_t nprep = 3 * grid_for(n_groups), nscale = n_parts ? grid_for(n_parts) : 0;
+    rc = timed(c, "tv_phase_a", s, [&] {
+      hipLaunchKernelGGL(k_tv_phase_a, dim3((unsigned)(nprep + nscale)), dim3(kBlock), 0, s, d_dvpks, d_msgs, d_moffs,
+                         n_groups, d_ids, d_goffs, ws, d_vstatus, d_sigs, n_parts, pts, pst);
+    });
+  } else {
+    rc = timed(c, "tv_prep_pk", s, [&] {
+      hipLaunchKernelGGL(k_tv_prep_pk, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s, d_dvpks, d_msgs,
                          d_moffs, n_groups, d_ids, d_goffs, ws, d_vstatus);
-    else
-      hipLaunchKernelGGL(k_tv_prep_pk, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s1, d_dvpks, d_msgs,
-                         d_moffs, n_groups, d_ids, d_goffs, ws, d_vstatus);
-  });
-  if (rc) return rc;
-  HIP_TRY(hipEventRecord(c.ev_join[1], s1));
-  if (n_parts) {
-    rc = timed(c, "tagg_scale", s0, [&] {
-      hipLaunchKernelGGL(k_tagg_scale, dim3((unsigned)grid_for(n_parts)), dim3(kBlock), 0, s0, d_sigs, d_ids, d_goffs,
-                         n_groups, n_parts, (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);
     });
     if (rc) return rc;
+    if (n_parts)
+      rc = timed(c, "tagg_scale", s, [&] {
+        hipLaunchKernelGGL(k_tagg_scale, dim3((unsigned)grid_for(n_parts)), dim3(kBlock), 0, s, d_sigs, d_ids,
+                           d_goffs, n_groups, n_parts, pts, pst);
+      });
   }
-  rc = timed(c, "tagg_sum", s0, [&] {
-    hipLaunchKernelGGL(k_tagg_sum_s, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s0,
-                       (const uint32_t*)c.b_pts.p, (const int32_t*)c.b_pst.p, d_goffs, n_groups, n_parts, d_astatus,
-                       ws, agg_inf);
+  if (rc) return rc;
+  rc = timed(c, "tagg_sum", s, [&] {
+    hipLaunchKernelGGL(k_tagg_sum_s, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s, (const uint32_t*)pts,
+                       (const int32_t*)pst, d_goffs, n_groups, n_parts, d_astatus, ws, agg_inf);
   });
   if (rc) return rc;
-  HIP_TRY(hipEventRecord(c.ev_join[0], s0));
-  rc = timed(c, "tagg_unscale", s0, [&] {
-    hipLaunchKernelGGL(k_tagg_unscale, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s0, d_ids, d_goffs,
-                       n_groups, (const uint32_t*)ws, (const int32_t*)agg_inf, (const int32_t*)d_astatus, d_out);
-  });
-  if (rc) return rc;
-  HIP_TRY(hipEventRecord(c.ev_hash, s0));
-  HIP_TRY(hipStreamWaitEvent(s, c.ev_join[0], 0));
-  HIP_TRY(hipStreamWaitEvent(s, c.ev_join[1], 0));
   hipLaunchKernelGGL(k_tv_join, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s, n_groups,
                      (const int32_t*)d_astatus, (const int32_t*)agg_inf, d_vstatus);
   HIP_TRY(hipGetLastError());
-  if (use_quads(n_groups))
-    rc = timed(c, "verify_pair_lq4", s, [&] {
-      hipLaunchKernelGGL(k_verify_pair_lq4, dim3((unsigned)grid_for(4 * n_groups)), dim3(kBlock), 0, s,
-                         (const uint32_t*)ws, n_groups, d_vstatus);
+  HIP_TRY(hipEventRecord(c.tv_phase, s));
+  if (use_quads(n_groups)) {
+    rc = timed(c, "tv_check_unscale", s, [&] {
+      hipLaunchKernelGGL(k_tv_check_unscale, dim3((unsigned)(grid_for(4 * n_groups) + grid_for(n_groups))),
+                         dim3(kBlock), 0, s, (const uint32_t*)ws, n_groups, d_vstatus, d_ids, d_goffs,
+                         (const int32_t*)agg_inf, (const int32_t*)d_astatus, d_out);
     });
-  else if (use_pairs(n_groups, kLg2MaxVerify))
-    rc = timed(c, "verify_pair_lg2", s, [&] {
-      hipLaunchKernelGGL(k_verify_pair_lg2, dim3((unsigned)grid_for(2 * n_groups)), dim3(kBlock), 0, s,
-                         (const uint32_t*)ws, n_groups, d_vstatus);
+  } else {
+    if (use_pairs(n_groups, kLg2MaxVerify))
+      rc = timed(c, "verify_pair_lg2", s, [&] {
+        hipLaunchKernelGGL(k_verify_pair_lg2, dim3((unsigned)grid_for(2 * n_groups)), dim3(kBlock), 0, s,
+                           (const uint32_t*)ws, n_groups, d_vstatus);
+      });
+    else
+      rc = timed(c, "verify_pair_single", s, [&] {
+        hipLaunchKernelGGL(k_verify_pair_single, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s,
+                           (const uint32_t*)ws, n_groups, d_vstatus);
+      });
+    if (rc) return rc;
+    rc = timed(c, "tagg_unscale", s, [&] {
+      hipLaunchKernelGGL(k_tagg_unscale, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s, d_ids, d_goffs,
+                         n_groups, (const uint32_t*)ws, (const int32_t*)agg_inf, (const int32_t*)d_astatus, d_out);
     });
-  else
-    rc = timed(c, "verify_pair_single", s, [&] {
-      hipLaunchKernelGGL(k_verify_pair_single, dim3((unsigned)grid_for(n_groups)), dim3(kBlock), 0, s,
-                         (const uint32_t*)ws, n_groups, d_vstatus);
-    });
+  }
   if (rc) return rc;
-  HIP_TRY(hipStreamWaitEvent(s, c.ev_hash, 0));  // the aggregates are part of the call's result
-  return ws_end(c, s);
+  HIP_TRY(hipEventRecord(c.tv_done[p], s));
+  return HIPBLS_OK;
 }
 
 int launch_fav(Context& c, const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_goff, uint64_t n_groups,
@@ -1737,6 +1746,8 @@ int tagg_verify_host(Context& c, const uint8_t* sigs, const int64_t* share_idx, 
   HIP_TRY(c.b_kidx.ensure((n_groups + 1) * 8));  // message offsets
   HIP_TRY(c.b_out.ensure(n_groups * 96));
   HIP_TRY(c.b_st.ensure(n_groups * 8));          // aggregate statuses, then verify statuses
+  int wrc = ws_begin(c, c.stream);
+  if (wrc) return wrc;
   if (n_parts) {
     HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_parts * 96, hipMemcpyHostToDevice, c.stream));
     HIP_TRY(hipMemcpyAsync(c.b_ids.p, share_idx, n_parts * 8, hipMemcpyHostToDevice, c.stream));
@@ -1750,6 +1761,8 @@ int tagg_verify_host(Context& c, const uint8_t* sigs, const int64_t* share_idx, 
   int rc = launch_tagg_verify(c, (const uint8_t*)c.b_sig.p, (const int64_t*)c.b_ids.p, (const uint64_t*)c.b_off.p,
                               n_groups, n_parts, (const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p,
                               (const uint64_t*)c.b_kidx.p, (uint8_t*)c.b_out.p, ast, vst, c.stream);
+  if (rc) return rc;
+  rc = ws_end(c, c.stream);  // the general input/output buffers above
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(out_sigs, c.b_out.p, n_groups * 96, hipMemcpyDeviceToHost, c.stream));
   HIP_TRY(hipMemcpyAsync(agg_status, ast, n_groups * 4, hipMemcpyDeviceToHost, c.stream));

@@ -133,9 +133,8 @@ __global__ void __launch_bounds__(kBlock) k_verify_pair_lg2(const uint32_t* __re
 
 // Stage 2 on a lane quad per item (lg2.h lq4_verify): lanes 4i, 4i+1 split e(pk, H(m))'s Miller loop, lanes 4i+2,
 // 4i+3 e(-g1, sig)'s, then the split final exponentiation.  Same statuses as k_verify_pair_lg2.
-__global__ void __launch_bounds__(kBlock) k_verify_pair_lq4(const uint32_t* __restrict__ ws, uint64_t n,
-                                                            int32_t* __restrict__ status) {
-  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+__device__ __forceinline__ void verify_pair_lq4_lane(uint64_t t, const uint32_t* __restrict__ ws, uint64_t n,
+                                                     int32_t* __restrict__ status) {
   const uint64_t i = t >> 2;
   const int q = (int)(t & 3);
   if (i >= n || status[i] != RLC_PENDING) return;  // same decision on all four lanes of the quad
@@ -146,6 +145,10 @@ __global__ void __launch_bounds__(kBlock) k_verify_pair_lq4(const uint32_t* __re
   soa_load<48>(&sig.x.c0.v[0], ws + 72 * n, n, i);
   const int st = lq4_verify(pk, hm, sig, q);
   if (q == 0) status[i] = st;
+}
+__global__ void __launch_bounds__(kBlock) k_verify_pair_lq4(const uint32_t* __restrict__ ws, uint64_t n,
+                                                            int32_t* __restrict__ status) {
+  verify_pair_lq4_lane(blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, ws, n, status);
 }
 
 __global__ void __launch_bounds__(kBlock) k_sign(const uint8_t* __restrict__ sks, const uint8_t* __restrict__ msgs,
@@ -176,13 +179,10 @@ __global__ void __launch_bounds__(kBlock) k_sk_to_pk(const uint8_t* __restrict__
 #ifndef BLS_TAGG_WAVES
 #define BLS_TAGG_WAVES 1
 #endif
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BLS_TAGG_WAVES, BLS_TAGG_WAVES)))
-k_tagg_scale(const uint8_t* __restrict__ sigs,
-                                                       const int64_t* __restrict__ ids,
-                                                       const uint64_t* __restrict__ goffs, uint64_t n_groups,
-                                                       uint64_t n_parts, uint32_t* __restrict__ pts,
-                                                       int32_t* __restrict__ pstat) {
-  const uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+__device__ __forceinline__ void tagg_scale_lane(uint64_t k, const uint8_t* __restrict__ sigs,
+                                                const int64_t* __restrict__ ids, const uint64_t* __restrict__ goffs,
+                                                uint64_t n_groups, uint64_t n_parts, uint32_t* __restrict__ pts,
+                                                int32_t* __restrict__ pstat) {
   if (k >= n_parts) return;
   uint64_t lo = 0, hi = n_groups;  // find g with goffs[g] <= k < goffs[g+1]
   while (hi - lo > 1) {
@@ -228,6 +228,11 @@ k_tagg_scale(const uint8_t* __restrict__ sigs,
   const uint32_t* src = &acc.x.c0.v[0];
   for (int w = 0; w < 72; ++w) pts[(uint64_t)w * n_parts + k] = src[w];
   pstat[k] = st;
+}
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BLS_TAGG_WAVES, BLS_TAGG_WAVES)))
+k_tagg_scale(const uint8_t* __restrict__ sigs, const int64_t* __restrict__ ids, const uint64_t* __restrict__ goffs,
+             uint64_t n_groups, uint64_t n_parts, uint32_t* __restrict__ pts, int32_t* __restrict__ pstat) {
+  tagg_scale_lane(blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, sigs, ids, goffs, n_groups, n_parts, pts, pstat);
 }
 
 // ThresholdAggregate, stage 2: one lane per group sums its scaled partials, multiplies the sum by L^-1 on the
@@ -319,12 +324,10 @@ __global__ void __launch_bounds__(kBlock) k_tagg_sum_s(const uint32_t* __restric
 
 // Stage 3 (beside the pairing check): sigma = [L^-1] S on the small-integer path (S itself otherwise), compressed.
 // The output bytes equal k_tagg_sum's: the encoding of sigma for a group that combined, zeros otherwise.
-__global__ void __launch_bounds__(kBlock) k_tagg_unscale(const int64_t* __restrict__ ids,
-                                                         const uint64_t* __restrict__ goffs, uint64_t n_groups,
-                                                         const uint32_t* __restrict__ ws,
-                                                         const int32_t* __restrict__ agg_inf,
-                                                         const int32_t* __restrict__ status, uint8_t* __restrict__ out) {
-  const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+__device__ __forceinline__ void tagg_unscale_lane(uint64_t g, const int64_t* __restrict__ ids,
+                                                  const uint64_t* __restrict__ goffs, uint64_t n_groups,
+                                                  const uint32_t* __restrict__ ws, const int32_t* __restrict__ agg_inf,
+                                                  const int32_t* __restrict__ status, uint8_t* __restrict__ out) {
   if (g >= n_groups) return;
   const int st = status[g];
   g2j acc;
@@ -339,6 +342,13 @@ __global__ void __launch_bounds__(kBlock) k_tagg_unscale(const int64_t* __restri
   uint8_t sig[96];
   g2_compress(sig, acc);
   for (int b = 0; b < 96; ++b) out[96 * g + b] = st == HIPBLS_OK ? sig[b] : (uint8_t)0;
+}
+__global__ void __launch_bounds__(kBlock) k_tagg_unscale(const int64_t* __restrict__ ids,
+                                                         const uint64_t* __restrict__ goffs, uint64_t n_groups,
+                                                         const uint32_t* __restrict__ ws,
+                                                         const int32_t* __restrict__ agg_inf,
+                                                         const int32_t* __restrict__ status, uint8_t* __restrict__ out) {
+  tagg_unscale_lane(blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, ids, goffs, n_groups, ws, agg_inf, status, out);
 }
 
 // Verify prep of the key side (one lane per group, beside the aggregation): decode + subgroup-check the
@@ -375,15 +385,14 @@ __global__ void __launch_bounds__(kBlock) k_tv_prep_pk(const uint8_t* __restrict
 // k_tv_prep_pk with the roles split per workgroup, as k_verify_prep: the first grid_for(n) blocks decode and scale
 // the keys (status, pk), the next 2 grid_for(n) blocks hash the messages on lane pairs (lg2.h hash_to_g2_pair), so the
 // key decode runs beside the hash and each hash takes about half the latency.  Every message is hashed.
-__global__ void __launch_bounds__(kBlock) k_tv_prep_pk2(const uint8_t* __restrict__ pks,
-                                                        const uint8_t* __restrict__ msgs,
-                                                        const uint64_t* __restrict__ offs, uint64_t n,
-                                                        const int64_t* __restrict__ ids,
-                                                        const uint64_t* __restrict__ goffs,
-                                                        uint32_t* __restrict__ ws, int32_t* __restrict__ vstatus) {
+__device__ __forceinline__ void tv_prep_pk2_block(uint64_t blk, const uint8_t* __restrict__ pks,
+                                                  const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offs,
+                                                  uint64_t n, const int64_t* __restrict__ ids,
+                                                  const uint64_t* __restrict__ goffs, uint32_t* __restrict__ ws,
+                                                  int32_t* __restrict__ vstatus) {
   const uint64_t nb = (n + kBlock - 1) / kBlock;
-  if (blockIdx.x >= nb) {  // uniform per workgroup
-    const uint64_t t = (blockIdx.x - nb) * (uint64_t)blockDim.x + threadIdx.x;
+  if (blk >= nb) {  // uniform per workgroup
+    const uint64_t t = (blk - nb) * (uint64_t)blockDim.x + threadIdx.x;
     const uint64_t i = t >> 1;
     if (i >= n) return;  // same on both lanes of the pair
     const uint32_t m = (t & 1) ? ~0u : 0u;
@@ -397,7 +406,7 @@ __global__ void __launch_bounds__(kBlock) k_tv_prep_pk2(const uint8_t* __restric
     }
     return;
   }
-  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t i = blk * (uint64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   g1a pk;
   const int dp = g1_decompress(pk, pks + 48 * i, true);
@@ -413,6 +422,33 @@ __global__ void __launch_bounds__(kBlock) k_tv_prep_pk2(const uint8_t* __restric
   }
   vstatus[i] = st;
 }
+__global__ void __launch_bounds__(kBlock) k_tv_prep_pk2(const uint8_t* __restrict__ pks,
+                                                        const uint8_t* __restrict__ msgs,
+                                                        const uint64_t* __restrict__ offs, uint64_t n,
+                                                        const int64_t* __restrict__ ids,
+                                                        const uint64_t* __restrict__ goffs,
+                                                        uint32_t* __restrict__ ws, int32_t* __restrict__ vstatus) {
+  tv_prep_pk2_block(blockIdx.x, pks, msgs, offs, n, ids, goffs, ws, vstatus);
+}
+
+// sigagg in one call, phase A as ONE launch (roles per workgroup, uniform): workgroups [0, 3 grid_for(n)) are
+// k_tv_prep_pk2's (key decode + [L] pk, then the lane-pair hashes), the rest k_tagg_scale's (one lane per partial).
+// The prep's workgroups come first so they take their wave slots before the scaling's; with the check and the
+// unscale also one launch (k_tv_check_unscale), a sigagg call is three kernels on the caller's stream and needs no
+// sub-streams, so calls on different streams overlap (the next call's phase A in the check's idle SIMDs).
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(BLS_TAGG_WAVES, BLS_TAGG_WAVES)))
+k_tv_phase_a(const uint8_t* __restrict__ pks, const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offs,
+             uint64_t n, const int64_t* __restrict__ ids, const uint64_t* __restrict__ goffs,
+             uint32_t* __restrict__ ws, int32_t* __restrict__ vstatus, const uint8_t* __restrict__ sigs,
+             uint64_t n_parts, uint32_t* __restrict__ pts, int32_t* __restrict__ pstat) {
+  const uint64_t nprep = 3 * ((n + kBlock - 1) / kBlock);
+  if (blockIdx.x < nprep) {
+    tv_prep_pk2_block(blockIdx.x, pks, msgs, offs, n, ids, goffs, ws, vstatus);
+    return;
+  }
+  tagg_scale_lane((blockIdx.x - nprep) * (uint64_t)blockDim.x + threadIdx.x, sigs, ids, goffs, n, n_parts, pts,
+                  pstat);
+}
 
 // Join: a group whose aggregation failed reports that status for its Verify too; otherwise the key's status
 // stands (Verify checks the key first), and an aggregate at infinity is "signature not verified".
@@ -424,6 +460,23 @@ __global__ void __launch_bounds__(kBlock) k_tv_join(uint64_t n, const int32_t* _
     vstatus[i] = astatus[i];
   else if (vstatus[i] == RLC_PENDING && agg_inf[i])
     vstatus[i] = HIPBLS_ERR_VERIFY;
+}
+
+// sigagg's pairing check on lane quads beside [L^-1] S (roles per workgroup, uniform): workgroups [0, grid_for(4 n))
+// run k_verify_pair_lq4's lanes, the rest k_tagg_unscale's.  Both only read ws.
+__global__ void __launch_bounds__(kBlock) k_tv_check_unscale(const uint32_t* __restrict__ ws, uint64_t n,
+                                                             int32_t* __restrict__ vstatus,
+                                                             const int64_t* __restrict__ ids,
+                                                             const uint64_t* __restrict__ goffs,
+                                                             const int32_t* __restrict__ agg_inf,
+                                                             const int32_t* __restrict__ astatus,
+                                                             uint8_t* __restrict__ out) {
+  const uint64_t nq = (4 * n + kBlock - 1) / kBlock;
+  if (blockIdx.x < nq) {
+    verify_pair_lq4_lane(blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, ws, n, vstatus);
+    return;
+  }
+  tagg_unscale_lane((blockIdx.x - nq) * (uint64_t)blockDim.x + threadIdx.x, ids, goffs, n, ws, agg_inf, astatus, out);
 }
 
 // One lane per item on the lane-pair Verify layout (for batches too large for lane pairs).

@@ -244,7 +244,9 @@ int hipbls_hcache_stats(uint64_t* hits, uint64_t* misses, uint64_t* entries);
  * device that owns the status array. */
 int hipbls_verify_batch_device(const uint8_t* d_pks, const uint8_t* d_msgs, const uint64_t* d_msg_offsets,
                                const uint8_t* d_sigs, uint64_t n, int32_t* d_status, void* stream);
-/* n_parts = group_offsets[n_groups], passed explicitly so the call never reads device memory. */
+/* n_parts = group_offsets[n_groups], passed explicitly so the call never reads device memory.  The _device sigagg
+ * call is three kernels on `stream`; calls enqueued on different streams overlap (two workspace sets, each call's
+ * first kernel after the previous call's), so a caller with consecutive duties can keep two in flight. */
 /* core/sigagg (sigagg.go:138-159) in one call: ThresholdAggregate of every group (as
  * hipbls_threshold_aggregate_batch: out_sigs, agg_status) and Verify(dv_pks[g], msg g, out_sigs[g]) of each
  * aggregate (verify_status, as hipbls_verify_batch).  A group whose aggregation failed reports its aggregation

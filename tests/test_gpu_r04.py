@@ -160,6 +160,58 @@ def test_c3_fused_sigagg_device_twin_bytes(impl, c3):
     assert d_gst.cpu().tolist() == [0] * G and d_vst.cpu().tolist() == [0] * G
 
 
+def test_c3_calls_in_flight_on_two_streams(impl, c3):
+    """Four sigagg calls on different inputs enqueued back to back, alternating two streams (the library's two
+    workspace sets, each call's phase A chained behind the previous call's): every call's bytes and statuses equal
+    the same call made alone through the host API, including a group with an undecodable partial."""
+    import torch
+    groups, secrets_, roots, dv_pks, offpath = c3
+    dev = torch.device("cuda", 0)
+    B = 2500
+    batches = []
+    for b in range(4):
+        gs = [list(g) for g in groups[b * B:(b + 1) * B]]
+        if b == 1:
+            i, sig = gs[7][2]
+            gs[7][2] = (i, bytes([sig[0] ^ 0x01]) + sig[1:])  # not a valid encoding: the group's aggregate fails
+        batches.append((gs, roots[b * B:(b + 1) * B], dv_pks[b * B:(b + 1) * B]))
+
+    def u8(blobs):
+        return torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8).to(dev)
+
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    torch.cuda.synchronize(dev)
+    outs = []
+    for b, (gs, rs, pks) in enumerate(batches):
+        ids = [i for grp in gs for i, _ in grp]
+        offs = [0]
+        for grp in gs:
+            offs.append(offs[-1] + len(grp))
+        t = dict(psig=u8([x for grp in gs for _, x in grp]), pid=torch.tensor(ids, dtype=torch.int64).to(dev),
+                 poff=torch.tensor(offs, dtype=torch.int64).to(dev), dpk=u8(pks), msg=u8(rs),
+                 moff=torch.arange(0, 32 * (B + 1), 32, dtype=torch.int64).to(dev),
+                 agg=torch.zeros(B * 96, dtype=torch.uint8, device=dev),
+                 gst=torch.full((B,), -1, dtype=torch.int32, device=dev),
+                 vst=torch.full((B,), -1, dtype=torch.int32, device=dev), n_parts=len(ids))
+        outs.append(t)
+    torch.cuda.synchronize(dev)
+    for b, t in enumerate(outs):
+        rc = impl.lib.hipbls_threshold_aggregate_verify_batch_device(
+            t["psig"].data_ptr(), t["pid"].data_ptr(), t["poff"].data_ptr(), B, t["n_parts"], t["dpk"].data_ptr(),
+            t["msg"].data_ptr(), t["moff"].data_ptr(), t["agg"].data_ptr(), t["gst"].data_ptr(), t["vst"].data_ptr(),
+            ctypes.c_void_p(streams[b % 2].cuda_stream))
+        assert rc == 0
+    torch.cuda.synchronize(dev)
+    for b, (gs, rs, pks) in enumerate(batches):
+        res, vst = impl.batch_threshold_aggregate_verify([dict(g) for g in gs], pks, rs)
+        got = bytes(outs[b]["agg"].cpu().numpy().tobytes())
+        want = b"".join(r if isinstance(r, bytes) else bytes(96) for r in res)
+        assert got == want, "batch %d bytes" % b
+        assert outs[b]["vst"].cpu().tolist() == list(vst), "batch %d verify statuses" % b
+        gst = outs[b]["gst"].cpu().tolist()
+        assert (gst[7] != 0) == (b == 1) and sum(1 for x in gst if x != 0) == (1 if b == 1 else 0), b
+
+
 def test_c1_workload_partials_aggregates_verify(impl):
     """BASELINE configs[0] on the GPU: 250 DVs x 4-of-6.  1,000 partial Verify through the drop-in n = 1 call from 16
     threads (the queue) == the batch call == oracle sample; 250 ThresholdAggregate + Verify of each aggregate in one
