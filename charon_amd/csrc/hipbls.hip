@@ -1385,7 +1385,9 @@ int rlc_range(Context& c, const uint8_t* pks, const uint32_t* key_idx, const uin
 // partials or by a committee is hashed once, and once across batches while it stays cached.  Statuses are exactly
 // the per-item Verify's (rlc.h).  Batches with a key outside the table take the wire-format Verify.
 std::atomic<uint64_t> g_q_max_batch{65536};
-std::atomic<uint32_t> g_q_gather_us{200};
+// 50 us: a lone synchronous call (the parsigex loop) pays at most this before its launch; callers arriving while a
+// batch runs coalesce into the next one regardless (two batches in flight).
+std::atomic<uint32_t> g_q_gather_us{50};
 constexpr uint64_t kQueueKeyedMin = 8;  // without the H(m) cache, batches below this take the lane-pair Verify
 
 // Copies a wire-format batch in and launches it on slot k; the status comes back into the slot's pinned buffer and
@@ -1564,7 +1566,7 @@ void queue_worker(Context* cp) {
       const bool ready = sl.rc != HIPBLS_OK || hipEventQuery(sl.done_ev) != hipErrorNotReady;
       if (!ready && (int)q.inflight.size() < VerifyQueue::kSlots) {
         // a slot is free: wait for new work or the batch, whichever comes first (arrivals launch at once)
-        q.cv_work.wait_for(lk, std::chrono::microseconds(100),
+        q.cv_work.wait_for(lk, std::chrono::microseconds(20),  // completion polled every 20 us
                            [&] { return q.stop || (!q.open.empty() && q.open.front()->n() > 0); });
         continue;
       }

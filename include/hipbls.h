@@ -114,7 +114,7 @@ int hipbls_verify(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, con
 int hipbls_verify_submit(const uint8_t* pk48, const uint8_t* msg, uint64_t msg_len, const uint8_t* sig96,
                          uint64_t* ticket);
 int hipbls_verify_wait(uint64_t ticket, int32_t* status);
-/* Queue policy (defaults 65,536 items, 200 us) and counters (batches launched, items verified), summed over the
+/* Queue policy (defaults 65,536 items, 50 us) and counters (batches launched, items verified), summed over the
  * devices.  An item goes to the device its message hashes to, so the partials of one signing root meet in one
  * batch.  A batch of >= 8 items whose keys are all in the resident pubshare table runs as an RLC BatchVerify with
  * keys by index over its distinct messages, through the H(m) cache (statuses unchanged); the number of batches
