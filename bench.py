@@ -79,6 +79,9 @@ def parse():
                          "invalid partial), ii_all_valid (ii, no invalid partial)")
     ap.add_argument("--c5", type=int, default=1, help="time the C5 full-slot mix (0 = skip)")
     ap.add_argument("--keys", type=int, default=1, help="also time C2 / C4 with the resident pubshare table (0 = skip)")
+    ap.add_argument("--host-path", type=int, default=1,
+                    help="time the host-buffer calls charon's Go code makes (C2 hipbls_verify_batch[_keys], C3 "
+                         "hipbls_threshold_aggregate_verify_batch), PCIe copies included; rank 0 (0 = skip)")
     ap.add_argument("--latency-calls", type=int, default=1000,
                     help="synchronous n = 1 tbls.Verify calls (hipbls_verify on an idle queue) timed one after another, "
                          "the unpatched parsigex loop's shape (0 = skip; rank 0 only)")
@@ -585,6 +588,53 @@ def main():
         if tagg2:
             tagg_roofline["frac_two_streams"] = round(unit * MADS_PER_FPMUL * (tagg2 / world) / 1e12 / MAD_PEAK_T, 4)
 
+    # ---- the host-buffer calls charon's Go side makes (INTEGRATION.md "What charon reaches"): tbls.BatchVerify ->
+    # hipbls_verify_batch, or hipbls_verify_batch_keys once app loaded the pubshare table; sigagg.NewFused ->
+    # hipbls_threshold_aggregate_verify_batch.  Inputs copied in and statuses / aggregates copied out inside every call
+    # (the PCIe-inclusive rate; `value` stays the resident-input rate).  Rank 0, this rank's items, untimed by the step
+    # loop's barrier.
+    host_path = None
+    if args.host_path and rank == 0:
+        from charon_amd.tbls import _offsets
+        host_path = {"note": "host buffers in and out per call (cgo's path), rank 0's items, synchronous calls"}
+        blob, offs = _offsets(roots)
+        c_pk, c_sig = b"".join(pks), b"".join(sigs)
+        c_st = (ctypes.c_int32 * n)()
+
+        def hstep():
+            assert lib.hipbls_verify_batch(c_pk, blob, offs, c_sig, n, c_st) == 0
+
+        hstep()
+        th = timed_loop(hstep, args.steps, dev, lambda: None, 1)
+        assert list(c_st) == st, "host-buffer C2 statuses differ from the device call"
+        host_path["c2_verify_batch_per_s"] = round(n * args.steps / th, 1)
+        if args.keys:
+            kidx = (ctypes.c_uint32 * n)(*[pos[p] for p in pks])
+
+            def hkstep():
+                assert lib.hipbls_verify_batch_keys(kidx, blob, offs, c_sig, n, c_st) == 0
+
+            hkstep()
+            thk = timed_loop(hkstep, args.steps, dev, lambda: None, 1)
+            assert list(c_st) == st, "host-buffer keyed C2 statuses differ"
+            host_path["c2_verify_batch_keys_per_s"] = round(n * args.steps / thk, 1)
+        if args.tagg_groups > 0:
+            gblob, goffs = _offsets(droots)
+            c_psig, c_dpk = b"".join(psigs), b"".join(dv_pks)
+            c_pid = (ctypes.c_int64 * len(pids))(*pids)
+            c_poff = (ctypes.c_uint64 * len(poffs))(*poffs)
+            c_out = ctypes.create_string_buffer(96 * G)
+            c_ast, c_vst = (ctypes.c_int32 * G)(), (ctypes.c_int32 * G)()
+
+            def hc3():
+                assert lib.hipbls_threshold_aggregate_verify_batch(c_psig, c_pid, c_poff, G, c_dpk, gblob, goffs, c_out,
+                                                                   c_ast, c_vst) == 0
+
+            hc3()
+            th3 = timed_loop(hc3, args.tagg_steps, dev, lambda: None, 1)
+            assert set(c_ast) == {0} and set(c_vst) == {0} and c_out.raw == b"".join(want_aggs), "host C3"
+            host_path["c3_threshold_aggregate_verify_batch_per_s"] = round(G * args.tagg_steps / th3, 1)
+
     # ---- C4: RLC BatchVerify of the 1M-partial node batch, validator-index slices over the ranks (strong scaling:
     # the node batch is fixed); node bitmap all-gathered inside the timed step
     rlc = {}
@@ -809,6 +859,7 @@ def main():
                        "parallelism": "shard-by-validator-index x %d (RCCL all-gather of the verify bitmaps)" % world},
             "pairings_per_s": round(2 * value, 1),
             "drop_in_latency": latency,
+            "host_path": host_path,
             "verified_partial_sigs_per_s_pubshare_table": round(keys_rate, 1) if keys_rate else None,
             "threshold_aggregates_per_s": round(tagg, 1) if tagg else None,
             "threshold_aggregates_per_s_two_streams": round(tagg2, 1) if tagg2 else None,

@@ -5,17 +5,34 @@ libhipbls.so carries a clang offload bundle (section .hip_fatbin, magic __CLANG_
 every kernel with `.private_segment_fixed_size` (scratch bytes per lane), `.vgpr_count`, `.group_segment_fixed_size`
 (LDS) and the rest.
 
-Why it matters: each hardware queue that runs a kernel holds a scratch allocation sized by that
-kernel's private segment over the waves the device can hold, and HIP spreads a process's streams over
-GPU_MAX_HW_QUEUES (4) hardware queues.  Round 3 saw HSA_STATUS_ERROR_OUT_OF_RESOURCES (a process abort, not an error
-code) under 32-64 concurrent callers once every queue carried ~17.9 KB/lane kernels; the fix was headroom
-(12.7 KB/lane) plus one stream per queue.  `build.py` now refuses a library whose deepest kernel exceeds
-PRIVATE_SEGMENT_BUDGET, so a regression fails the build instead of aborting a node under load.
+Why it matters: each hardware queue that dispatches a kernel holds a scratch block of the kernel's
+private segment x 64 lanes x 32 wave slots per CU x 256 CUs, rounded to 2 MiB (measured: 1,040 B/lane -> 520 MiB,
+12,480 B/lane -> 6,240 MiB, profiles/r05/r05_scratch_probe.txt and _layout.txt), and every queue of the process takes
+its block from one 32 GiB region per device (HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX), first fit.  A block that grows
+leaves a hole, so four queues grown in stages to 12,480 B/lane left no 6.1 GiB gap for a fifth queue: the round-4
+abort (HSA_STATUS_ERROR_OUT_OF_RESOURCES).  The library now reserves its four queues' blocks once, contiguously, at
+init, so the rest of the region stays one free block.  The budget is what keeps that rest large enough for one more
+queue running the library's deepest kernel: (LIBRARY_QUEUES + 1) blocks within the region.  `build.py` refuses a
+library whose deepest kernel exceeds it, so a regression fails the build instead of aborting a node under load.
 """
 import struct
 
-# Bytes of scratch per lane that any kernel may use (round-3 maximum: k_verify_pair_lq4, 12,744 B).
-PRIVATE_SEGMENT_BUDGET = 13312
+SCRATCH_REGION = 32 << 30      # HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX on MI355X (profiles/r05/r05_scratch_probe.txt)
+WAVE_SLOTS = 64 * 32 * 256     # lanes per wave x scratch wave slots per CU (KFD max_slots_scratch_cu) x CUs
+BLOCK_ALIGN = 2 << 20          # blocks are placed on 2 MiB boundaries
+LIBRARY_QUEUES = 4             # the library's streams per device (hipbls_device_streams), one hardware queue each
+HEADROOM_QUEUES = 1            # queues of the same depth the rest of the region must still hold
+
+
+def derived_budget(region=SCRATCH_REGION, queues=LIBRARY_QUEUES + HEADROOM_QUEUES):
+    """Largest private segment (bytes per lane, a multiple of 16) whose 2 MiB-aligned block fits `queues` times."""
+    block = region // queues // BLOCK_ALIGN * BLOCK_ALIGN
+    return block // WAVE_SLOTS // 16 * 16
+
+
+# Bytes of scratch per lane that any kernel may use: 13,104 B (the deepest at the end of round 4: k_rlcb_chunks,
+# 12,480 B).  The reserve kernels (k_scratch_reserve<S>) stop at the same figure.
+PRIVATE_SEGMENT_BUDGET = derived_budget()
 BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 NT_AMDGPU_METADATA = 32

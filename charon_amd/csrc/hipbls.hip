@@ -20,6 +20,8 @@
 //   * A goroutine can move between OS threads between two calls, and hipSetDevice is per host thread, so every
 //     entry point binds its context's device on the calling thread before it touches memory or streams.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <array>
@@ -41,6 +43,7 @@
 #include <sys/random.h>
 
 #include "kernels.h"
+#include "ranges.h"
 
 // The eight-lane latency path (verify_lat.hip, its own translation unit: BLS_FP2_PAIR build in namespace bls_fp2p).
 namespace bls_fp2p {
@@ -124,6 +127,7 @@ struct QSlot {
   uint64_t h_cap = 0;
   std::shared_ptr<VBatch> b;
   int rc = HIPBLS_OK;
+  std::chrono::steady_clock::time_point launched;
 };
 
 // Per-context submission queue (worker, streams and buffers of its own).
@@ -137,6 +141,8 @@ struct VerifyQueue {
   std::thread worker;
   bool started = false, stop = false;
   uint64_t batches = 0, items = 0, keyed = 0, overlapped = 0;
+  uint64_t wakeups = 0;   // completion polls of the worker (hipbls_queue_worker_stats)
+  double batch_us[26] = {};  // running estimate of a wire batch's launch-to-completion time, per log2(batch size)
   hipStream_t stream = nullptr;  // the keyed path's stream
   QSlot slot[kSlots];
   std::deque<int> inflight;  // slots in launch order
@@ -179,7 +185,13 @@ struct Context {
   // launch_rlc_batch issue every record/wait pair on those within one call under c.mu, which
   // is what makes the sharing safe.  sigagg in one call uses neither: its workspace sets (tv_*) carry their own events.
   hipEvent_t ws_done = nullptr, ws_done_rlc = nullptr;
-  uint64_t r_windows = 0;        // window count of this context's last RLC call (hipbls_rlc_stats)
+  // A caller stream that would put the library's kernels on a hardware queue of its own (non-default priority, a CU
+  // mask) is joined to the library stream instead (StreamJoin): these events carry the ordering.
+  hipEvent_t ev_join_in = nullptr, ev_join_out = nullptr;
+  int stream_prio = 0;                // the library streams' priority (the device default)
+  std::vector<uint32_t> cu_mask;      // the library stream's CU mask (all CUs)
+  uint64_t joined = 0;                // *_device calls run on the library stream for that reason
+  uint64_t r_windows = 0;       // window count of this context's last RLC call (hipbls_rlc_stats)
   uint64_t r_call = 0;           // entry-point call that call belonged to
   // batch-wide RLC check (rlcb.h): MSM inputs and stages, Miller values, verdict flag
   DevBuf m_pts, m_sc, m_cnt, m_off, m_cur, m_list, m_B, m_P, m_Sg, m_Wp, m_W, m_F, m_F2, m_flag, m_Fs;
@@ -234,6 +246,177 @@ int arg_err(const char* what) {
 int nctx() { return g_nctx.load(std::memory_order_acquire); }
 Context& ctx(int k) { return *g_ctxs[k]; }
 
+// ============================================================================ scratch
+// Each hardware queue that dispatches a kernel holds a scratch block of (private segment per lane) x 64 lanes x 32
+// wave slots per CU x CUs, rounded to 2 MiB: 520 MiB for 1,040 B/lane, 6,240 MiB for 12,480 B/lane
+// (profiles/r05/r05_scratch_probe.txt, _layout.txt).  The blocks come from one region per device whose size is the
+// agent's scratch limit (HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX: 32 GiB on MI355X), placed first-fit: a queue whose
+// block must grow for a deeper kernel takes a new block and frees the old one, which leaves a hole.  Four queues grown
+// in stages to 12,480 B/lane hold 24.4 GiB but leave at most 4.6 GiB contiguous of the 7.6 GiB free, so a fifth
+// queue (a priority stream) asking for 6.1 GiB failed: HSA_STATUS_ERROR_OUT_OF_RESOURCES, a process abort (round 4).
+// So the library (1) reserves each of its queues' blocks once at full size in stream order at init (contiguous, no
+// holes: the rest of the region stays one block), (2) never launches on a stream that would give it a queue of its
+// own (StreamJoin), and (3) refuses at init a device whose limit cannot hold its queues.
+constexpr uint32_t kCuMaskWords = 16;  // 512 CUs
+constexpr uint64_t kScratchAlign = 2ull << 20;
+constexpr uint32_t kLaneBytes = 64;
+
+struct Scratch {
+  uint64_t per_lane = 0;   // deepest private segment of the library's kernels (bytes per lane)
+  uint64_t per_queue = 0;  // the block one hardware queue holds for it
+  uint64_t limit = 0;      // the device's scratch region (0: the runtime does not report one)
+  uint32_t slots = 0;      // scratch wave slots per CU
+  uint32_t cus = 0;
+  uint32_t queues = 0;     // GPU_MAX_HW_QUEUES (HIP's normal-priority hardware queues per process)
+  std::string deepest;
+};
+std::map<int, Scratch> g_scratch;      // per device, written once at init
+std::atomic<bool> g_join_all{false};   // every *_device call runs on the library's streams (StreamJoin)
+
+// Reserve kernels: a private segment of S bytes per lane (a volatile frame of S - 16 bytes; the frame adds 16), never
+// touched when n == 0.  Launched once per library stream at init so each queue's block is allocated at full size.
+template <int S>
+__global__ void k_scratch_reserve(uint32_t* out, uint32_t n) {
+  constexpr int W = (S - 16) / 4;
+  volatile uint32_t frame[W];
+  if (n) {
+    frame[n % W] = n;
+    out[threadIdx.x] = frame[(n * 7u) % W];
+  }
+}
+
+struct KernelRef {
+  const char* name;
+  const void* fn;
+};
+#define KREF(k) {#k, reinterpret_cast<const void*>(&k)}
+#define KREF8(k) {#k, reinterpret_cast<const void*>(&bls_fp2p::k)}
+// Every kernel the library launches (tests/test_kernel_resources.py: the same set as both code objects hold, minus the
+// reserve kernels).
+const KernelRef kKernels[] = {
+    KREF(k_fav_batch), KREF(k_fp12_prod64), KREF(k_g1_decode), KREF(k_g1m_count), KREF(k_g1m_fix), KREF(k_g1m_fold),
+    KREF(k_g1m_hist), KREF(k_g1m_plan), KREF(k_g1m_rank), KREF(k_g1m_run), KREF(k_g1m_scatter), KREF(k_g2_decode),
+    KREF(k_g2_sum_final), KREF(k_g2_sum_partial), KREF(k_msm_fix), KREF(k_msm_hist), KREF(k_msm_run), KREF(k_msm_scan),
+    KREF(k_msm_scatter), KREF(k_msm_segment), KREF(k_msm_window), KREF(k_msm_wsum), KREF(k_pubtab_load),
+    KREF(k_recover_secret), KREF(k_rlc_fallback), KREF(k_rlc_fallback_lg2), KREF(k_rlc_hash), KREF(k_rlc_items),
+    KREF(k_rlc_window), KREF(k_rlc_window_lg2), KREF(k_rlcb_chunks), KREF(k_rlcb_items), KREF(k_rlcb_mark),
+    KREF(k_scan_apply), KREF(k_scan_part), KREF(k_scan_top), KREF(k_sign), KREF(k_signing_roots), KREF(k_sk_to_pk),
+    KREF(k_tagg_scale), KREF(k_tagg_sum), KREF(k_tagg_sum_s), KREF(k_tagg_unscale), KREF(k_threshold_split),
+    KREF(k_tv_check_unscale), KREF(k_tv_join), KREF(k_tv_phase_a), KREF(k_tv_prep_pk), KREF(k_tv_prep_pk2),
+    KREF(k_verify_fused), KREF(k_verify_keys), KREF(k_verify_pair_lg2), KREF(k_verify_pair_lq4),
+    KREF(k_verify_pair_single), KREF(k_verify_prep), KREF(k_zero_sig_status), KREF8(k_g1m_miller8),
+    KREF8(k_rlcb_final8), KREF8(k_rlcb_sfactor8), KREF8(k_verify_pair_lq8), KREF8(k_verify_prep8),
+};
+#define RES(s) reinterpret_cast<const void*>(&k_scratch_reserve<s>)
+// 8 KiB to the per-lane budget (charon_amd/codeobj.py PRIVATE_SEGMENT_BUDGET, 13,104 B) in 256-byte steps: at most
+// 128 MiB of a queue's block beyond the deepest kernel's
+const void* const kReserve[] = {
+    RES(8192), RES(8448), RES(8704), RES(8960), RES(9216), RES(9472), RES(9728), RES(9984), RES(10240), RES(10496),
+    RES(10752), RES(11008), RES(11264), RES(11520), RES(11776), RES(12032), RES(12288), RES(12544), RES(12800),
+    RES(13056), RES(13104),
+};
+#undef RES
+#undef KREF
+#undef KREF8
+
+std::string kernel_names() {
+  std::string s;
+  for (const KernelRef& k : kKernels) {
+    if (!s.empty()) s += ' ';
+    s += k.name;
+  }
+  return s;
+}
+
+// The device's scratch region, from the HSA agent at the device's PCI location (0 when the runtime has no such query).
+uint64_t scratch_limit(int device) {
+  int bus = -1, dev = -1, dom = -1;
+  if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainId, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  struct Find {
+    uint32_t bdf, dom;
+    hsa_agent_t agent;
+    bool found;
+  } f{(uint32_t)((bus << 8) | (dev << 3)), (uint32_t)dom, {}, false};
+  if (hsa_init() != HSA_STATUS_SUCCESS) return 0;  // HIP already holds the runtime open: this only adds a reference
+  hsa_iterate_agents(
+      [](hsa_agent_t a, void* p) -> hsa_status_t {
+        Find& f = *(Find*)p;
+        hsa_device_type_t t;
+        uint32_t bdf = 0, dom = 0;
+        if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+          return HSA_STATUS_SUCCESS;
+        if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS ||
+            hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) != HSA_STATUS_SUCCESS)
+          return HSA_STATUS_SUCCESS;
+        if ((bdf & ~7u) == f.bdf && dom == f.dom) {
+          f.agent = a;
+          f.found = true;
+          return HSA_STATUS_INFO_BREAK;
+        }
+        return HSA_STATUS_SUCCESS;
+      },
+      &f);
+  uint64_t lim = 0;
+  if (!f.found ||
+      hsa_agent_get_info(f.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX, &lim) != HSA_STATUS_SUCCESS)
+    lim = 0;
+  return lim;
+}
+
+int scratch_budget(int device, Scratch& s) {
+  s = Scratch();
+  for (const KernelRef& k : kKernels) {
+    hipFuncAttributes fa;
+    HIP_TRY(hipFuncGetAttributes(&fa, k.fn));
+    if ((uint64_t)fa.localSizeBytes > s.per_lane) {
+      s.per_lane = fa.localSizeBytes;
+      s.deepest = k.name;
+    }
+  }
+  int threads = 0, warp = 0, cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&threads, hipDeviceAttributeMaxThreadsPerMultiProcessor, device));
+  HIP_TRY(hipDeviceGetAttribute(&warp, hipDeviceAttributeWarpSize, device));
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  s.slots = warp > 0 ? (uint32_t)(threads / warp) : 32;
+  s.cus = (uint32_t)cus;
+  const uint64_t raw = s.per_lane * kLaneBytes * s.slots * s.cus;
+  s.per_queue = (raw + kScratchAlign - 1) / kScratchAlign * kScratchAlign;
+  const char* q = getenv("GPU_MAX_HW_QUEUES");
+  s.queues = q && atoi(q) > 0 ? (uint32_t)atoi(q) : 4u;
+  s.limit = scratch_limit(device);
+  return HIPBLS_OK;
+}
+
+// One dispatch of the smallest reserve kernel at least as deep as the library's deepest kernel on each stream, in
+// order, then a wait: each hardware queue takes its block now, at full size, next to the previous one.
+int scratch_reserve(const hipStream_t* ss, int n, uint64_t per_lane) {
+  const void* fn = nullptr;
+  for (const void* r : kReserve) {
+    hipFuncAttributes fa;
+    HIP_TRY(hipFuncGetAttributes(&fa, r));
+    if ((uint64_t)fa.localSizeBytes >= per_lane) {
+      fn = r;
+      break;
+    }
+  }
+  if (!fn) return HIPBLS_OK;  // deeper than the largest reserve kernel: blocks grow on first use as before
+  void* args[2];
+  uint32_t* none = nullptr;
+  uint32_t zero = 0;
+  args[0] = &none;
+  args[1] = &zero;
+  for (int k = 0; k < n; ++k) {
+    HIP_TRY(hipLaunchKernel(fn, dim3(1), dim3(64), args, 0, ss[k]));
+    HIP_TRY(hipStreamSynchronize(ss[k]));
+  }
+  return HIPBLS_OK;
+}
+
 int init_locked(const std::vector<int>& ids) {
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
@@ -263,7 +446,39 @@ int init_locked(const std::vector<int>& ids) {
     c->q.stream = it->second[3];
     HIP_TRY(hipEventCreateWithFlags(&c->ws_done, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ws_done_rlc, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_join_in, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_join_out, hipEventDisableTiming));
+    HIP_TRY(hipStreamGetPriority(c->stream, &c->stream_prio));
+    c->cu_mask.assign(kCuMaskWords, 0);
+    if (hipExtStreamGetCUMask(c->stream, kCuMaskWords, c->cu_mask.data()) != hipSuccess) {
+      (void)hipGetLastError();
+      c->cu_mask.clear();  // no CU-mask query on this runtime: only the priority decides
+    }
     made.push_back(c);
+  }
+  // Scratch: refuse a device whose scratch limit cannot hold the library's own hardware queues at
+  // its deepest kernel, and reserve each library queue's scratch once, at full size, in stream order.
+  for (auto& kv : dev_streams) {
+    HIP_TRY(hipSetDevice(kv.first));
+    Scratch sb;
+    int rc = scratch_budget(kv.first, sb);
+    if (rc) return rc;
+    if (sb.limit && (uint64_t)kStreamsPerDevice * sb.per_queue > sb.limit) {
+      g_last_error = "scratch: " + std::to_string(kStreamsPerDevice) + " hardware queues x " +
+                     std::to_string(sb.per_queue) + " B (" + std::to_string(sb.per_lane) + " B per lane, " + sb.deepest +
+                     ") exceed device " + std::to_string(kv.first) + "'s scratch limit of " + std::to_string(sb.limit) +
+                     " B";
+      return HIPBLS_ERR_DEVICE;
+    }
+    // GPU_MAX_HW_QUEUES normal-priority queues that could all carry the library's kernels through callers' streams
+    // must fit as well; otherwise every *_device call runs on the library's own streams (StreamJoin).
+    if (sb.limit && (uint64_t)sb.queues * sb.per_queue > sb.limit) g_join_all = true;
+    const char* rs = getenv("HIPBLS_SCRATCH_RESERVE");
+    if (!(rs && rs[0] == '0')) {
+      rc = scratch_reserve(kv.second.data(), kStreamsPerDevice, sb.per_lane);
+      if (rc) return rc;
+    }
+    g_scratch[kv.first] = sb;
   }
   const char* t = getenv("HIPBLS_TIMING");
   if (t && t[0] == '1') g_timing = true;
@@ -342,7 +557,57 @@ Context& ctx_of(const void* p) {
   return ctx(0);
 }
 
-hipStream_t pick(Context& c, void* stream) { return stream ? (hipStream_t)stream : c.stream; }
+// Whether a caller's stream shares the hardware queues the library's own streams hold: HIP spreads streams of the
+// default priority without a CU mask over GPU_MAX_HW_QUEUES queues per process, and gives a priority stream (high or
+// low) or a CU-masked one a queue of its own (profiles/r05/r05_scratch_probe.txt: a fifth normal stream took no new
+// block, a high- and a low-priority stream each took one).
+bool shares_library_queues(Context& c, hipStream_t st) {
+  if (g_join_all.load()) return false;
+  int prio = 0;
+  if (hipStreamGetPriority(st, &prio) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (prio != c.stream_prio) return false;
+  if (c.cu_mask.empty()) return true;
+  uint32_t m[kCuMaskWords] = {};
+  if (hipExtStreamGetCUMask(st, kCuMaskWords, m) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return std::equal(c.cu_mask.begin(), c.cu_mask.end(), m);
+}
+
+// The stream a *_device call launches on.  The caller's stream when it shares the library's hardware queues;
+// otherwise the context's library stream, joined to the caller's both ways (the call starts after the caller's
+// earlier work and the caller's later work waits for the call), so the library's kernels never make the process hold
+// one more queue's scratch block.  Declared after ENTER_CTX: it runs under the context lock, and
+// the destructor enqueues the join-back before the lock is released.
+struct StreamJoin {
+  Context& c;
+  hipStream_t user = nullptr, s = nullptr;
+  bool joined = false;
+  StreamJoin(Context& cc, void* stream) : c(cc), user((hipStream_t)stream), s(stream ? (hipStream_t)stream : cc.stream) {}
+  int begin() {
+    if (!user || user == c.stream || shares_library_queues(c, user)) return HIPBLS_OK;
+    HIP_TRY(hipEventRecord(c.ev_join_in, user));
+    HIP_TRY(hipStreamWaitEvent(c.stream, c.ev_join_in, 0));
+    s = c.stream;
+    joined = true;
+    c.joined += 1;
+    return HIPBLS_OK;
+  }
+  ~StreamJoin() {
+    if (joined && hipEventRecord(c.ev_join_out, c.stream) == hipSuccess) (void)hipStreamWaitEvent(user, c.ev_join_out, 0);
+  }
+};
+#define ON_STREAM(c, stream, s)        \
+  StreamJoin _sj((c), (stream));       \
+  {                                    \
+    const int _jrc = _sj.begin();      \
+    if (_jrc) return _jrc;             \
+  }                                    \
+  const hipStream_t s = _sj.s
 
 // Workspace ordering: the call's stream waits for the previous workspace user, and publishes its own end.
 enum { WS_GEN = 0, WS_RLC = 1 };
@@ -356,28 +621,7 @@ int ws_end(Context& c, hipStream_t s, int group = WS_GEN) {
 }
 
 // ============================================================================ splitting a batch across contexts
-// Contiguous ranges: bounds[0] = 0 < ... < bounds[parts] = n, as equal as possible.  With run keys (e.g. the message
-// index of each item, equal for all partials of one validator), an inner bound moves forward to the start of the
-// next run, so a run never straddles two devices, unless that would move it by more than half a share.
-std::vector<uint64_t> plan_ranges(uint64_t n, uint64_t parts, const uint32_t* keys) {
-  if (parts < 1) parts = 1;
-  if (parts > n && n > 0) parts = n;
-  std::vector<uint64_t> b(parts + 1);
-  b[0] = 0;
-  b[parts] = n;
-  const uint64_t share = parts ? n / parts : 0;
-  for (uint64_t k = 1; k < parts; ++k) {
-    uint64_t x = (uint64_t)((unsigned __int128)n * k / parts);
-    if (keys && x > 0 && x < n) {
-      const uint64_t lim = x + share / 2;
-      uint64_t y = x;
-      while (y < n && y < lim && keys[y] == keys[y - 1]) ++y;
-      if (y == n || keys[y] != keys[y - 1]) x = y;  // the next run start, within half a share
-    }
-    b[k] = x < b[k - 1] ? b[k - 1] : x;
-  }
-  return b;
-}
+// plan_ranges: charon_amd/csrc/ranges.h (host-only, also built by the sanitizer test, tests/test_sanitizers.py).
 
 // How many ranges a batch of n units gets: one per context, but never ranges below min_per units.
 uint64_t parts_for(uint64_t n, uint64_t min_per) {
@@ -1093,10 +1337,23 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
   int32_t* agg_inf = (int32_t*)c.tv_aux[p].p;
   uint32_t* pts = (uint32_t*)c.tv_pts[p].p;
   int32_t* pst = (int32_t*)c.tv_pst[p].p;
+  if (!c.tv_phase) HIP_TRY(hipEventCreateWithFlags(&c.tv_phase, hipEventDisableTiming));
   HIP_TRY(hipStreamWaitEvent(s, c.tv_done[p], 0));
+  // From here on every exit records tv_done[p] (and tv_phase, if phase A's end was not recorded yet) on s: the call
+  // two later reuses workspace set p and waits on tv_done[p], so a call that fails after enqueueing work must still
+  // publish the end of what it enqueued, or the next user of the set could overwrite buffers its kernels still read.
+  struct TvEnd {
+    Context& c;
+    hipStream_t s;
+    int p;
+    bool phase = false;
+    ~TvEnd() {
+      if (!phase) (void)hipEventRecord(c.tv_phase, s);
+      (void)hipEventRecord(c.tv_done[p], s);
+    }
+  } tv_end{c, s, p};
   // Phase A after the previous call's phase A, whatever its stream: two calls' phase A would only share the same
   // wave slots, while this call's phase A beside the previous call's check fills the SIMDs that check leaves idle.
-  if (!c.tv_phase) HIP_TRY(hipEventCreateWithFlags(&c.tv_phase, hipEventDisableTiming));
   HIP_TRY(hipStreamWaitEvent(s, c.tv_phase, 0));
   int rc = HIPBLS_OK;
   if (BLS_TV_PAIR_HASH && n_groups <= kPairHashMaxVerify) {
@@ -1127,6 +1384,7 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
                      (const int32_t*)d_astatus, (const int32_t*)agg_inf, d_vstatus);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c.tv_phase, s));
+  tv_end.phase = true;
   if (use_quads(n_groups)) {
     rc = timed(c, "tv_check_unscale", s, [&] {
       hipLaunchKernelGGL(k_tv_check_unscale, dim3((unsigned)(grid_for(4 * n_groups) + grid_for(n_groups))),
@@ -1150,9 +1408,7 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
                          n_groups, (const uint32_t*)ws, (const int32_t*)agg_inf, (const int32_t*)d_astatus, d_out);
     });
   }
-  if (rc) return rc;
-  HIP_TRY(hipEventRecord(c.tv_done[p], s));
-  return HIPBLS_OK;
+  return rc;  // tv_end records tv_done[p]
 }
 
 int launch_fav(Context& c, const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_goff, uint64_t n_groups,
@@ -1512,6 +1768,15 @@ void batch_done(VerifyQueue& q, VBatch& b, int rc) {
 // The worker: up to kSlots wire batches in flight (the next one is copied in and launched while the previous one
 // runs, on its own stream), keyed batches run synchronously on the queue's stream.  An idle worker (nothing in
 // flight) waits gather_us for company before launching a small batch.
+int size_class(uint64_t n) {
+  int k = 0;
+  while (n > 1 && k < 25) {
+    n >>= 1;
+    ++k;
+  }
+  return k;
+}
+
 void queue_worker(Context* cp) {
   Context& c = *cp;
   VerifyQueue& q = c.q;
@@ -1552,6 +1817,7 @@ void queue_worker(Context* cp) {
       QSlot& sl = q.slot[k];
       sl.b = b;
       sl.rc = dev_ok ? wire_launch(c, sl, *b) : HIPBLS_ERR_DEVICE;
+      sl.launched = std::chrono::steady_clock::now();
       // A launch that failed after its first copy was queued never records done_ev, and batch_done frees the batch's
       // host vectors as soon as it is collected: drain the stream first so no queued copy reads freed memory.
       if (sl.rc != HIPBLS_OK && dev_ok) (void)hipStreamSynchronize(sl.stream);
@@ -1563,17 +1829,32 @@ void queue_worker(Context* cp) {
     if (!q.inflight.empty()) {  // collect the oldest batch in flight
       const int k = q.inflight.front();
       QSlot& sl = q.slot[k];
+      q.wakeups += 1;
       const bool ready = sl.rc != HIPBLS_OK || hipEventQuery(sl.done_ev) != hipErrorNotReady;
       if (!ready && (int)q.inflight.size() < VerifyQueue::kSlots) {
-        // a slot is free: wait for new work or the batch, whichever comes first (arrivals launch at once)
-        q.cv_work.wait_for(lk, std::chrono::microseconds(20),  // completion polled every 20 us
-                           [&] { return q.stop || (!q.open.empty() && q.open.front()->n() > 0); });
+        // A slot is free: wait for new work or the batch, whichever comes first (arrivals launch at once).  The
+        // completion is polled every 20 us, but only from 85 % of the running estimate of a batch's time on: a
+        // 12 ms n = 1 batch costs ~100 wakeups instead of ~600, at the same completion latency.
+        const auto now = std::chrono::steady_clock::now();
+        const auto due = sl.launched + std::chrono::microseconds((int64_t)(0.85 * q.batch_us[size_class(sl.b->n())]));
+        const auto until = due > now + std::chrono::microseconds(20) ? due : now + std::chrono::microseconds(20);
+        q.cv_work.wait_until(lk, until, [&] { return q.stop || (!q.open.empty() && q.open.front()->n() > 0); });
         continue;
+      }
+      if (sl.rc == HIPBLS_OK) {
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - sl.launched).count();
+        double& e = q.batch_us[size_class(sl.b->n())];
+        e = e > 0 ? 0.75 * e + 0.25 * us : us;
       }
       lk.unlock();
       const int rc = wire_finish(sl);
       lk.lock();
       q.inflight.pop_front();
+      // the next batch queued behind this one on the stream starts now: its estimate runs from here
+      if (!q.inflight.empty()) {
+        QSlot& nx = q.slot[q.inflight.front()];
+        nx.launched = std::max(nx.launched, std::chrono::steady_clock::now());
+      }
       std::shared_ptr<VBatch> b = std::move(sl.b);
       sl.b.reset();
       batch_done(q, *b, rc);
@@ -1971,6 +2252,47 @@ int hipbls_device_streams(int device) {
   return it == g_streams_per_device.end() ? 0 : it->second;
 }
 
+int hipbls_scratch_budget(int device, uint64_t* per_lane, uint64_t* per_queue, uint64_t* limit, uint32_t* queues) {
+  if (!per_lane || !per_queue || !limit || !queues) return arg_err("null output");
+  if (!nctx()) return arg_err("no context on that device");
+  auto it = g_scratch.find(device);
+  if (it == g_scratch.end()) return arg_err("no context on that device");
+  *per_lane = it->second.per_lane;
+  *per_queue = it->second.per_queue;
+  *limit = it->second.limit;
+  *queues = it->second.queues;
+  return HIPBLS_OK;
+}
+
+int hipbls_stream_joins(uint64_t* calls) {
+  if (!calls) return arg_err("null output");
+  *calls = 0;
+  const int n = nctx();
+  for (int k = 0; k < n; ++k) {
+    std::lock_guard<std::mutex> lk(ctx(k).mu);
+    *calls += ctx(k).joined;
+  }
+  return HIPBLS_OK;
+}
+
+const char* hipbls_kernel_names(void) {
+  static const std::string names = kernel_names();
+  return names.c_str();
+}
+
+int hipbls_queue_worker_stats(uint64_t* wakeups, uint64_t* batches) {
+  if (!wakeups || !batches) return arg_err("null output");
+  *wakeups = *batches = 0;
+  const int n = nctx();
+  for (int k = 0; k < n; ++k) {
+    VerifyQueue& q = ctx(k).q;
+    std::lock_guard<std::mutex> lk(q.mu);
+    *wakeups += q.wakeups;
+    *batches += q.batches;
+  }
+  return HIPBLS_OK;
+}
+
 int hipbls_device_slots(int32_t* ids, uint32_t cap) {
   const int n = nctx();
   for (int k = 0; k < n && ids && (uint32_t)k < cap; ++k) ids[k] = ctx(k).device;
@@ -2053,7 +2375,7 @@ int hipbls_verify_batch_device(const uint8_t* d_pks, const uint8_t* d_msgs, cons
   ENSURE_INIT();
   Context& c = ctx_of(d_status);
   ENTER_CTX(c);
-  const hipStream_t s = pick(c, stream);
+  ON_STREAM(c, stream, s);
   int rc = ws_begin(c, s);
   if (rc) return rc;
   rc = launch_verify(c, d_pks, d_msgs, d_msg_offsets, d_sigs, n, d_status, s, c.v_ws);
@@ -2184,8 +2506,9 @@ int hipbls_threshold_aggregate_verify_batch_device(const uint8_t* d_sigs, const 
   ENSURE_INIT();
   Context& c = ctx_of(d_agg_status);
   ENTER_CTX(c);
+  ON_STREAM(c, stream, s);
   return launch_tagg_verify(c, d_sigs, d_share_idx, d_group_offsets, n_groups, n_parts, d_dv_pks, d_msgs,
-                            d_msg_offsets, d_out_sigs, d_agg_status, d_verify_status, pick(c, stream));
+                            d_msg_offsets, d_out_sigs, d_agg_status, d_verify_status, s);
 }
 
 int hipbls_threshold_aggregate_batch_device(const uint8_t* d_sigs, const int64_t* d_share_idx,
@@ -2196,8 +2519,9 @@ int hipbls_threshold_aggregate_batch_device(const uint8_t* d_sigs, const int64_t
   ENSURE_INIT();
   Context& c = ctx_of(d_status);
   ENTER_CTX(c);
+  ON_STREAM(c, stream, s);
   return launch_tagg(c, d_sigs, d_share_idx, d_group_offsets, n_groups, n_parts, d_out_sigs, d_status,
-                     pick(c, stream));
+                     s);
 }
 
 int hipbls_sign_batch(const uint8_t* sks, const uint8_t* msgs, const uint64_t* msg_offsets, uint64_t n,
@@ -2220,7 +2544,8 @@ int hipbls_sign_batch_device(const uint8_t* d_sks, const uint8_t* d_msgs, const 
   ENSURE_INIT();
   Context& c = ctx_of(d_status);
   ENTER_CTX(c);
-  hipLaunchKernelGGL(k_sign, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, pick(c, stream), d_sks, d_msgs,
+  ON_STREAM(c, stream, s);
+  hipLaunchKernelGGL(k_sign, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_sks, d_msgs,
                      d_msg_offsets, n, d_out_sigs, d_status);
   HIP_TRY(hipGetLastError());
   return HIPBLS_OK;
@@ -2241,7 +2566,8 @@ int hipbls_secret_to_public_key_batch_device(const uint8_t* d_sks, uint64_t n, u
   ENSURE_INIT();
   Context& c = ctx_of(d_status);
   ENTER_CTX(c);
-  hipLaunchKernelGGL(k_sk_to_pk, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, pick(c, stream), d_sks, n, d_out_pks,
+  ON_STREAM(c, stream, s);
+  hipLaunchKernelGGL(k_sk_to_pk, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_sks, n, d_out_pks,
                      d_status);
   HIP_TRY(hipGetLastError());
   return HIPBLS_OK;
@@ -2273,8 +2599,9 @@ int hipbls_verify_aggregate_batch_device(const uint8_t* d_pks, uint64_t nkeys, c
   ENSURE_INIT();
   Context& c = ctx_of(d_status);
   ENTER_CTX(c);
+  ON_STREAM(c, stream, s);
   return launch_fav(c, d_pks, nkeys, d_key_offsets, n_groups, d_sigs, d_msgs, d_msg_offsets, d_status,
-                    pick(c, stream));
+                    s);
 }
 
 int hipbls_verify_aggregate(const uint8_t* pks, uint64_t n, const uint8_t* sig, const uint8_t* msg, uint64_t msg_len,
@@ -2327,7 +2654,8 @@ int hipbls_aggregate_device(const uint8_t* d_sigs, uint64_t n, uint8_t* d_out_si
   ENSURE_INIT();
   Context& c = ctx_of(d_status);
   ENTER_CTX(c);
-  return launch_aggregate(c, d_sigs, n, d_out_sig, d_status, pick(c, stream));
+  ON_STREAM(c, stream, s);
+  return launch_aggregate(c, d_sigs, n, d_out_sig, d_status, s);
 }
 
 int hipbls_threshold_split(const uint8_t* secret, const uint8_t* poly_tail, uint32_t total, uint32_t threshold,
@@ -2450,8 +2778,9 @@ int hipbls_batch_verify_rlc_device(const uint8_t* d_pks, const uint8_t* d_sigs, 
   ENSURE_INIT();
   Context& c = ctx_of(d_status);
   ENTER_CTX(c);
+  ON_STREAM(c, stream, s);
   return launch_rlc(c, d_pks, d_sigs, d_msg_idx, n, d_msgs, d_msg_offsets, n_msgs, parse_seed(seed32), d_status,
-                    pick(c, stream), g_call_seq.fetch_add(1) + 1);
+                    s, g_call_seq.fetch_add(1) + 1);
 }
 
 int hipbls_hcache_config(uint64_t capacity) {
@@ -2532,7 +2861,7 @@ int hipbls_verify_batch_keys_device(const uint32_t* d_key_idx, const uint8_t* d_
   ENSURE_INIT();
   Context& c = ctx_of(d_status);
   ENTER_CTX(c);
-  hipStream_t s = pick(c, stream);
+  ON_STREAM(c, stream, s);
   return timed(c, "verify_keys", s, [&] {
     hipLaunchKernelGGL(k_verify_keys, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_key_idx, c.t_size,
                        (const int32_t*)c.t_code.p, (const uint32_t*)c.t_tab.p, d_msgs, d_msg_offsets, d_sigs, n,
@@ -2569,8 +2898,9 @@ int hipbls_batch_verify_rlc_keys_device(const uint32_t* d_key_idx, const uint8_t
   ENSURE_INIT();
   Context& c = ctx_of(d_status);
   ENTER_CTX(c);
+  ON_STREAM(c, stream, s);
   return launch_rlc(c, nullptr, d_sigs, d_msg_idx, n, d_msgs, d_msg_offsets, n_msgs, parse_seed(seed32), d_status,
-                    pick(c, stream), g_call_seq.fetch_add(1) + 1, d_key_idx);
+                    s, g_call_seq.fetch_add(1) + 1, d_key_idx);
 }
 
 // Windows, failed windows and re-verified items of the newest RLC call, summed over the devices it ran on.

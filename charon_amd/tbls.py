@@ -117,6 +117,10 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_batch_verify_rlc_keys_device": ([vp, vp, vp, u64, vp, vp, u64, u8p, vp, vp], ctypes.c_int),
         "hipbls_kernel_timing": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), u64p], ctypes.c_int),
         "hipbls_kernel_timing_reset": ([], ctypes.c_int),
+        "hipbls_scratch_budget": ([ctypes.c_int, u64p, u64p, u64p, ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+        "hipbls_stream_joins": ([u64p], ctypes.c_int),
+        "hipbls_kernel_names": ([], ctypes.c_char_p),
+        "hipbls_queue_worker_stats": ([u64p, u64p], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -144,7 +148,8 @@ def exported_symbols() -> List[str]:
         "hipbls_rlc_set_mode", "hipbls_rlc_batch_stats", "hipbls_threshold_aggregate_verify_batch",
         "hipbls_threshold_aggregate_verify_batch_device", "hipbls_init_devices", "hipbls_device_slots",
         "hipbls_plan_ranges", "hipbls_queue_keyed_batches", "hipbls_deserialize_status", "hipbls_device_streams",
-        "hipbls_rlc_set_g1_msm_min",
+        "hipbls_rlc_set_g1_msm_min", "hipbls_scratch_budget", "hipbls_stream_joins", "hipbls_kernel_names",
+        "hipbls_queue_worker_stats",
     ]
 
 

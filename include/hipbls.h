@@ -61,7 +61,7 @@ enum {
 };
 
 /* Library/ABI version (bumped on any signature change). */
-#define HIPBLS_ABI_VERSION 11
+#define HIPBLS_ABI_VERSION 12
 int hipbls_abi_version(void);
 
 /* Bind the library to the n devices ids[0..n) (n <= 64; a device may repeat: each entry is one context, e.g. to
@@ -84,6 +84,20 @@ int hipbls_device_count(void);
  * stream), shared by every context bound to that device: at most 4 whatever the number of contexts, so the library's
  * launches never need more than GPU_MAX_HW_QUEUES hardware queues.  0 for a device without a context. */
 int hipbls_device_streams(int device);
+/* Scratch budget of `device`.  Each hardware queue that runs the library's kernels holds a scratch
+ * block of per_lane (the deepest kernel's private segment) x 64 lanes x 32 wave slots x CUs, rounded to 2 MiB
+ * (*per_queue); all of a process's queues on the device share one region of *limit bytes (the HSA agent's scratch
+ * limit, 32 GiB on MI355X; 0 = not reported), and *queues is GPU_MAX_HW_QUEUES (HIP's normal-priority queues per
+ * process).  The library holds 4 queues (hipbls_device_streams), reserves their blocks at init (HIPBLS_SCRATCH_RESERVE=0
+ * skips it), refuses a device where they do not fit (hipbls_init* -> HIPBLS_ERR_DEVICE), and never launches on a
+ * stream that would take another queue: a *_device call on a priority or CU-masked stream (or on any caller stream when
+ * *queues blocks would not fit) runs on the library stream, ordered after the caller's stream and before its later
+ * work (hipbls_stream_joins counts those calls).  So (*limit - 4 x *per_queue) is what other queues of the process
+ * may still hold.  HIPBLS_ERR_ARG for a device without a context. */
+int hipbls_scratch_budget(int device, uint64_t* per_lane, uint64_t* per_queue, uint64_t* limit, uint32_t* queues);
+int hipbls_stream_joins(uint64_t* calls);
+/* Space-separated names of every kernel the library can launch (no GPU needed; the scratch budget's kernel set). */
+const char* hipbls_kernel_names(void);
 /* Thread-local text of the last HIPBLS_ERR_DEVICE / HIPBLS_ERR_ARG. */
 const char* hipbls_last_error(void);
 /* Device index the library is bound to (-1 before the first call). */
@@ -122,6 +136,9 @@ int hipbls_verify_wait(uint64_t ticket, int32_t* status);
 int hipbls_queue_config(uint64_t max_batch, uint32_t gather_us);
 int hipbls_queue_stats(uint64_t* batches, uint64_t* items);
 int hipbls_queue_keyed_batches(uint64_t* batches);
+/* Completion polls of the queue workers (a batch in flight is polled every 20 us from 85 % of the running estimate
+ * of its time on) and wire batches collected, summed over the devices. */
+int hipbls_queue_worker_stats(uint64_t* wakeups, uint64_t* batches);
 
 /* ---------------------------------------------------------------- batched, host buffers ---- */
 

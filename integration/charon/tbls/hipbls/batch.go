@@ -32,8 +32,14 @@ func (HipBLS) BatchVerify(pks []tbls.PublicKey, msgs [][]byte, sigs []tbls.Signa
 	}
 	flat, offs := flatten(msgs)
 	status := make([]int32, n)
-	rc := C.hipbls_verify_batch((*C.uint8_t)(unsafe.Pointer(&pks[0][0])), u8(flat), u64(offs),
-		(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), C.uint64_t(n), i32(status))
+	var rc C.int
+	if kidx, ok := tableIndices(pks); ok { // keys by resident table index: no per-call decode or subgroup test
+		rc = C.hipbls_verify_batch_keys((*C.uint32_t)(unsafe.Pointer(&kidx[0])), u8(flat), u64(offs),
+			(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), C.uint64_t(n), i32(status))
+	} else {
+		rc = C.hipbls_verify_batch((*C.uint8_t)(unsafe.Pointer(&pks[0][0])), u8(flat), u64(offs),
+			(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), C.uint64_t(n), i32(status))
+	}
 	if rc != C.HIPBLS_OK {
 		return nil, devErr(rc)
 	}
@@ -63,9 +69,16 @@ func (HipBLS) BatchVerifyRLC(pks []tbls.PublicKey, sigs []tbls.Signature, msgIdx
 		return nil, errors.Wrap(err, "rlc seed")
 	}
 	status := make([]int32, n)
-	rc := C.hipbls_batch_verify_rlc((*C.uint8_t)(unsafe.Pointer(&pks[0][0])), (*C.uint8_t)(unsafe.Pointer(&sigs[0][0])),
-		(*C.uint32_t)(unsafe.Pointer(&msgIdx[0])), C.uint64_t(n), u8(flat), u64(offs), C.uint64_t(len(msgs)),
-		u8(seed[:]), i32(status))
+	var rc C.int
+	if kidx, ok := tableIndices(pks); ok { // keys by resident table index
+		rc = C.hipbls_batch_verify_rlc_keys((*C.uint32_t)(unsafe.Pointer(&kidx[0])),
+			(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), (*C.uint32_t)(unsafe.Pointer(&msgIdx[0])), C.uint64_t(n), u8(flat),
+			u64(offs), C.uint64_t(len(msgs)), u8(seed[:]), i32(status))
+	} else {
+		rc = C.hipbls_batch_verify_rlc((*C.uint8_t)(unsafe.Pointer(&pks[0][0])),
+			(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), (*C.uint32_t)(unsafe.Pointer(&msgIdx[0])), C.uint64_t(n), u8(flat),
+			u64(offs), C.uint64_t(len(msgs)), u8(seed[:]), i32(status))
+	}
 	if rc != C.HIPBLS_OK {
 		return nil, devErr(rc)
 	}

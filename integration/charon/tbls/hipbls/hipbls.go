@@ -1,7 +1,7 @@
 //go:build hipbls
 
 // Package hipbls implements tbls.Implementation on AMD MI355X (gfx950) GPUs through libhipbls, the C-ABI in
-// include/hipbls.h (ABI 11).  It replaces tbls.Herumi (tbls/herumi.go) method for method: same argument meaning,
+// include/hipbls.h (ABI 12).  It replaces tbls.Herumi (tbls/herumi.go) method for method: same argument meaning,
 // same error strings and wrapping, bit-identical keys, signatures and verdicts.  Every curve operation runs in the
 // library's HIP kernels; Go only range-checks 32-byte scalars (as herumi's SecretKey.Deserialize does) and moves
 // bytes.
@@ -24,6 +24,7 @@ import (
 	"fmt"
 	"io"
 	"math/big"
+	"sync"
 	"testing"
 	"unsafe"
 
@@ -35,19 +36,27 @@ import (
 )
 
 // abiVersion is the include/hipbls.h ABI this file is written against.
-const abiVersion = 11
+const abiVersion = 12
 
 // BLS12-381 group order r: a 32-byte big-endian scalar deserializes iff it is < r (herumi SecretKey.Deserialize).
 var order, _ = new(big.Int).SetString("73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001", 16)
 
-// HipBLS is stateless on the Go side; libhipbls holds one context per GPU (device, streams, workspaces, the resident
-// pubshare table and H(m) cache, a Verify submission queue).  Every method is safe for concurrent use.
+// HipBLS holds no state of its own: libhipbls holds one context per GPU (device, streams, workspaces, the resident
+// pubshare table and H(m) cache, a Verify submission queue), and the Go side keeps only the table's key -> index map
+// (pubShareIndex, process-wide like the library).  Every method is safe for concurrent use.
 type HipBLS struct{}
 
 var (
 	_ tbls.Implementation = HipBLS{} // all 11 methods
 	_ tbls.BatchVerifier  = HipBLS{} // the batch extension (patches/0001)
+	_ tbls.PubShareLoader = HipBLS{} // the resident pubshare table (patches/0001, loaded by app/app.go)
 )
+
+// pubShareIndex maps every pubshare loaded into the library's resident table (LoadPubShares) to its table index.
+var pubShareIndex struct {
+	sync.RWMutex
+	idx map[tbls.PublicKey]uint32
+}
 
 // New binds the charon process to the given GPUs (all of the node's, normally: charon is one process per node,
 // app/app.go:127).  Every batch is split into contiguous validator ranges across them and the results land in the
@@ -70,10 +79,95 @@ func New(devices ...int) (HipBLS, error) {
 		ids[i] = C.int32_t(d)
 	}
 	if rc := C.hipbls_init_devices(&ids[0], C.uint32_t(len(ids))); rc != C.HIPBLS_OK {
-		return HipBLS{}, devErr(rc)
+		return HipBLS{}, devErr(rc) // includes a device whose scratch region cannot hold the library's queues
+	}
+	for _, d := range devices {
+		if _, err := ScratchBudget(d); err != nil {
+			return HipBLS{}, err
+		}
 	}
 
 	return HipBLS{}, nil
+}
+
+// Scratch is a device's scratch budget (hipbls_scratch_budget, DESIGN.md 5.1.1): every hardware queue that runs the
+// library's kernels holds PerQueue bytes of the device's Limit-byte scratch region; the library holds four queues
+// (reserved at New) and never puts its kernels on a caller's priority or CU-masked stream, so Headroom is what the
+// rest of the process (another GPU library, a priority stream) may still hold on the device.
+type Scratch struct {
+	PerLane, PerQueue, Limit uint64
+	Queues                   uint32
+}
+
+// Headroom is the scratch the library's four queues leave on the device (0 when the runtime reports no limit).
+func (s Scratch) Headroom() uint64 {
+	if s.Limit < 4*s.PerQueue {
+		return 0
+	}
+
+	return s.Limit - 4*s.PerQueue
+}
+
+// ScratchBudget returns device d's scratch budget as the library computed it when New bound the device.
+func ScratchBudget(d int) (Scratch, error) {
+	var pl, pq, lim C.uint64_t
+	var q C.uint32_t
+	if rc := C.hipbls_scratch_budget(C.int(d), &pl, &pq, &lim, &q); rc != C.HIPBLS_OK {
+		return Scratch{}, devErr(rc)
+	}
+
+	return Scratch{PerLane: uint64(pl), PerQueue: uint64(pq), Limit: uint64(lim), Queues: uint32(q)}, nil
+}
+
+// LoadPubShares decodes and subgroup-checks the cluster's pubshares once into every GPU's resident table
+// (hipbls_pubshare_table_load; SURVEY.md §8f.2: the lock's keys, app/app.go:344-381).  Afterwards BatchVerify and
+// BatchVerifyRLC name keys by table index when every key of a call is in the table (no per-call decode or subgroup
+// test; herumi does both on every Verify, tbls/herumi.go:286-289), and the submission queue behind Verify turns
+// batches of table keys into random-linear-combination checks.  Results are unchanged.  A key that does not decode
+// stays out of the index, so calls naming it take the wire-format path and get herumi's error for it.  Loading again
+// replaces the table.
+func (HipBLS) LoadPubShares(pubshares []tbls.PublicKey) error {
+	pubShareIndex.Lock()
+	defer pubShareIndex.Unlock()
+	idx := make(map[tbls.PublicKey]uint32, len(pubshares))
+	if len(pubshares) > 0 {
+		flat := make([]byte, 0, 48*len(pubshares))
+		for _, k := range pubshares {
+			flat = append(flat, k[:]...)
+		}
+		status := make([]int32, len(pubshares))
+		if rc := C.hipbls_pubshare_table_load(u8(flat), C.uint64_t(len(pubshares)), i32(status)); rc != C.HIPBLS_OK {
+			pubShareIndex.idx = nil
+			return devErr(rc)
+		}
+		for i, k := range pubshares {
+			if _, dup := idx[k]; !dup && status[i] == C.HIPBLS_OK {
+				idx[k] = uint32(i)
+			}
+		}
+	}
+	pubShareIndex.idx = idx
+
+	return nil
+}
+
+// tableIndices returns every key's index in the resident pubshare table, or false when one is not in it.
+func tableIndices(pks []tbls.PublicKey) ([]uint32, bool) {
+	pubShareIndex.RLock()
+	defer pubShareIndex.RUnlock()
+	if len(pubShareIndex.idx) == 0 {
+		return nil, false
+	}
+	out := make([]uint32, len(pks))
+	for i, k := range pks {
+		j, ok := pubShareIndex.idx[k]
+		if !ok {
+			return nil, false
+		}
+		out[i] = j
+	}
+
+	return out, true
 }
 
 func devErr(rc C.int) error {

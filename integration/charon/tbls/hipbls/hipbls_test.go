@@ -112,3 +112,40 @@ func TestBatchEqualsSerial(t *testing.T) {
 		require.Equal(t, errs[i] == nil, rlc[i] == nil, i)
 	}
 }
+
+func TestPubShareTableSameResults(t *testing.T) {
+	h, ref := gpu(t), tbls.Herumi{}
+	const n = 48
+	pks := make([]tbls.PublicKey, n)
+	sigs := make([]tbls.Signature, n)
+	msgs := make([][]byte, n)
+	root := make([]byte, 32)
+	_, _ = rand.Read(root)
+	for i := 0; i < n; i++ {
+		secret, err := ref.GenerateSecretKey()
+		require.NoError(t, err)
+		pks[i], err = ref.SecretToPublicKey(secret)
+		require.NoError(t, err)
+		msgs[i] = root // one committee root: the RLC path over one message
+		sigs[i], err = ref.Sign(secret, msgs[i])
+		require.NoError(t, err)
+	}
+	sigs[5], sigs[6] = sigs[6], sigs[5] // two wrong signatures
+	before, err := h.BatchVerify(pks, msgs, sigs)
+	require.NoError(t, err)
+	require.NoError(t, h.LoadPubShares(pks))
+	_, ok := tableIndices(pks)
+	require.True(t, ok)
+	after, err := h.BatchVerify(pks, msgs, sigs)
+	require.NoError(t, err)
+	rlc, err := h.BatchVerifyRLC(pks, sigs, make([]uint32, n), [][]byte{root})
+	require.NoError(t, err)
+	for i := range pks {
+		require.Equal(t, before[i] == nil, after[i] == nil, i)
+		require.Equal(t, before[i] == nil, rlc[i] == nil, i)
+		require.Equal(t, ref.Verify(pks[i], msgs[i], sigs[i]) == nil, after[i] == nil, i)
+	}
+	require.NoError(t, h.LoadPubShares(nil)) // empty table: the wire-format path again
+	_, ok = tableIndices(pks)
+	require.False(t, ok)
+}

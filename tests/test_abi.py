@@ -37,7 +37,7 @@ def test_ctypes_mirror_declares_header_set():
     from charon_amd import tbls
     assert sorted(tbls.exported_symbols()) == header_functions()
     lib = tbls.load_library()
-    assert lib.hipbls_abi_version() == 11
+    assert lib.hipbls_abi_version() == 12
 
 
 def test_no_cpu_fallback_without_library(tmp_path):

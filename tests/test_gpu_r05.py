@@ -1,0 +1,154 @@
+"""GPU tests added in round 5 (VERDICT r04 "Next round" 1).
+
+The round-4 abort (HSA_STATUS_ERROR_OUT_OF_RESOURCES when a high-priority stream ran the library's kernels beside a
+C5 step) came from the scratch arithmetic measured in profiles/r05/r05_scratch_probe.txt and
+r05_scratch_layout.txt: every hardware queue that dispatches a kernel holds a block of (private segment) x 64 x 32 x
+256 CUs from one 32 GiB region per device, placed first fit; queues grown in stages leave holes, and a priority stream
+is a queue of its own.  The library now reserves its four queues' blocks at init, refuses a device where they do not
+fit, and runs a *_device call on a priority stream on its own library stream instead (StreamJoin).  Here:
+
+* the budget the library computed at init equals the code objects' arithmetic (hipbls_scratch_budget);
+* a C5-sized RLC call on a HIGH-priority caller stream beside a FastAggregateVerify on a LOW-priority one (two
+  hardware queues the library does not hold): the statuses equal the construction, both calls were joined to the
+  library stream, and the device's free memory does not drop by a scratch block (6.1 GiB);
+* the submission queue's worker polls a batch in flight from its expected end on, not every 20 us from its start.
+"""
+import ctypes
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "charon_amd", "libhipbls.so")
+V = 262144  # C4/C5 node batch: 262,144 validators x 4 partials
+
+
+@pytest.fixture(scope="module")
+def impl():
+    from charon_amd.tbls import HipBLS
+    return HipBLS()
+
+
+def _budget(impl, dev=0):
+    pl, pq, lim = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    q = ctypes.c_uint32()
+    assert impl.lib.hipbls_scratch_budget(dev, ctypes.byref(pl), ctypes.byref(pq), ctypes.byref(lim),
+                                          ctypes.byref(q)) == 0
+    return pl.value, pq.value, lim.value, q.value
+
+
+def _joins(impl):
+    n = ctypes.c_uint64()
+    assert impl.lib.hipbls_stream_joins(ctypes.byref(n)) == 0
+    return n.value
+
+
+def test_scratch_budget_matches_code_objects(impl):
+    from charon_amd import codeobj
+    impl.batch_verify_status([b"\xc0" + bytes(47)], [b"x"], [b"\xc0" + bytes(95)])  # binds the device
+    per_lane, per_queue, limit, queues = _budget(impl)
+    deepest = max(r[1] for r in codeobj.resource_table(LIB) if r[0] != "k_scratch_reserve")
+    assert per_lane == deepest
+    assert per_queue == -(-per_lane * codeobj.WAVE_SLOTS // codeobj.BLOCK_ALIGN) * codeobj.BLOCK_ALIGN
+    assert limit == codeobj.SCRATCH_REGION  # 32 GiB on MI355X
+    assert queues == int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    assert impl.lib.hipbls_device_streams(0) == 4
+    # the four library queues plus one more of the same depth fit the region (the build's budget)
+    assert 5 * per_queue <= limit
+    print("scratch: %d B/lane, %.2f GiB per queue, limit %.1f GiB" % (per_lane, per_queue / 2**30, limit / 2**30))
+
+
+def test_priority_streams_beside_c5_run_on_library_queues(impl):
+    import torch
+
+    import bench
+    from oracle import bls12381 as bls
+    keys4 = bench.share_keys(impl, 4096, "c4")
+    pks, sigs, midx, roots, bad = bench.make_c4(impl, keys4, "c4i", 0, V, V, 0)
+    sync_sks = [bench._scalar("c5sync", k).to_bytes(32, "big") for k in range(512)]
+    sync_pks, _ = impl.secret_to_public_key_batch(sync_sks)
+    sync_root = bench._hb("c5sync", "root")
+    ssigs, _ = impl.sign_batch(sync_sks, [sync_root] * 512)
+    sync_agg = impl.aggregate(ssigs)
+    dev = torch.device("cuda", 0)
+
+    def u8(blobs):
+        return torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8).to(dev)
+
+    n = len(pks)
+    d_pk, d_sig, d_msg = u8(pks), u8(sigs), u8(roots)
+    d_midx = torch.tensor(midx, dtype=torch.int32).to(dev)
+    d_off = torch.arange(0, 32 * (len(roots) + 1), 32, dtype=torch.int64).to(dev)
+    d_st = torch.full((n,), -7, dtype=torch.int32, device=dev)
+    d_spk2 = torch.cat([u8(sync_pks), u8(sync_pks)])
+    d_ssig, d_smsg = u8([sync_agg, sync_agg]), u8([sync_root, sync_root[::-1]])
+    d_skoff = torch.tensor([0, 512, 1024], dtype=torch.int64).to(dev)
+    d_smoff = torch.tensor([0, 32, 64], dtype=torch.int64).to(dev)
+    d_sst = torch.full((2,), -7, dtype=torch.int32, device=dev)
+    lib = impl.lib
+
+    def run(s_rlc, s_fav):
+        d_st.fill_(-7)
+        d_sst.fill_(-7)
+        torch.cuda.synchronize(dev)
+        assert lib.hipbls_verify_aggregate_batch_device(d_spk2.data_ptr(), 1024, d_skoff.data_ptr(), 2,
+                                                        d_ssig.data_ptr(), d_smsg.data_ptr(), d_smoff.data_ptr(),
+                                                        d_sst.data_ptr(), ctypes.c_void_p(s_fav.cuda_stream)) == 0
+        assert lib.hipbls_batch_verify_rlc_device(d_pk.data_ptr(), d_sig.data_ptr(), d_midx.data_ptr(), n,
+                                                  d_msg.data_ptr(), d_off.data_ptr(), len(roots), os.urandom(32),
+                                                  d_st.data_ptr(), ctypes.c_void_p(s_rlc.cuda_stream)) == 0
+        # the caller's streams are ordered after the calls: reading on them sees the results
+        with torch.cuda.stream(s_rlc):
+            st = d_st.cpu()
+        with torch.cuda.stream(s_fav):
+            sst = d_sst.cpu()
+        torch.cuda.synchronize(dev)
+        assert {i for i, s in enumerate(st.tolist()) if s != 0} == bad
+        assert sst.tolist() == [0, 3]
+
+    # warm-up on normal-priority streams: workspaces allocated, no join
+    j0 = _joins(impl)
+    run(torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+    assert _joins(impl) == j0
+    torch.cuda.synchronize(dev)
+    free0, _ = torch.cuda.mem_get_info(dev)
+    hi = torch.cuda.Stream(dev, priority=-1)
+    # torch clamps priorities to [-1, 0]: the least priority (+1 on this runtime, its own hardware queue as well,
+    # profiles/r05/r05_scratch_probe.txt) comes from HIP directly
+    hip = ctypes.CDLL("libamdhip64.so")
+    least, greatest = ctypes.c_int(), ctypes.c_int()
+    assert hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest)) == 0
+    raw = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithPriority(ctypes.byref(raw), 1, least) == 0  # hipStreamNonBlocking
+    lo = torch.cuda.ExternalStream(raw.value, device=dev)
+    assert least.value != 0 and hi.priority != 0
+    run(hi, lo)
+    free1, _ = torch.cuda.mem_get_info(dev)
+    joined = _joins(impl) - j0
+    assert joined == 2
+    _, per_queue, _, _ = _budget(impl)
+    drop = free0 - free1
+    print("priority streams: %d calls joined, free memory drop %.3f GiB (a queue's block: %.2f GiB)"
+          % (joined, drop / 2**30, per_queue / 2**30))
+    assert drop < per_queue // 4
+    bls.verify_aggregate(sync_pks, sync_agg, sync_root)
+
+
+def test_queue_worker_polls_from_expected_end(impl):
+    import bench
+    pks, roots, sigs, bad = bench.make_c2(impl, bench.share_keys(impl, 64, "c2q"), 0, 64)
+    st = impl.batch_verify_status(pks, roots, sigs)
+    assert {i for i, s in enumerate(st) if s} == bad
+    w0, b0 = ctypes.c_uint64(), ctypes.c_uint64()
+    impl.verify_queued(pks[0], roots[0], sigs[0])  # starts the worker; learns the n = 1 batch time
+    assert impl.lib.hipbls_queue_worker_stats(ctypes.byref(w0), ctypes.byref(b0)) == 0
+    for j in range(1, 33):
+        assert impl.verify_queued(pks[j], roots[j], sigs[j]) == st[j]
+    w1, b1 = ctypes.c_uint64(), ctypes.c_uint64()
+    assert impl.lib.hipbls_queue_worker_stats(ctypes.byref(w1), ctypes.byref(b1)) == 0
+    per_batch = (w1.value - w0.value) / max(1, b1.value - b0.value)
+    print("queue worker: %.1f completion polls per n = 1 batch" % per_batch)
+    # a ~12 ms batch polled every 20 us from its launch would take ~600 polls
+    assert per_batch < 250

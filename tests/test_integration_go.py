@@ -41,7 +41,7 @@ def test_patch_series_targets():
     touched = [f for p in PATCHES for f in _patched_files(p)]
     for f in ("tbls/tbls.go", "core/parsigex/parsigex.go", "core/validatorapi/validatorapi.go", "core/sigagg/sigagg.go",
               "core/eth2signeddata.go", "app/app.go", "app/featureset/featureset.go", "tbls/hipbls/hipbls.go",
-              "tbls/hipbls/batch.go", "tbls/hipbls_suite_test.go"):
+              "tbls/hipbls/batch.go", "tbls/hipbls_suite_test.go", "eth2util/signing/signing.go", "cluster/lock.go"):
         assert f in touched, f
 
 
@@ -59,8 +59,36 @@ def test_patch_series_applies_to_reference(tmp_path):
         assert r.returncode == 0, (p, r.stdout, r.stderr)
     s = open(tmp_path / "tbls" / "tbls.go").read()
     assert "type BatchVerifier interface" in s and "func Impl() Implementation" in s
+    for fn in ("BatchVerify", "BatchVerifyRLC", "BatchThresholdAggregate", "BatchThresholdAggregateVerify",
+               "BatchVerifyAggregate", "LoadPubShares"):
+        assert re.search(r"^func %s\(" % fn, s, flags=re.M), fn
+    assert "type PubShareLoader interface" in s
     assert "verifySetFunc" in open(tmp_path / "core" / "parsigex" / "parsigex.go").read()
-    assert "tbls.BatchThresholdAggregate(groups)" in open(tmp_path / "core" / "sigagg" / "sigagg.go").read()
+    sig = open(tmp_path / "core" / "sigagg" / "sigagg.go").read()
+    assert "tbls.BatchThresholdAggregate(groups)" in sig
+    # sigagg in one call: the fused aggregator computes the signing roots first
+    assert "tbls.BatchThresholdAggregateVerify(groups, dvPks, msgs)" in sig and "func NewFused(" in sig
+    # signing roots shared by many items go through the RLC check
+    sg = open(tmp_path / "eth2util" / "signing" / "signing.go").read()
+    assert "func VerifyBatch(" in sg and "tbls.BatchVerifyRLC(pks, sigs, msgIdx, msgs)" in sg
+    assert "signing.VerifyBatch(ctx, eth2Cl, items)" in open(tmp_path / "core" / "eth2signeddata.go").read()
+    # the five per-item validatorapi loops and SubmitAttestations: no per-item
+    # verifyPartialSig left in them, one core.FirstFailure batch each
+    va = open(tmp_path / "core" / "validatorapi" / "validatorapi.go").read()
+    for fn in ("SubmitAttestations", "AggregateBeaconCommitteeSelections", "SubmitAggregateAttestations",
+               "SubmitSyncCommitteeMessages", "SubmitSyncCommitteeContributions", "AggregateSyncCommitteeSelections"):
+        body = va[va.index("func (c Component) %s(" % fn):]
+        body = body[:body.index("\n}\n")]
+        assert "c.verifyPartialSig(" not in body, fn
+        assert "core.VerifyEth2SignedData(" not in body and "signing.VerifyAggregateAndProofSelection(" not in body, fn
+        assert body.count("core.FirstFailure(ctx, c.eth2Cl, steps)") == 1, fn
+    # app: the resident pubshare table loaded from the lock's shares, fused sigagg
+    app = open(tmp_path / "app" / "app.go").read()
+    assert "tbls.LoadPubShares(pubShareTable)" in app and "sigagg.NewFused(" in app
+    # cluster lock: registrations in one batch, bulk lock verification
+    lk = open(tmp_path / "cluster" / "lock.go").read()
+    assert "tbls.BatchVerifyAggregate(aggKeys, aggSigs, aggMsgs)" in lk and "func VerifyLocksSignatures(" in lk
+    assert "tbls.BatchVerify(regs.pks, regs.msgs, regs.sigs)" in lk
 
 
 def test_new_files_match_integration_tree():
@@ -107,7 +135,11 @@ def test_every_implementation_method_bound():
     src = open(os.path.join(INT, "charon", "tbls", "hipbls", "hipbls.go")).read()
     for m in methods:
         assert re.search(r"^func \((?:\w+ )?HipBLS\) " + m + r"\(", src, flags=re.M), m
+    assert re.search(r"^func \(HipBLS\) LoadPubShares\(", src, flags=re.M)
+    assert "C.hipbls_pubshare_table_load(" in src and "C.hipbls_scratch_budget(" in src
     batch = open(os.path.join(INT, "charon", "tbls", "hipbls", "batch.go")).read()
+    # table-indexed twins of the wire-format batch calls
+    assert "C.hipbls_verify_batch_keys(" in batch and "C.hipbls_batch_verify_rlc_keys(" in batch
     for m in ("BatchVerify", "BatchVerifyRLC", "BatchThresholdAggregate", "BatchVerifyAggregate",
               "BatchThresholdAggregateVerify"):
         assert re.search(r"^func \((?:\w+ )?HipBLS\) " + m + r"\(", batch, flags=re.M), m

@@ -1,9 +1,11 @@
 """The built library's kernel resources, read from its gfx950 code object on the CPU (charon_amd/codeobj.py).
 
-The per-lane private segment (scratch) of the deepest kernel sizes every hardware queue's scratch allocation; round 3
-saw HSA_STATUS_ERROR_OUT_OF_RESOURCES aborts once kernels reached ~17.9 KB/lane.  The build refuses
-a library above PRIVATE_SEGMENT_BUDGET; this test holds the shipped .so to the same bound and checks the metadata the
-roofline and occupancy arguments use (VGPRs, the LDS-resident Miller slot).
+The per-lane private segment (scratch) of the deepest kernel sizes every hardware queue's scratch block (x 64 lanes x
+32 wave slots x 256 CUs); all queues of a process share one 32 GiB region per device.  The build
+refuses a library above PRIVATE_SEGMENT_BUDGET, derived so the library's four queues plus one more of the same depth
+fit the region; this test holds the shipped .so to the same bound, checks that the runtime's kernel table (the
+scratch budget hipbls_scratch_budget computes at init) names every kernel of the code objects, and checks the
+metadata the roofline and occupancy arguments use (VGPRs, the LDS-resident Miller slot).
 """
 import os
 
@@ -15,6 +17,39 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "charon_amd", "libhipbls.so")
 
 pytestmark = pytest.mark.skipif(not os.path.exists(LIB), reason="libhipbls.so not built (run __graft_entry__.build())")
+
+
+def test_budget_is_the_scratch_arithmetic():
+    """PRIVATE_SEGMENT_BUDGET is the largest per-lane segment whose 2 MiB-aligned block (x 64 x 32 x 256) fits five
+    times (the library's four queues + one) in the 32 GiB region: measured per-queue blocks 1,040 B -> 520 MiB and
+    12,480 B -> 6,240 MiB (profiles/r05/r05_scratch_probe.txt, r05_scratch_layout.txt)."""
+    b = codeobj.PRIVATE_SEGMENT_BUDGET
+    assert b == 13104
+    blk = lambda p: -(-p * codeobj.WAVE_SLOTS // codeobj.BLOCK_ALIGN) * codeobj.BLOCK_ALIGN
+    assert blk(1040) == 520 << 20 and blk(12480) == 6240 << 20
+    assert 5 * blk(b) <= codeobj.SCRATCH_REGION < 5 * blk(b + 16) + 5 * codeobj.BLOCK_ALIGN
+    # round 3's 17,880 B/lane: four queues alone exceed the region (the round-3 aborts)
+    assert 4 * blk(17880) > codeobj.SCRATCH_REGION
+
+
+def test_runtime_kernel_table_names_every_kernel():
+    import ctypes
+    lib = ctypes.CDLL(LIB)
+    lib.hipbls_kernel_names.restype = ctypes.c_char_p
+    table = lib.hipbls_kernel_names().decode().split()
+    assert len(table) == len(set(table))
+    co = {r[0] for r in codeobj.resource_table(LIB)}
+    assert set(table) == co - {"k_scratch_reserve"}
+
+
+def test_reserve_kernels_cover_the_deepest_kernel():
+    """The init-time reserve kernels (one dispatch per library stream) reach at least the deepest kernel's segment and
+    stop at the budget."""
+    rows = codeobj.resource_table(LIB)
+    res = sorted(r[1] for r in rows if r[0] == "k_scratch_reserve")
+    deepest = max(r[1] for r in rows if r[0] != "k_scratch_reserve")
+    assert res and res[-1] == codeobj.PRIVATE_SEGMENT_BUDGET
+    assert any(deepest <= x < deepest + 256 for x in res)
 
 
 def test_every_kernel_within_scratch_budget():
