@@ -469,7 +469,20 @@ def main():
                    "min_ms": round(1000 * lat[0], 3), "serial_verifies_per_s": round(k / tot, 1),
                    "seconds_per_1000_serial": round(1000 * tot / k, 2),
                    "path": "hipbls_verify (submission queue, n = 1 batch: eight-lane prep + pairing check, "
-                           "verify_lat.hip)"}
+                           "verify_lat.hip; each stage raced by 8 replicas, one per XCD)"}
+        # the same calls without the replica race (hipbls_set_latency_replicas(1)), for comparison
+        k1 = min(200, k)
+        prev = lib.hipbls_set_latency_replicas(1)
+        lat1 = []
+        for j in range(k1):
+            a = time.perf_counter()
+            got = impl.verify_queued(pks[j], roots[j], sigs[j])
+            lat1.append(time.perf_counter() - a)
+            assert got == st[j], "queued Verify differs from the batch call"
+        lib.hipbls_set_latency_replicas(prev)
+        lat1.sort()
+        latency["no_replicas"] = {"calls": k1, "p50_ms": round(1000 * lat1[k1 // 2], 3),
+                                  "p90_ms": round(1000 * lat1[(9 * k1) // 10], 3)}
 
     # ---- C2 with the resident pubshare table (extra field): same items, keys by index
     keys_rate = None
@@ -634,6 +647,30 @@ def main():
             th3 = timed_loop(hc3, args.tagg_steps, dev, lambda: None, 1)
             assert set(c_ast) == {0} and set(c_vst) == {0} and c_out.raw == b"".join(want_aggs), "host C3"
             host_path["c3_threshold_aggregate_verify_batch_per_s"] = round(G * args.tagg_steps / th3, 1)
+            # two threads each making the same calls (two goroutines with consecutive sigagg duties): the host call
+            # holds the context lock only while it enqueues, so the second call's copies and phase A run beside the
+            # first call's checks
+            import threading
+            outs2 = [(ctypes.create_string_buffer(96 * G), (ctypes.c_int32 * G)(), (ctypes.c_int32 * G)())
+                     for _ in range(2)]
+
+            k3 = max(4, args.tagg_steps)
+
+            def hc3_thread(o):
+                for _ in range(k3):
+                    assert lib.hipbls_threshold_aggregate_verify_batch(c_psig, c_pid, c_poff, G, c_dpk, gblob, goffs,
+                                                                       o[0], o[1], o[2]) == 0
+
+            t0 = time.perf_counter()
+            ths = [threading.Thread(target=hc3_thread, args=(o,)) for o in outs2]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            t2 = time.perf_counter() - t0
+            for o in outs2:
+                assert set(o[1]) == {0} and set(o[2]) == {0} and o[0].raw == b"".join(want_aggs), "host C3 x2"
+            host_path["c3_two_threads_per_s"] = round(2 * G * k3 / t2, 1)
 
     # ---- C4: RLC BatchVerify of the 1M-partial node batch, validator-index slices over the ranks (strong scaling:
     # the node batch is fixed); node bitmap all-gathered inside the timed step

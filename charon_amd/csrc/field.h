@@ -255,6 +255,18 @@ __device__ __attribute__((used, noinline)) static void bls_fp_asm_routines() {
                ".p2align 6\n.type bls_fp2_sqr_rt,@function\nbls_fp2_sqr_rt:\n\t" BLS_FP2_SQR_ASM_BODY
                "\n\ts_setpc_b64 s[30:31]\n");
 }
+#ifndef BLS_LAZY_FP6
+#define BLS_LAZY_FP6 0
+#endif
+#if BLS_LAZY_FP6 && !BLS_FP2_PAIR
+// The lazy-reduction experiment's routines (tools/gen_fp_asm.py gen_fp2_mul2 / gen_fp2_mul3).
+__device__ __attribute__((used, noinline)) static void bls_fp2_lazy_routines() {
+  asm volatile("s_endpgm\n.p2align 6\n.type bls_fp2_mul2_rt,@function\nbls_fp2_mul2_rt:\n\t" BLS_FP2_MUL2_ASM_BODY
+               "\n\ts_setpc_b64 s[30:31]\n"
+               ".p2align 6\n.type bls_fp2_mul3_rt,@function\nbls_fp2_mul3_rt:\n\t" BLS_FP2_MUL3_ASM_BODY
+               "\n\ts_setpc_b64 s[30:31]\n");
+}
+#endif
 #if BLS_FP2_PAIR
 // The split-Fp2 build (verify_lat.hip): an Fp2 value is held in full on lanes l and l ^ 4, each computes one output
 // coefficient of a product or square (tools/gen_fp_asm.py gen_fp2_mul_half / gen_fp2_sqr_half), then they swap.

@@ -48,8 +48,10 @@
 // The eight-lane latency path (verify_lat.hip, its own translation unit: BLS_FP2_PAIR build in namespace bls_fp2p).
 namespace bls_fp2p {
 __global__ void k_verify_prep8(const uint8_t* pks, const uint8_t* msgs, const uint64_t* offs, const uint8_t* sigs,
-                               uint64_t n, uint32_t* ws, int32_t* status);
-__global__ void k_verify_pair_lq8(const uint32_t* ws, uint64_t n, int32_t* status);
+                               uint64_t n, uint32_t* ws, int32_t* status, uint32_t replicas, uint32_t* race,
+                               uint32_t epoch);
+__global__ void k_verify_pair_lq8(const uint32_t* ws, uint64_t n, int32_t* status, uint32_t replicas, uint32_t* race,
+                                  uint32_t epoch);
 __global__ void k_rlcb_sfactor8(const uint32_t* W, uint32_t* Fs);
 __global__ void k_rlcb_final8(const uint32_t* Ftot, const uint32_t* Fs, int32_t* flag);
 __global__ void k_g1m_miller8(uint64_t nl_max, const uint32_t* meta, const uint32_t* lmsg, const uint32_t* Wv,
@@ -80,7 +82,8 @@ struct DevBuf {
     if (p) (void)hipFree(p);  // hipFree waits for the device: no in-flight kernel still uses the old buffer
     p = nullptr;
     cap = 0;
-    const size_t want = n < 4096 ? 4096 : n + n / 4;
+    // 256-byte multiples: a buffer's tail (the octet path's race words, launch_verify) stays naturally aligned
+    const size_t want = ((n < 4096 ? 4096 : n + n / 4) + 255) & ~(size_t)255;
     hipError_t e = hipMalloc(&p, want);
     if (e == hipSuccess) cap = want;
     return e;
@@ -166,6 +169,19 @@ struct Context {
   // sigagg in one call (launch_tagg_verify): two workspace sets used alternately, each with the completion event of
   // the call that last used it
   DevBuf tv_pts[2], tv_pst[2], tv_ws[2], tv_aux[2];
+  // The host-buffer sigagg call (tagg_verify_host): two slots of input/output buffers, used alternately, each on its
+  // own library sub-stream; a call holds its slot for its whole duration but the context lock only while it enqueues,
+  // so the next caller's copies and phase A run beside this call's checks (the _device path's two-stream overlap,
+  // reached from host buffers: two goroutines with consecutive duties).
+  struct TvHostSlot {
+    std::mutex mu;
+    DevBuf sig, ids, off, pk, msg, moff, out, st;
+    uint8_t* h_out = nullptr;  // pinned: the outputs come back by a real async D2H
+    int32_t* h_st = nullptr;
+    uint64_t h_groups = 0;
+    hipEvent_t done = nullptr;
+  } tvh[2];
+  std::atomic<uint64_t> tvh_seq{0};
   hipEvent_t tv_done[2] = {}, tv_phase = nullptr;  // tv_phase: the last call's phase A (and S, statuses) done
   uint64_t tv_seq = 0;
   uint64_t t_size = 0;
@@ -669,6 +685,40 @@ int run_ranges(const std::vector<uint64_t>& b, F fn) {
   return HIPBLS_OK;
 }
 
+// run_ranges without the context lock: fn takes what it needs itself (tagg_verify_host).
+template <class F>
+int run_ranges_unlocked(const std::vector<uint64_t>& b, F fn) {
+  const size_t k = b.size() - 1;
+  if (k == 1) {
+    const int n = nctx();
+    Context& c = n == 1 ? ctx(0) : ctx((int)(g_rr.fetch_add(1) % (uint64_t)n));
+    const int brc = bind(c);
+    if (brc) return brc;
+    return fn(c, b[0], b[1]);
+  }
+  std::vector<int> rc(k, HIPBLS_OK);
+  std::vector<std::string> err(k);
+  auto one = [&](size_t j) {
+    if (b[j] == b[j + 1]) return;
+    Context& c = ctx((int)j);
+    int r = bind(c);
+    if (!r) r = fn(c, b[j], b[j + 1]);
+    rc[j] = r;
+    if (r) err[j] = g_last_error;
+  };
+  std::vector<std::thread> th;
+  th.reserve(k - 1);
+  for (size_t j = 1; j < k; ++j) th.emplace_back(one, j);
+  one(0);
+  for (auto& t : th) t.join();
+  for (size_t j = 0; j < k; ++j)
+    if (rc[j]) {
+      g_last_error = err[j];
+      return rc[j];
+    }
+  return HIPBLS_OK;
+}
+
 // Runs fn(context) on every context (table loads, cache configuration), in parallel.
 template <class F>
 int run_all(F fn) {
@@ -773,6 +823,16 @@ constexpr uint64_t kLq4MaxVerify = BLS_LQ4_MAX_VERIFY;  // auto: Verify-shaped b
 #endif
 constexpr uint64_t kLq8MaxVerify = BLS_LQ8_MAX_VERIFY;  // auto: Verify batches up to this many take octets
 
+// Replicas of a one-workgroup octet Verify (verify_lat.hip bls_race; HIPBLS_LAT_REPLICAS, 1 = off) and the epoch that
+// names each raced launch in its race words.
+uint32_t initial_lat_replicas() {
+  const char* r = getenv("HIPBLS_LAT_REPLICAS");
+  const int v = r ? atoi(r) : 8;
+  return v < 1 ? 1u : (v > 32 ? 32u : (uint32_t)v);
+}
+std::atomic<uint32_t> g_lat_replicas{initial_lat_replicas()};
+std::atomic<uint32_t> g_race_epoch{0};
+
 bool use_pairs(uint64_t units, uint64_t auto_max) {
   const int mode = g_pair_mode.load();
   if (mode == HIPBLS_PAIR_SINGLE) return false;
@@ -801,16 +861,36 @@ int launch_verify(Context& c, const uint8_t* d_pks, const uint8_t* d_msgs, const
       hipLaunchKernelGGL(k_verify_fused, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs,
                          d_sigs, n, d_status);
     });
-  HIP_TRY(ws.ensure(n * 122 * 4));  // + two decode codes per item for the octet path
+  // + two decode codes per item for the octet path, and the octet path's race words in the buffer's last 64 bytes (a
+  // fixed place per allocation, 64-byte aligned since the capacity is a multiple of 256, beyond every batch's data;
+  // zeroed when the buffer is allocated, then only ever written with a launch's epoch, so a stale word never equals a
+  // new epoch)
+  void* const before = ws.p;
+  HIP_TRY(ws.ensure(n * 122 * 4 + 128));
+  if (ws.p != before) HIP_TRY(hipMemsetAsync((uint8_t*)ws.p + ws.cap - 64, 0, 64, s));
   if (use_octets(n)) {
     const unsigned g8 = (unsigned)grid_for(8 * n);
+    // A batch of one workgroup (<= 8 items: the drop-in n = 1 calls) races `lat_replicas` copies of it, one per XCD
+    // (verify_lat.hip bls_race): the first copy to finish each stage wins.  Race words after the workspace.
+    uint32_t* race = (uint32_t*)((uint8_t*)ws.p + ws.cap - 64);
+    // (the race words must be naturally aligned: a misaligned word faults the device -- round 5, before capacities
+    // were rounded to 256 bytes)
+    const uint32_t reps = g8 == 1 && ((uintptr_t)race & 63) == 0 ? g_lat_replicas.load() : 1u;
+    uint32_t epoch = reps > 1 ? g_race_epoch.fetch_add(1) + 1u : 0u;
+    if (reps > 1 && epoch == 0) epoch = g_race_epoch.fetch_add(1) + 1u;  // 0 is a fresh word's value
     int rc = timed(c, "verify_prep8", s, [&] {  // three roles: key, signature, hash (verify_lat.hip)
-      hipLaunchKernelGGL(bls_fp2p::k_verify_prep8, dim3(3 * g8), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs, d_sigs, n,
-                         (uint32_t*)ws.p, d_status);
+      hipLaunchKernelGGL(bls_fp2p::k_verify_prep8, dim3(3 * g8 * reps), dim3(kBlock), 0, s, d_pks, d_msgs, d_offs,
+                         d_sigs, n, (uint32_t*)ws.p, d_status, reps, race, epoch);
     });
     if (rc) return rc;
     return timed(c, "verify_pair_lq8", s, [&] {
-      hipLaunchKernelGGL(bls_fp2p::k_verify_pair_lq8, dim3(g8), dim3(kBlock), 0, s, (const uint32_t*)ws.p, n, d_status);
+#if defined(BLS_LQ8_XCD_PROBE) && BLS_LQ8_XCD_PROBE
+      hipLaunchKernelGGL(bls_fp2p::k_verify_pair_lq8, dim3(8 * g8), dim3(kBlock), 0, s, (const uint32_t*)ws.p, n,
+                         d_status, 1u, race, 0u);  // experiment build: every workgroup once per XCD (verify_lat.hip)
+#else
+      hipLaunchKernelGGL(bls_fp2p::k_verify_pair_lq8, dim3(g8 * reps), dim3(kBlock), 0, s, (const uint32_t*)ws.p, n,
+                         d_status, reps, race, epoch);
+#endif
     });
   }
   int rc = timed(c, "verify_prep", s, [&] {
@@ -971,9 +1051,13 @@ int launch_rlc(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const ui
       });
     if (rc) return rc;
     // The list length is only known on the device: launch for the worst case, idle lanes exit.  The list is short
-    // (failed windows only) and latency-bound, so lane pairs unless the caller forced single lanes.
-    rc = launch_fallback(c, ss, list + i0, cnt + k, i1 - i0, nsub, d_pks, d_sigs, d_midx, d_H, hstride, d_hslot,
-                         d_status, d_kidx, T, tab);
+    // (failed windows only) and latency-bound, so lane pairs unless the caller forced single lanes.  The last
+    // sub-batch's list is the call's tail -- the other sub-batches' stages are done by then -- so with
+    // HIPBLS_RLC_TAIL_PAIRS=1 it takes pairs up to the whole chip's lanes (the earlier ones share the chip with the
+    // next sub-batch's windows); off by default until measured on its own.
+    static const bool tail_pairs = getenv("HIPBLS_RLC_TAIL_PAIRS") && getenv("HIPBLS_RLC_TAIL_PAIRS")[0] == '1';
+    rc = launch_fallback(c, ss, list + i0, cnt + k, i1 - i0, tail_pairs && k + 1 == nsub ? 1 : nsub, d_pks, d_sigs,
+                         d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c.ev_join[k], ss));
     HIP_TRY(hipStreamWaitEvent(s, c.ev_join[k], 0));
@@ -2016,41 +2100,64 @@ int tagg_host(Context& c, const uint8_t* sigs, const int64_t* share_idx, const u
   return HIPBLS_OK;
 }
 
+// Called WITHOUT the context lock (run_ranges_unlocked): it takes a host slot for the whole call and the context lock
+// only to enqueue (copies in, the sigagg kernels, copies out into the slot's pinned buffers), then waits for the slot's
+// completion event with no lock held.
 int tagg_verify_host(Context& c, const uint8_t* sigs, const int64_t* share_idx, const uint64_t* goffs,
                      uint64_t n_groups, const uint8_t* dv_pks, const uint8_t* msgs, const uint64_t* moffs,
                      uint8_t* out_sigs, int32_t* agg_status, int32_t* verify_status) {
   const uint64_t n_parts = goffs[n_groups];
   const uint64_t msg_total = moffs[n_groups];
-  HIP_TRY(c.b_sig.ensure((n_parts ? n_parts : 1) * 96));
-  HIP_TRY(c.b_ids.ensure((n_parts ? n_parts : 1) * 8));
-  HIP_TRY(c.b_off.ensure((n_groups + 1) * 8));
-  HIP_TRY(c.b_pk.ensure(n_groups * 48));
-  HIP_TRY(c.b_msg.ensure(msg_total ? msg_total : 1));
-  HIP_TRY(c.b_kidx.ensure((n_groups + 1) * 8));  // message offsets
-  HIP_TRY(c.b_out.ensure(n_groups * 96));
-  HIP_TRY(c.b_st.ensure(n_groups * 8));          // aggregate statuses, then verify statuses
-  int wrc = ws_begin(c, c.stream);
-  if (wrc) return wrc;
-  if (n_parts) {
-    HIP_TRY(hipMemcpyAsync(c.b_sig.p, sigs, n_parts * 96, hipMemcpyHostToDevice, c.stream));
-    HIP_TRY(hipMemcpyAsync(c.b_ids.p, share_idx, n_parts * 8, hipMemcpyHostToDevice, c.stream));
+  const int p = (int)(c.tvh_seq.fetch_add(1) & 1);
+  Context::TvHostSlot& h = c.tvh[p];
+  std::lock_guard<std::mutex> slot_lock(h.mu);
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    const hipStream_t s = c.sub[p];
+    if (!h.done) HIP_TRY(hipEventCreateWithFlags(&h.done, hipEventDisableTiming));
+    HIP_TRY(h.sig.ensure((n_parts ? n_parts : 1) * 96));
+    HIP_TRY(h.ids.ensure((n_parts ? n_parts : 1) * 8));
+    HIP_TRY(h.off.ensure((n_groups + 1) * 8));
+    HIP_TRY(h.pk.ensure(n_groups * 48));
+    HIP_TRY(h.msg.ensure(msg_total ? msg_total : 1));
+    HIP_TRY(h.moff.ensure((n_groups + 1) * 8));
+    HIP_TRY(h.out.ensure(n_groups * 96));
+    HIP_TRY(h.st.ensure(n_groups * 8));  // aggregate statuses, then verify statuses
+    if (h.h_groups < n_groups) {
+      if (h.h_out) HIP_TRY(hipHostFree(h.h_out));
+      if (h.h_st) HIP_TRY(hipHostFree(h.h_st));
+      h.h_out = nullptr;
+      h.h_st = nullptr;
+      h.h_groups = 0;
+      HIP_TRY(hipHostMalloc((void**)&h.h_out, n_groups * 96, hipHostMallocDefault));
+      HIP_TRY(hipHostMalloc((void**)&h.h_st, n_groups * 8, hipHostMallocDefault));
+      h.h_groups = n_groups;
+    }
+    if (n_parts) {
+      HIP_TRY(hipMemcpyAsync(h.sig.p, sigs, n_parts * 96, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(h.ids.p, share_idx, n_parts * 8, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(hipMemcpyAsync(h.off.p, goffs, (n_groups + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(h.pk.p, dv_pks, n_groups * 48, hipMemcpyHostToDevice, s));
+    if (msg_total) HIP_TRY(hipMemcpyAsync(h.msg.p, msgs, msg_total, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(h.moff.p, moffs, (n_groups + 1) * 8, hipMemcpyHostToDevice, s));
+    int32_t* ast = (int32_t*)h.st.p;
+    int32_t* vst = ast + n_groups;
+    const int rc = launch_tagg_verify(c, (const uint8_t*)h.sig.p, (const int64_t*)h.ids.p, (const uint64_t*)h.off.p,
+                                      n_groups, n_parts, (const uint8_t*)h.pk.p, (const uint8_t*)h.msg.p,
+                                      (const uint64_t*)h.moff.p, (uint8_t*)h.out.p, ast, vst, s);
+    if (rc) {
+      (void)hipStreamSynchronize(s);  // nothing the failed call enqueued may still read the caller's host arrays
+      return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(h.h_out, h.out.p, n_groups * 96, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h.h_st, h.st.p, n_groups * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(h.done, s));
   }
-  HIP_TRY(hipMemcpyAsync(c.b_off.p, goffs, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_pk.p, dv_pks, n_groups * 48, hipMemcpyHostToDevice, c.stream));
-  if (msg_total) HIP_TRY(hipMemcpyAsync(c.b_msg.p, msgs, msg_total, hipMemcpyHostToDevice, c.stream));
-  HIP_TRY(hipMemcpyAsync(c.b_kidx.p, moffs, (n_groups + 1) * 8, hipMemcpyHostToDevice, c.stream));
-  int32_t* ast = (int32_t*)c.b_st.p;
-  int32_t* vst = ast + n_groups;
-  int rc = launch_tagg_verify(c, (const uint8_t*)c.b_sig.p, (const int64_t*)c.b_ids.p, (const uint64_t*)c.b_off.p,
-                              n_groups, n_parts, (const uint8_t*)c.b_pk.p, (const uint8_t*)c.b_msg.p,
-                              (const uint64_t*)c.b_kidx.p, (uint8_t*)c.b_out.p, ast, vst, c.stream);
-  if (rc) return rc;
-  rc = ws_end(c, c.stream);  // the general input/output buffers above
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(out_sigs, c.b_out.p, n_groups * 96, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipMemcpyAsync(agg_status, ast, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipMemcpyAsync(verify_status, vst, n_groups * 4, hipMemcpyDeviceToHost, c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
+  HIP_TRY(hipEventSynchronize(h.done));
+  memcpy(out_sigs, h.h_out, n_groups * 96);
+  memcpy(agg_status, h.h_st, n_groups * 4);
+  memcpy(verify_status, h.h_st + n_groups, n_groups * 4);
   return HIPBLS_OK;
 }
 
@@ -2348,6 +2455,11 @@ int hipbls_rlc_batch_stats(uint64_t* attempted, uint64_t* passed, int32_t* last)
   return HIPBLS_OK;
 }
 
+int hipbls_set_latency_replicas(uint32_t replicas) {
+  if (replicas < 1 || replicas > 32) return arg_err("latency replicas out of range (1-32)");
+  return (int)g_lat_replicas.exchange(replicas);
+}
+
 int hipbls_set_pair_mode(int mode) {
   if (mode != HIPBLS_PAIR_AUTO && mode != HIPBLS_PAIR_SINGLE && mode != HIPBLS_PAIR_LANES && mode != HIPBLS_PAIR_QUADS &&
       mode != HIPBLS_PAIR_OCTETS)
@@ -2485,7 +2597,7 @@ int hipbls_threshold_aggregate_verify_batch(const uint8_t* sigs, const int64_t* 
   if (msg_offsets[n_groups] && !msgs) return arg_err("null messages");
   if (mul_overflows(n_parts, 288)) return arg_err("too many partials");
   ENSURE_INIT();
-  return run_ranges(plan_ranges(n_groups, parts_for(n_groups, kSplitGroups), nullptr),
+  return run_ranges_unlocked(plan_ranges(n_groups, parts_for(n_groups, kSplitGroups), nullptr),
                     [&](Context& c, uint64_t lo, uint64_t hi) {
                       std::vector<uint64_t> tg, tm;
                       const uint64_t p0 = group_offsets[lo];

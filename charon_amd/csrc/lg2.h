@@ -26,6 +26,13 @@ namespace bls {
 
 #if defined(__HIPCC__)
 
+// Replica race hook (verify_lat.hip): a latency kernel launched as several replicas of the same work, one per XCD,
+// polls here at coarse steps and ends a replica once another has finished (the first finisher wins; every replica
+// computes the same result).  An empty statement in every other build.
+#ifndef BLS_RACE_POLL
+#define BLS_RACE_POLL() ((void)0)
+#endif
+
 // Partner lane's value (lane ^ 1).  Both lanes of the pair must be active.
 __device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -536,6 +543,7 @@ BLS_CALL __device__ void miller_loop_split(fp6& h_out, const g1a& P_in, const g2
   fp6_set_zero(zero6);
   h = sel(m, zero6, one6);
   for (int bit = 62; bit >= 0; --bit) {
+    if ((bit & 7) == 7) BLS_RACE_POLL();
     if (bit != 62) fp12h_sqr_split(h, m);
     fp2 g0, g1, h1;
 #if BLS_LQ4_DBL_SPLIT
@@ -696,6 +704,7 @@ BLS_CALL __device__ bool fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, cons
   int s = 0;
 #pragma unroll 1
   for (int k = 1; k <= 63; ++k) {
+    if ((k & 7) == 0) BLS_RACE_POLL();
     cyc_sqr_compressed_quad(c, qm);
     if (k == 16 || k == 48 || k == 57 || k == 60 || k == 62 || k == 63) st[s++] = c;
   }
@@ -771,6 +780,7 @@ BLS_HD BLS_INLINE void fp12q_exp_xabs(fp12& r, const fp12& a_in, const quad_m& q
 
 // final_exponentiation (pairing.h) on a quad: the same formula and the same result on every lane.
 BLS_CALL __device__ void final_exponentiation_quad(fp12& r, const fp12& f_in, const quad_m& qm) {
+  BLS_RACE_POLL();
   // temporaries scoped so their frame slots can be shared (pairing_lds.h final_exponentiation_l); r may alias f_in
   fp12 m;
   {
@@ -962,6 +972,7 @@ BLS_CALL __device__ void hash_to_g2_pair_sum(g2j& s, const uint8_t* msg, uint32_
   fp_from_be64_words(u1.c0, uni + 32);
   fp_from_be64_words(u1.c1, uni + 48);
   fp2 zu0, zu1, d0, d1, t0, t1, inv;
+  BLS_RACE_POLL();
   sswu_den(zu0, d0, u0);
   sswu_den(zu1, d1, u1);
   fp2_mul(inv, d0, d1);
@@ -975,8 +986,10 @@ BLS_CALL __device__ void hash_to_g2_pair_sum(g2j& s, const uint8_t* msg, uint32_
   }
   const fp2 u = sel(m, u1, u0), zu = sel(m, zu1, zu0), t = sel(m, t1, t0);
   g2a qa;
+  BLS_RACE_POLL();
   map_to_curve_sswu_tv(qa, u, zu, t);
   g2j q, qo, q0, q1;
+  BLS_RACE_POLL();
   iso_map_g2(q, qa);
   pair_swap_words<72>(&qo.x.c0.v[0], &q.x.c0.v[0]);
   sel_words<72>(&q0.x.c0.v[0], m, &qo.x.c0.v[0], &q.x.c0.v[0]);  // the even lane's point (u0)

@@ -82,6 +82,23 @@ struct f12l {
 };
 
 // fp6_mul (tower.h) with the operands' coefficients fetched at each use: a(i), b(i) return coefficient i.
+#if BLS_LAZY_FP6
+// The lazy-reduction experiment: schoolbook, each output coefficient one sum of three Fp2
+// products with ONE Montgomery reduction per Fp coefficient (fp2_mul3): c0 = a0 b0 + (xi a1) b2 + (xi a2) b1,
+// c1 = a0 b1 + a1 b0 + (xi a2) b2, c2 = a0 b2 + a1 b1 + a2 b0.  Operands canonical.
+template <class A, class B>
+BLS_HD BLS_INLINE void fp6_mul_fetch(fp6& r, const A& a, const B& b) {
+  fp2 xa1, xa2, c0, c1, c2;
+  fp2_mul_xi(xa1, a(1));
+  fp2_mul_xi(xa2, a(2));
+  fp2_mul3(c0, a(0), b(0), xa1, b(2), xa2, b(1));
+  fp2_mul3(c1, a(0), b(1), a(1), b(0), xa2, b(2));
+  fp2_mul3(c2, a(0), b(2), a(1), b(1), a(2), b(0));
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+#else
 template <class A, class B>
 BLS_HD BLS_INLINE void fp6_mul_fetch(fp6& r, const A& a, const B& b) {
   fp2 t0, t1, t2, s0, s1, u0, u1, u2;
@@ -113,6 +130,7 @@ BLS_HD BLS_INLINE void fp6_mul_fetch(fp6& r, const A& a, const B& b) {
   r.c1 = u1;
   r.c2 = u2;
 }
+#endif
 
 // f <- f^2 in place (fp12_sqr_inl's complex squaring).  t = a0 a1 first; then a0 + a1 and a0 + v a1 overwrite a0 and
 // a1 (a1 held in registers for the pass), and their product s gives c0 = s - t - v t, c1 = 2t.
@@ -199,6 +217,16 @@ BLS_HD BLS_INLINE void fp12_mul_line2_l(const f12l<S>& F, const fp2& ga0_in, con
   fp2_sub(y, y, phh);  // ga1 hb1 + ha1 gb1
   fp6 t0, t1;
   fp6_mul_fetch(t0, [&](int i) { return F.ld(i); }, [&](int i) { return i == 0 ? L0.c0 : (i == 1 ? L0.c1 : L0.c2); });
+#if BLS_LAZY_FP6
+  {  // t1 = F1 (x v + y v^2) = xi(a1 y + a2 x) + (a0 x + xi a2 y) v + (a0 y + a1 x) v^2, one reduction per coefficient
+    fp2 u, xa2;
+    fp2_mul2(u, F.ld(4), y, F.ld(5), x);
+    fp2_mul_xi(t1.c0, u);
+    fp2_mul_xi(xa2, F.ld(5));
+    fp2_mul2(t1.c1, F.ld(3), x, xa2, y);
+    fp2_mul2(t1.c2, F.ld(3), y, F.ld(4), x);
+  }
+#else
   {  // t1 = F1 (x v + y v^2) = xi(a1 y + a2 x) + (a0 x + xi a2 y) v + (a0 y + a1 x) v^2
     fp2 m1, m2, m0, u, w2;
     fp2_mul(m1, F.ld(4), x);
@@ -215,6 +243,7 @@ BLS_HD BLS_INLINE void fp12_mul_line2_l(const f12l<S>& F, const fp2& ga0_in, con
     fp2_mul(u, F.ld(3), y);
     fp2_add(t1.c2, u, m1);
   }
+#endif
   fp2 c;
   for (int i = 0; i < 3; ++i) {  // F1 <- F0 + F1
     fp2_add(c, F.ld(i), F.ld(3 + i));
@@ -248,6 +277,16 @@ BLS_HD BLS_INLINE void fp12_mul_line2_l(const f12l<S>& F, const fp2& ga0_in, con
 // fp6_mul_01 / fp6_mul_1 (tower.h) with a's coefficients fetched at each use.
 template <class A>
 BLS_HD BLS_INLINE void fp6_mul_01_fetch(fp6& r, const A& a, const fp2& b0, const fp2& b1) {
+#if BLS_LAZY_FP6  // one reduction per coefficient: c0 = a0 b0 + (xi a2) b1, c1 = a0 b1 + a1 b0, c2 = a2 b0 + a1 b1
+  fp2 xa2, c0, c1, c2;
+  fp2_mul_xi(xa2, a(2));
+  fp2_mul2(c0, a(0), b0, xa2, b1);
+  fp2_mul2(c1, a(0), b1, a(1), b0);
+  fp2_mul2(c2, a(2), b0, a(1), b1);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+#else
   fp2 t0, t1, s0, s1, u, c0, c1, c2;
   fp2_mul(t0, a(0), b0);
   fp2_mul(t1, a(1), b1);
@@ -264,6 +303,7 @@ BLS_HD BLS_INLINE void fp6_mul_01_fetch(fp6& r, const A& a, const fp2& b0, const
   r.c0 = c0;
   r.c1 = c1;
   r.c2 = c2;
+#endif
 }
 template <class A>
 BLS_HD BLS_INLINE void fp6_mul_1_fetch(fp6& r, const A& a, const fp2& b1) {

@@ -219,6 +219,49 @@ BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
   fp_sub(r.c1, t2, t1);
 }
 #endif
+// Sums of Fp2 products with ONE Montgomery reduction per output coefficient (the lazy-reduction experiment,
+// BLS_LAZY_FP6; tools/gen_fp_asm.py gen_fp2_mul2 / gen_fp2_mul3): r = x y + z w (+ u t).  Canonical operands.
+#if defined(__HIP_DEVICE_COMPILE__) && BLS_LAZY_FP6 && !BLS_FP2_PAIR
+BLS_HD BLS_INLINE void fp2_mul2(fp2& r, const fp2& x, const fp2& y, const fp2& z, const fp2& w) {
+  u32x12 x0 = fp_to_vec(x.c0), x1 = fp_to_vec(x.c1), y0 = fp_to_vec(y.c0), y1 = fp_to_vec(y.c1);
+  u32x12 z0 = fp_to_vec(z.c0), z1 = fp_to_vec(z.c1), w0 = fp_to_vec(w.c0), w1 = fp_to_vec(w.c1), c0, c1;
+  asm volatile(BLS_ASM_CALL("bls_fp2_mul2_rt")
+               : "+{v[0:11]}"(x0), "+{v[12:23]}"(x1), "+{v[24:35]}"(y0), "+{v[36:47]}"(y1), "+{v[88:99]}"(z0),
+                 "+{v[100:111]}"(z1), "+{v[112:123]}"(w0), "+{v[124:135]}"(w1), "={v[52:63]}"(c1), "={v[64:75]}"(c0)
+               :
+               : BLS_FP2_MUL2_ASM_CLOBBERS, "s30", "s31", "scc");
+  fp_from_vec(r.c0, c0);
+  fp_from_vec(r.c1, c1);
+}
+BLS_HD BLS_INLINE void fp2_mul3(fp2& r, const fp2& x, const fp2& y, const fp2& z, const fp2& w, const fp2& u,
+                                const fp2& t) {
+  u32x12 x0 = fp_to_vec(x.c0), x1 = fp_to_vec(x.c1), y0 = fp_to_vec(y.c0), y1 = fp_to_vec(y.c1);
+  u32x12 z0 = fp_to_vec(z.c0), z1 = fp_to_vec(z.c1), w0 = fp_to_vec(w.c0), w1 = fp_to_vec(w.c1);
+  u32x12 u0 = fp_to_vec(u.c0), u1 = fp_to_vec(u.c1), t0 = fp_to_vec(t.c0), t1 = fp_to_vec(t.c1), c0, c1;
+  asm volatile(BLS_ASM_CALL("bls_fp2_mul3_rt")
+               : "+{v[0:11]}"(x0), "+{v[12:23]}"(x1), "+{v[24:35]}"(y0), "+{v[36:47]}"(y1), "+{v[88:99]}"(z0),
+                 "+{v[100:111]}"(z1), "+{v[112:123]}"(w0), "+{v[124:135]}"(w1), "+{v[136:147]}"(u0),
+                 "+{v[148:159]}"(u1), "+{v[160:171]}"(t0), "+{v[172:183]}"(t1), "={v[52:63]}"(c1), "={v[64:75]}"(c0)
+               :
+               : BLS_FP2_MUL2_ASM_CLOBBERS, "s30", "s31", "scc");
+  fp_from_vec(r.c0, c0);
+  fp_from_vec(r.c1, c1);
+}
+#else
+BLS_HD BLS_INLINE void fp2_mul2(fp2& r, const fp2& x, const fp2& y, const fp2& z, const fp2& w) {
+  fp2 a, b;
+  fp2_mul(a, x, y);
+  fp2_mul(b, z, w);
+  fp2_add(r, a, b);
+}
+BLS_HD BLS_INLINE void fp2_mul3(fp2& r, const fp2& x, const fp2& y, const fp2& z, const fp2& w, const fp2& u,
+                                const fp2& t) {
+  fp2 a, b;
+  fp2_mul2(a, x, y, z, w);
+  fp2_mul(b, u, t);
+  fp2_add(r, a, b);
+}
+#endif
 // (a0+a1)(a0-a1) + 2 a0 a1 u with three Fp products; the sum and difference only feed the product: unreduced
 BLS_HD BLS_INLINE void fp2_sqr_c(fp2& r, const fp2& a) {
   fp s, d, m;

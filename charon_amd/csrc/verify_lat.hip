@@ -16,6 +16,45 @@
 #define bls bls_fp2p
 #include <hip/hip_runtime.h>
 
+// ---------------------------------------------------------------- replica races (the n = 1 drop-in path)
+// The octet check of one item takes 7.2 to 9.8 ms depending on where its single wave runs: eight copies of the same
+// work in one launch, one per XCD, finished 7.2-9.8 ms apart with no XCD consistently fast
+// (profiles/r05/r05_xcd_lq8.txt).  So a batch of at most 8 items runs as `replicas` copies of its workgroups; every
+// copy computes the same result, polls its race word at coarse steps (BLS_RACE_POLL in lg2.h and below), and the
+// first to finish sets the word to this launch's epoch, which ends the others.  The word lives in LDS per workgroup
+// (nullptr: not raced); EVERY kernel of this translation unit sets it at entry, since LDS is not zero-initialized.
+namespace bls_race {
+__shared__ uint32_t* s_word;
+__shared__ uint32_t s_epoch;
+__device__ __forceinline__ void init(uint32_t* word, uint32_t epoch) {
+  s_word = word;
+  s_epoch = epoch;
+}
+__device__ __forceinline__ uint32_t* word_u() {  // wave-uniform copy of the LDS pointer; nullptr unless 64-aligned
+  const uint64_t w = (uint64_t)s_word;
+  // readfirstlane returns int: each half goes through uint32_t, or a low half with bit 31 set (half of all buffer
+  // addresses) sign-extends over the high half -- round 5's first race build read a wild address (an illegal access in
+  // one run, a hung queue worker in the next)
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)w);
+  const uint64_t u = ((uint64_t)hi << 32) | lo;
+  return (u & 63) ? nullptr : (uint32_t*)u;
+}
+__device__ __forceinline__ void poll() {
+  uint32_t* w = word_u();
+  if (!w) return;
+  const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((uint32_t)__builtin_amdgcn_readfirstlane(v) == (uint32_t)__builtin_amdgcn_readfirstlane(s_epoch))
+    asm volatile("s_endpgm");
+}
+// After this copy's results are stored: the race is won (the other copies end at their next poll).
+__device__ __forceinline__ void finish() {
+  uint32_t* w = word_u();
+  if (w && threadIdx.x == 0) __hip_atomic_store(w, s_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace bls_race
+#define BLS_RACE_POLL() ::bls_race::poll()
+
 #include "lg2.h"
 #include "rlcb.h"
 
@@ -63,6 +102,7 @@ __device__ void g2_mul_xabs_quad(g2j& r, const g2j& p_in, int q) {
   const g2j p = p_in;
   g2j acc = p;
   for (int i = 62; i >= 0; --i) {
+    if ((i & 7) == 7) BLS_RACE_POLL();
     g2j t;
     g2_dbl_quad(t, acc, q);
     acc = t;
@@ -100,15 +140,20 @@ __device__ void g2_clear_cofactor_quad(g2j& r, const g2j& p_in, int q) {
 // quad split the two SSWU maps, lg2.h hash_to_g2_pair_sum, and the quad clears the cofactor).  The decode codes go
 // to ws + 120 n (two words per item); k_verify_pair_lq8 composes the status in herumi's order.  ws: pk (24 x n),
 // H(m) (48 x n), sig (48 x n), SoA.
+// Replicas: `replicas` consecutive workgroups run the same original workgroup (race word race[role], epoch).
 __global__ void __launch_bounds__(kOctBlock) k_verify_prep8(const uint8_t* __restrict__ pks,
                                                             const uint8_t* __restrict__ msgs,
                                                             const uint64_t* __restrict__ offs,
                                                             const uint8_t* __restrict__ sigs, uint64_t n,
-                                                            uint32_t* __restrict__ ws, int32_t* __restrict__ status) {
+                                                            uint32_t* __restrict__ ws, int32_t* __restrict__ status,
+                                                            uint32_t replicas, uint32_t* __restrict__ race,
+                                                            uint32_t epoch) {
   (void)status;  // k_verify_pair_lq8 writes every status
   const uint64_t nb = (8 * n + kOctBlock - 1) / kOctBlock;
-  const uint64_t role = blockIdx.x / nb;  // 0 key, 1 signature, 2 hash: uniform per workgroup
-  const uint64_t t = (blockIdx.x - role * nb) * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t rb = blockIdx.x / replicas;  // the original workgroup this copy runs
+  const uint64_t role = rb / nb;              // 0 key, 1 signature, 2 hash: uniform per workgroup
+  bls_race::init(replicas > 1 ? race + role : nullptr, epoch);
+  const uint64_t t = (rb - role * nb) * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t i = t >> 3;
   if (i >= n) return;  // the same on all eight lanes
   const bool lead = (t & 7) == 0;
@@ -122,6 +167,7 @@ __global__ void __launch_bounds__(kOctBlock) k_verify_prep8(const uint8_t* __res
     g2a hm;
     jac_to_aff(hm, hj);
     if (lead) soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);
+    bls_race::finish();
     return;
   }
   if (role == 0) {
@@ -131,6 +177,7 @@ __global__ void __launch_bounds__(kOctBlock) k_verify_prep8(const uint8_t* __res
       codes[2 * i] = dp;
       if (dp == DEC_OK) soa_store<24>(ws, n, i, &pk.x.v[0]);
     }
+    bls_race::finish();
     return;
   }
   g2a sig;
@@ -139,13 +186,44 @@ __global__ void __launch_bounds__(kOctBlock) k_verify_prep8(const uint8_t* __res
     codes[2 * i + 1] = ds;
     if (ds == DEC_OK) soa_store<48>(ws + 72 * n, n, i, &sig.x.c0.v[0]);
   }
+  bls_race::finish();
 }
+
+#ifndef BLS_LQ8_XCD_PROBE
+#define BLS_LQ8_XCD_PROBE 0
+#endif
+#if BLS_LQ8_XCD_PROBE
+// Experiment build only (scripts/xcd_lq8_probe.py): every workgroup runs 8 times, once per XCD, each copy recording its
+// XCC id and its start / end on the 100 MHz real-time counter, to see whether the check's duration depends on the XCD
+// its workgroup lands on.
+__device__ uint64_t g_xcd_probe[64 * 4];
+#endif
 
 // Stage 2, eight lanes per item: the status from the decode codes in herumi's order (key, then signature, then the
 // infinity cases), then lq4_verify on lanes 0-3 (q = t & 3) and, as their Fp2 twins, on 4-7.
 __global__ void __launch_bounds__(kOctBlock) k_verify_pair_lq8(const uint32_t* __restrict__ ws, uint64_t n,
-                                                               int32_t* __restrict__ status) {
-  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+                                                               int32_t* __restrict__ status, uint32_t replicas,
+                                                               uint32_t* __restrict__ race, uint32_t epoch) {
+  bls_race::init(replicas > 1 ? race + 3 : nullptr, epoch);
+#if BLS_LQ8_XCD_PROBE
+  const uint64_t t0_probe = __builtin_amdgcn_s_memrealtime();
+  const uint64_t t = (blockIdx.x >> 3) * (uint64_t)blockDim.x + threadIdx.x;
+  struct ProbeEnd {
+    uint64_t t0;
+    __device__ ~ProbeEnd() {
+      const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+      uint32_t x;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+      if (threadIdx.x == 0 && blockIdx.x < 64) {
+        g_xcd_probe[4 * blockIdx.x] = x;
+        g_xcd_probe[4 * blockIdx.x + 1] = t0;
+        g_xcd_probe[4 * blockIdx.x + 2] = t1;
+      }
+    }
+  } probe_end{t0_probe};
+#else
+  const uint64_t t = (blockIdx.x / replicas) * (uint64_t)blockDim.x + threadIdx.x;
+#endif
   const uint64_t i = t >> 3;
   if (i >= n) return;  // the same on all eight lanes
   const int32_t* codes = (const int32_t*)(ws + 120 * n);
@@ -170,12 +248,14 @@ __global__ void __launch_bounds__(kOctBlock) k_verify_pair_lq8(const uint32_t* _
   soa_load<48>(&hm.x.c0.v[0], ws + 24 * n, n, i);
   st = lq4_verify(pk, hm, sig, (int)(t & 3));
   if (lead) status[i] = st;
+  bls_race::finish();
 }
 
 // ---------------------------------------------------------------- the batch-wide RLC check's tail (rlcb.h)
 // The Miller value of (-g1, S), S = W0 + [2^16] W1 from the MSM's window sums (rlcb.h msm_combine): lanes 0/1 split
 // the loop (lg2.h miller_loop_split), lanes 4/5 are their Fp2 twins (2, 3, 6, 7 repeat them); 144 words to Fs.
 __global__ void __launch_bounds__(kOctBlock) k_rlcb_sfactor8(const uint32_t* __restrict__ W, uint32_t* __restrict__ Fs) {
+  bls_race::init(nullptr, 0);  // not raced (LDS is not zero-initialized)
   const int t = threadIdx.x;
   if (t >= 8) return;
   const uint32_t m = (t & 1) ? ~0u : 0u;
@@ -206,6 +286,7 @@ __global__ void __launch_bounds__(kOctBlock) k_rlcb_sfactor8(const uint32_t* __r
 // quad (lanes 0-3, lg2.h fp12q_mul / final_exponentiation_quad) with Fp2 twins on 4-7; flag[0] = 1 when it is 1.
 __global__ void __launch_bounds__(kOctBlock) k_rlcb_final8(const uint32_t* __restrict__ Ftot,
                                                            const uint32_t* __restrict__ Fs, int32_t* __restrict__ flag) {
+  bls_race::init(nullptr, 0);  // not raced (LDS is not zero-initialized)
   const int t = threadIdx.x;
   if (t >= 8) return;
   fp12 a, b, r, e;
@@ -229,6 +310,7 @@ __global__ void __launch_bounds__(kOctBlock) k_g1m_miller8(uint64_t nl_max, cons
                                                            const uint32_t* __restrict__ H, uint64_t hstride,
                                                            const uint32_t* __restrict__ hslot, uint32_t* __restrict__ F,
                                                            uint64_t col0, uint64_t fstride) {
+  bls_race::init(nullptr, 0);  // not raced (LDS is not zero-initialized)
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t L = t >> 3;
   if (L >= nl_max) return;  // the same on all eight lanes
@@ -252,3 +334,9 @@ __global__ void __launch_bounds__(kOctBlock) k_g1m_miller8(uint64_t nl_max, cons
 }
 
 }  // namespace bls
+
+#if BLS_LQ8_XCD_PROBE
+extern "C" int hipbls_debug_xcd_probe(uint64_t* out256) {
+  return hipMemcpyFromSymbol(out256, HIP_SYMBOL(bls_fp2p::g_xcd_probe), sizeof(uint64_t) * 256) == hipSuccess ? 0 : 17;
+}
+#endif

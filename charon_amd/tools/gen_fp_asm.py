@@ -399,6 +399,127 @@ def _gen_prod(w, X, Y, M, R=None):
     w("v_mov_b32 %s, v50" % R(N32 - 1))
 
 
+def _gen_sopn(w, pairs, M):
+    """Appends r = (sum of X*Y over `pairs`)/2^384 mod p to the stream w (_gen_sop with any number of product
+    terms per column): quotient digits in M(i), result limb j over M(j)."""
+    first = [True]
+    src2 = ["v[48:49]"]
+
+    def mac(x, y):
+        w("v_mad_u64_u32 v[48:49], vcc, %s, %s, %s" % (x, y, src2[0]))
+        src2[0] = "v[48:49]"
+        if first[0]:
+            w("v_addc_co_u32_e64 v51, vcc, 0, 0, vcc")
+            first[0] = False
+        else:
+            w("v_addc_co_u32_e32 v51, vcc, 0, v51, vcc")
+
+    def shift():
+        w("v_mov_b32 v50, v49")
+        src2[0] = "v[50:51]"
+        first[0] = True
+
+    Sp = lambda j: "s%d" % (16 + j)
+    X0, Y0 = pairs[0]
+    w("v_mad_u64_u32 v[48:49], vcc, %s, %s, 0" % (X0(0), Y0(0)))
+    w("v_mov_b32 v51, 0")
+    first[0] = False
+    for X, Y in pairs[1:]:
+        mac(X(0), Y(0))
+    w("v_mul_lo_u32 %s, v48, s28" % M(0))
+    mac(M(0), "s16")
+    shift()
+    for i in range(1, N32):
+        for j in range(i):
+            for X, Y in pairs:
+                mac(X(j), Y(i - j))
+            mac(M(j), Sp(i - j))
+        for X, Y in pairs:
+            mac(X(i), Y(0))
+        w("v_mul_lo_u32 %s, v48, s28" % M(i))
+        mac(M(i), "s16")
+        shift()
+    for i in range(N32, 2 * N32 - 1):
+        for j in range(i - N32 + 1, N32):
+            for X, Y in pairs:
+                mac(X(j), Y(i - j))
+            mac(M(j), Sp(i - j))
+        w("v_mov_b32 %s, v48" % M(i - N32))
+        shift()
+    w("v_mov_b32 %s, v50" % M(N32 - 1))
+
+
+# EXPERIMENT (VERDICT r04 item 7, lazy reduction): an Fp2 sum of two products with ONE Montgomery reduction per output
+# coefficient -- double-width accumulation of four 384 x 384 products per column:
+#   c1 = (x0 y1 + x1 y0 + z0 w1 + z1 w0)/R,   c0 = (x0 y0 + x1 (2p - y1) + z0 w0 + z1 (2p - w1))/R
+# 2 x 720 mads for x y + z w against 2 x 864 for two gen_fp2_mul calls plus an Fp2 addition.  Canonical operands
+# (< p): each sum is < 6p^2 < pR, the output < 1.61p, one conditional subtraction.  Registers: x0 = v[0:11],
+# x1 = v[12:23], y0 = v[24:35], y1 = v[36:47], z0 = v[88:99], z1 = v[100:111], w0 = v[112:123], w1 = v[124:135];
+# c1 -> v[52:63], c0 -> v[64:75]; y1 and w1 clobbered, v48-v51, v76-v87, s16-s28, vcc clobbered.
+FP2M2_Z0, FP2M2_Z1, FP2M2_W0, FP2M2_W1 = 88, 100, 112, 124
+
+
+# ... and the three-product form (fp12_sqr_l's dense Fp6 products as schoolbook sums): c = x y + z w + u t with
+# u0 = v[136:147], u1 = v[148:159], t0 = v[160:171], t1 = v[172:183] (t1 clobbered as well).  Canonical operands: each
+# coefficient's sum is < 9p^2 < pR (p < 2^380.8), the output < 1.92p.
+FP2M3_U0, FP2M3_U1, FP2M3_T0, FP2M3_T1 = 136, 148, 160, 172
+
+
+def gen_fp2_mul3():
+    PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
+    PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    P2L = [((2 * P) >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    V = lambda base: (lambda j: "v%d" % (base + j))
+    X0, X1, Y0, Y1, C1, C0, T = V(0), V(12), V(24), V(36), V(FP2_C1), V(FP2_C0), V(FP2_T)
+    Z0, Z1, W0, W1 = V(FP2M2_Z0), V(FP2M2_Z1), V(FP2M2_W0), V(FP2M2_W1)
+    U0, U1, T0, T1 = V(FP2M3_U0), V(FP2M3_U1), V(FP2M3_T0), V(FP2M3_T1)
+    out = []
+    w = out.append
+    for j in range(N32):
+        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
+    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    _gen_sopn(w, [(X0, Y1), (X1, Y0), (Z0, W1), (Z1, W0), (U0, T1), (U1, T0)], C1)
+    for j in range(N32):
+        w("v_mov_b32 %s, 0x%08x" % (C0(j), P2L[j]))
+    for B in (Y1, W1, T1):
+        w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (B(0), C0(0), B(0)))
+        for j in range(1, N32):
+            w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (B(j), C0(j), B(j)))
+    _gen_sopn(w, [(X0, Y0), (X1, Y1), (Z0, W0), (Z1, W1), (U0, T0), (U1, T1)], C0)
+    for j in range(N32):
+        w("v_mov_b32 %s, s%d" % (Y1(j), 16 + j))
+    for C in (C1, C0):
+        _final_sub(w, C, Y1, T, "v48")
+    return out
+
+
+def gen_fp2_mul2():
+    PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
+    PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    P2L = [((2 * P) >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+    V = lambda base: (lambda j: "v%d" % (base + j))
+    X0, X1, Y0, Y1, C1, C0, T = V(0), V(12), V(24), V(36), V(FP2_C1), V(FP2_C0), V(FP2_T)
+    Z0, Z1, W0, W1 = V(FP2M2_Z0), V(FP2M2_Z1), V(FP2M2_W0), V(FP2M2_W1)
+    out = []
+    w = out.append
+    for j in range(N32):
+        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
+    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    _gen_sopn(w, [(X0, Y1), (X1, Y0), (Z0, W1), (Z1, W0)], C1)   # c1 (raw, < 2p)
+    for j in range(N32):                                           # 2p into VGPRs
+        w("v_mov_b32 %s, 0x%08x" % (C0(j), P2L[j]))
+    for B in (Y1, W1):                                             # y1 <- 2p - y1, w1 <- 2p - w1
+        w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (B(0), C0(0), B(0)))
+        for j in range(1, N32):
+            w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (B(j), C0(j), B(j)))
+    _gen_sopn(w, [(X0, Y0), (X1, Y1), (Z0, W0), (Z1, W1)], C0)   # c0 (raw)
+    for j in range(N32):                                           # p over the dead 2p - y1
+        w("v_mov_b32 %s, s%d" % (Y1(j), 16 + j))
+    for C in (C1, C0):
+        _final_sub(w, C, Y1, T, "v48")
+    return out
+
+
 # Fp2 squaring: c0 = (a0 + a1)(a0 + p - a1)/R, c1 = a0 (a1 + a1)/R.  The three operand sums stay unreduced
 # (< 2p each, products < 4p^2 < pR) and the doubling of c1 moves onto an operand, so the routine is two products,
 # three 12-word add/sub chains and two final subtractions.  a0 = v[0:11], a1 = v[12:23] (clobbered); c0 -> v[24:35],
@@ -822,6 +943,9 @@ def emit_header(path, bodies, extra=()):
     lines.append("#define BLS_FP2_MUL_HALF_ASM_CLOBBERS %s" % clob4)
     clob5 = ", ".join('"v%d"' % r for r in range(36, 76)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
     lines.append("#define BLS_FP2_SQR_HALF_ASM_CLOBBERS %s" % clob5)
+    clob6 = ", ".join('"v%d"' % r for r in list(range(48, 52)) + list(range(76, 88))) + ', "vcc", ' + \
+        ", ".join('"s%d"' % r for r in range(16, 29))
+    lines.append("#define BLS_FP2_MUL2_ASM_CLOBBERS %s" % clob6)
     for name, body in extra:
         lines.append("")
         lines.append("// %s: %d instructions, positional operands (see tools/gen_fp_asm.py)" % (name, len(body)))
@@ -842,7 +966,8 @@ def main():
     fp2s = gen_fp2_sqr()
     emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul), ("BLS_FP2_MUL_ASM_BODY", fp2), ("BLS_FP2_SQR_ASM_BODY", fp2s),
                        ("BLS_FP2_MUL_HALF_ASM_BODY", gen_fp2_mul_half()),
-                       ("BLS_FP2_SQR_HALF_ASM_BODY", gen_fp2_sqr_half())],
+                       ("BLS_FP2_SQR_HALF_ASM_BODY", gen_fp2_sqr_half()),
+                       ("BLS_FP2_MUL2_ASM_BODY", gen_fp2_mul2()), ("BLS_FP2_MUL3_ASM_BODY", gen_fp2_mul3())],
                 extra=[("BLS_FP_ADD_ASM", gen_add()), ("BLS_FP_SUB_ASM", gen_sub()), ("BLS_FP_NEG_ASM", gen_sub(neg=True)),
                        ("BLS_FP_ADD_LAZY_ASM", gen_add_lazy()), ("BLS_FP_SUB_LAZY_ASM", gen_sub_lazy())])
     print("wrote %s: %d instructions" % (path, len(mul)))

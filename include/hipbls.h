@@ -117,6 +117,11 @@ int hipbls_set_timing(int enabled);
 enum { HIPBLS_PAIR_AUTO = 0, HIPBLS_PAIR_SINGLE = 1, HIPBLS_PAIR_LANES = 2, HIPBLS_PAIR_QUADS = 3,
        HIPBLS_PAIR_OCTETS = 4 };
 int hipbls_set_pair_mode(int mode);
+/* Replicas of a Verify batch of at most 8 items on octets (the drop-in n = 1 path): that many copies of its one
+ * workgroup race, one per XCD, and the first to finish each stage wins (the others end early); the results are the
+ * same.  A single wave's check time varies 7.2-9.8 ms with where it runs.  Default 8
+ * (HIPBLS_LAT_REPLICAS); 1 turns it off.  Returns the previous value, HIPBLS_ERR_ARG outside 1-32. */
+int hipbls_set_latency_replicas(uint32_t replicas);
 
 /* ------------------------------------------------ single-item Verify through the submission queue ---- */
 /* tbls.Verify for one item.  Concurrent callers (any thread) are coalesced into one kernel launch per batch:

@@ -198,3 +198,55 @@ def test_fp2_square_half_routine(half):
         assert c == want * R_INV % g.P, (t, hex(a0), hex(a1))
         for base, x in ((0, a0), (12, a1)):
             assert _val([regs[base + j] for j in range(12)]) == x
+
+
+def test_fp2_sum_of_products_routine():
+    """The lazy-reduction experiment's routine (BLS_FP2_MUL2_ASM_BODY, gen_fp2_mul2): c = x y + z w
+    with one Montgomery reduction per coefficient over four products, canonical on canonical operands (edges at the
+    final subtraction's boundary included); x0, x1, y0, z0, z1, w0 come back unchanged."""
+    body = _macro_body("BLS_FP2_MUL2_ASM_BODY")
+    assert body == g.gen_fp2_mul2(), "fp_asm_gfx950.h is stale: rerun charon_amd/tools/gen_fp_asm.py"
+    cases = _cases(60, 51)
+    rnd = random.Random(52)
+    for t in range(300):
+        x0, x1, y0, y1, z0, z1, w0, w1 = (rnd.choice(cases) for _ in range(8))
+        if t < 4:  # the largest sums the bound allows: every operand p - 1
+            x0 = x1 = y0 = z0 = z1 = w0 = g.P - 1
+            y1 = w1 = 0 if t & 1 else g.P - 1
+        regs = {}
+        for base, v in ((0, x0), (12, x1), (24, y0), (36, y1), (g.FP2M2_Z0, z0), (g.FP2M2_Z1, z1),
+                        (g.FP2M2_W0, w0), (g.FP2M2_W1, w1)):
+            regs.update({base + j: u for j, u in enumerate(_limbs(v))})
+        g.emulate(body, None, None, regs)
+        c0 = _val([regs[g.FP2_C0 + j] for j in range(12)])
+        c1 = _val([regs[g.FP2_C1 + j] for j in range(12)])
+        assert c0 == (x0 * y0 - x1 * y1 + z0 * w0 - z1 * w1) * R_INV % g.P, t
+        assert c1 == (x0 * y1 + x1 * y0 + z0 * w1 + z1 * w0) * R_INV % g.P, t
+        for base, v in ((0, x0), (12, x1), (24, y0), (g.FP2M2_Z0, z0), (g.FP2M2_Z1, z1), (g.FP2M2_W0, w0)):
+            assert _val([regs[base + j] for j in range(12)]) == v
+
+
+def test_fp2_sum_of_three_products_routine():
+    """BLS_FP2_MUL3_ASM_BODY (gen_fp2_mul3): c = x y + z w + u t, one reduction per coefficient over six products,
+    canonical on canonical operands, including all operands p - 1 (the largest sums)."""
+    body = _macro_body("BLS_FP2_MUL3_ASM_BODY")
+    assert body == g.gen_fp2_mul3(), "fp_asm_gfx950.h is stale: rerun charon_amd/tools/gen_fp_asm.py"
+    cases = _cases(60, 61)
+    rnd = random.Random(62)
+    for t in range(200):
+        v = [rnd.choice(cases) for _ in range(12)]
+        if t < 4:
+            v = [g.P - 1] * 12
+            if t & 1:
+                v[3] = v[7] = v[11] = 0
+        x0, x1, y0, y1, z0, z1, w0, w1, u0, u1, t0, t1 = v
+        regs = {}
+        for base, val in ((0, x0), (12, x1), (24, y0), (36, y1), (g.FP2M2_Z0, z0), (g.FP2M2_Z1, z1),
+                          (g.FP2M2_W0, w0), (g.FP2M2_W1, w1), (g.FP2M3_U0, u0), (g.FP2M3_U1, u1),
+                          (g.FP2M3_T0, t0), (g.FP2M3_T1, t1)):
+            regs.update({base + j: u for j, u in enumerate(_limbs(val))})
+        g.emulate(body, None, None, regs)
+        c0 = _val([regs[g.FP2_C0 + j] for j in range(12)])
+        c1 = _val([regs[g.FP2_C1 + j] for j in range(12)])
+        assert c0 == (x0 * y0 - x1 * y1 + z0 * w0 - z1 * w1 + u0 * t0 - u1 * t1) * R_INV % g.P, t
+        assert c1 == (x0 * y1 + x1 * y0 + z0 * w1 + z1 * w0 + u0 * t1 + u1 * t0) * R_INV % g.P, t

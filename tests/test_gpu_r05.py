@@ -152,3 +152,74 @@ def test_queue_worker_polls_from_expected_end(impl):
     print("queue worker: %.1f completion polls per n = 1 batch" % per_batch)
     # a ~12 ms batch polled every 20 us from its launch would take ~600 polls
     assert per_batch < 250
+
+
+def test_host_sigagg_calls_from_two_threads_overlap_and_match(impl):
+    """The host-buffer sigagg call holds the context lock only while it enqueues (two slots), so two
+    threads' calls run side by side on the GPU -- what two goroutines with consecutive sigagg duties do.  Every result
+    of 6 concurrent calls (3 per thread, different validator sets, two with a bad partial) equals the same call made
+    alone, and the aggregates equal Sign(secret)."""
+    import threading
+
+    from tests.test_gpu_r04 import _make_c3
+    sets = []
+    for k in range(6):
+        groups, secrets_, roots, dv_pks, _ = _make_c3(impl, G=1200, seed=0x5A + k)
+        gmaps = [dict(g) for g in groups]
+        if k in (1, 4):  # one partial of group 7 replaced by another group's: the aggregate fails Verify
+            key = next(iter(gmaps[7]))
+            gmaps[7][key] = groups[8][0][1]
+        sets.append((gmaps, dv_pks, roots, secrets_))
+    alone = [impl.batch_threshold_aggregate_verify(g, p, r) for g, p, r, _ in sets]
+    got = [None] * 6
+
+    def worker(ks):
+        for k in ks:
+            g, p, r, _ = sets[k]
+            got[k] = impl.batch_threshold_aggregate_verify(g, p, r)
+
+    th = [threading.Thread(target=worker, args=(ks,)) for ks in ((0, 2, 4), (1, 3, 5))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert got == alone
+    for k, (g, p, r, secrets_) in enumerate(sets):
+        aggs, vst = got[k]
+        want, st = impl.sign_batch([s.to_bytes(32, "big") for s in secrets_], r)
+        assert set(st) == {0}
+        for j in range(len(g)):
+            if k in (1, 4) and j == 7:
+                assert vst[j] == 3  # HIPBLS_ERR_VERIFY
+            else:
+                assert vst[j] == 0 and aggs[j] == want[j], (k, j)
+
+
+def test_raced_small_batches_across_workspace_growth(impl):
+    """Batches of at most 8 items run as replicas that race (verify_lat.hip bls_race) through words at the tail of
+    the Verify workspace.  The workspace moves every time a larger batch grows it, so small batches alternate with
+    larger ones here: every workspace address the sequence produces carries raced calls, and their statuses equal
+    the same items' statuses from one large call, with the race off (replicas = 1) and on (8).  Round 5's first race
+    build built the word's address from two sign-extended halves and read a wild address for half of all buffers."""
+    import bench
+    N = 20000
+    pks, roots, sigs, bad = bench.make_c2(impl, bench.share_keys(impl, 4096, "c2race"), 0, N)
+    want = impl.batch_verify_status(pks, roots, sigs)
+    assert {i for i, s in enumerate(want) if s} == bad
+    bad_l = sorted(bad)
+    good_l = [i for i in range(N) if i not in bad][:64]
+    small = [[bad_l[0]], [good_l[0]], [good_l[1], bad_l[1], good_l[2]], good_l[3:11], [bad_l[2]] + good_l[11:18]]
+    prev = impl.lib.hipbls_set_latency_replicas(8)
+    try:
+        for grow in (1, 700, 3000, 9000, N):
+            lo = (grow * 7) % max(1, N - grow)
+            got = impl.batch_verify_status(pks[lo:lo + grow], roots[lo:lo + grow], sigs[lo:lo + grow])
+            assert got == want[lo:lo + grow]
+            for reps in (8, 1, 8):
+                impl.lib.hipbls_set_latency_replicas(reps)
+                for idx in small:
+                    got = impl.batch_verify_status([pks[i] for i in idx], [roots[i] for i in idx],
+                                                   [sigs[i] for i in idx])
+                    assert got == [want[i] for i in idx], (grow, reps, idx)
+    finally:
+        impl.lib.hipbls_set_latency_replicas(prev)

@@ -74,3 +74,31 @@ def test_lds_slot_kernels_fit_four_workgroups_per_cu():
         if name in ("k_verify_fused", "k_verify_keys", "k_rlc_window", "k_rlcb_chunks"):
             assert lds == 36864, name
             assert 4 * lds <= 160 * 1024
+
+
+def test_race_polls_use_zero_extended_word_address(tmp_path):
+    """Every mid-program `s_endpgm` of the latency code object is a replica-race poll (verify_lat.hip bls_race::poll).
+    Its word address is rebuilt from two readfirstlane halves; readfirstlane returns int, and round 5's first race build
+    sign-extended the low half over the high one (`s_bfe_i64`), a wild address for half of all buffers.  The fixed code
+    builds the address with no sign extension, checked on the disassembly."""
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump) or not os.path.exists(LIB):
+        pytest.skip("llvm-objdump or the library missing")
+    polls = 0
+    for i, co in enumerate(codeobj.code_objects(LIB)):
+        f = tmp_path / ("co%d.elf" % i)
+        f.write_bytes(co)
+        lines = subprocess.run([objdump, "-d", "--no-show-raw-insn", str(f)], check=True, capture_output=True,
+                               text=True).stdout.splitlines()
+        for j, ln in enumerate(lines):
+            if "s_endpgm" not in ln or j + 1 >= len(lines) or not lines[j + 1].strip().startswith(("s_", "v_", "scratch",
+                                                                                                  "global", "flat",
+                                                                                                  "buffer", "ds_")):
+                continue
+            window = lines[max(0, j - 30):j]
+            if not any("flat_load_dword" in w or "global_load_dword" in w for w in window):
+                continue
+            polls += 1
+            assert not any("s_bfe_i64" in w or "s_ashr_i32" in w for w in window), "\n".join(window)
+    assert polls > 0
