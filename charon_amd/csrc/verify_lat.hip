@@ -30,7 +30,7 @@ __device__ __forceinline__ void init(uint32_t* word, uint32_t epoch) {
   s_word = word;
   s_epoch = epoch;
 }
-__device__ __forceinline__ uint32_t* word_u() {  // wave-uniform copy of the LDS pointer; nullptr unless 64-aligned
+__device__ __forceinline__ uint32_t* word_u() {  // wave-uniform copy of the LDS pointer; nullptr unless 4-aligned
   const uint64_t w = (uint64_t)s_word;
   // readfirstlane returns int: each half goes through uint32_t, or a low half with bit 31 set (half of all buffer
   // addresses) sign-extends over the high half -- round 5's first race build read a wild address (an illegal access in
@@ -38,19 +38,30 @@ __device__ __forceinline__ uint32_t* word_u() {  // wave-uniform copy of the LDS
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)w);
   const uint64_t u = ((uint64_t)hi << 32) | lo;
-  return (u & 63) ? nullptr : (uint32_t*)u;
+  return (u & 3) ? nullptr : (uint32_t*)u;  // the words are race[0..3]: the launch checks race's 64-B alignment
 }
+// The word is written by a wave on another XCD: the poll is a `global_load_dword ... sc1` (past this CU's L1, served
+// coherently across the XCDs' L2s) and the winner's store a write-through `global_store_dword ... sc1`
+// (MI355X_MICROARCH.md, inter-workgroup visibility: flag polls by global/buffer sc1 loads, never flat; the generic
+// pointer made __hip_atomic_load/store flat_ forms).  The second race build also asked each word for 64-byte alignment,
+// which only race[0] has: no polled stage was raced, and every raced kernel took as long as its slowest copy
+// (profiles/r05/race_trace_flat.json).
 __device__ __forceinline__ void poll() {
   uint32_t* w = word_u();
   if (!w) return;
-  const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(w) : "memory");
   if ((uint32_t)__builtin_amdgcn_readfirstlane(v) == (uint32_t)__builtin_amdgcn_readfirstlane(s_epoch))
     asm volatile("s_endpgm");
 }
 // After this copy's results are stored: the race is won (the other copies end at their next poll).
 __device__ __forceinline__ void finish() {
   uint32_t* w = word_u();
-  if (w && threadIdx.x == 0) __hip_atomic_store(w, s_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (w && threadIdx.x == 0) {
+    const uint32_t e = s_epoch;
+    asm volatile("s_waitcnt vmcnt(0)\n\tglobal_store_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : : "v"(w), "v"(e)
+                 : "memory");
+  }
 }
 }  // namespace bls_race
 #define BLS_RACE_POLL() ::bls_race::poll()

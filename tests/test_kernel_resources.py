@@ -80,7 +80,9 @@ def test_race_polls_use_zero_extended_word_address(tmp_path):
     """Every mid-program `s_endpgm` of the latency code object is a replica-race poll (verify_lat.hip bls_race::poll).
     Its word address is rebuilt from two readfirstlane halves; readfirstlane returns int, and round 5's first race build
     sign-extended the low half over the high one (`s_bfe_i64`), a wild address for half of all buffers.  The fixed code
-    builds the address with no sign extension, checked on the disassembly."""
+    builds the address with no sign extension and polls with a `global_load_dword ... sc1` (the first build's flat_ loads
+never saw another XCD's word), checked on the disassembly."""
+    import re
     import subprocess
     objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
     if not os.path.exists(objdump) or not os.path.exists(LIB):
@@ -92,13 +94,15 @@ def test_race_polls_use_zero_extended_word_address(tmp_path):
         lines = subprocess.run([objdump, "-d", "--no-show-raw-insn", str(f)], check=True, capture_output=True,
                                text=True).stdout.splitlines()
         for j, ln in enumerate(lines):
-            if "s_endpgm" not in ln or j + 1 >= len(lines) or not lines[j + 1].strip().startswith(("s_", "v_", "scratch",
-                                                                                                  "global", "flat",
-                                                                                                  "buffer", "ds_")):
+            # a poll: `s_cbranch_scc1` over one `s_endpgm`, more code after it (other kernels' early exits differ)
+            if "s_endpgm" not in ln or j + 1 >= len(lines) or not re.search(r"s_cbranch_scc1 1\s", lines[j - 1]):
+                continue
+            if not lines[j + 1].strip() or lines[j + 1].strip().startswith(("0", "<")):
                 continue
             window = lines[max(0, j - 30):j]
-            if not any("flat_load_dword" in w or "global_load_dword" in w for w in window):
-                continue
             polls += 1
             assert not any("s_bfe_i64" in w or "s_ashr_i32" in w for w in window), "\n".join(window)
+            # a flag written on another XCD is seen by global/buffer sc1 loads, never flat ones (MI355X_MICROARCH.md)
+            assert not any("flat_load" in w for w in window), "\n".join(window)
+            assert any("global_load_dword" in w and "sc1" in w for w in window), "\n".join(window)
     assert polls > 0
