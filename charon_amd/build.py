@@ -30,6 +30,7 @@ def build(force=False, verbose=True, extra=(), out=LIB):
     cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-I" + CSRC, "-I" + os.path.join(ROOT, "include"),
            "-o", out + ".tmp", os.path.join(CSRC, "hipbls.hip"), os.path.join(CSRC, "verify_lat.hip"),
+           os.path.join(CSRC, "verify_hex.hip"),
            "-L/opt/rocm/lib", "-lhsa-runtime64"] + list(extra)
     if verbose:
         print("[hipbls] " + " ".join(cmd), flush=True)

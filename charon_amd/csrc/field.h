@@ -287,6 +287,11 @@ __device__ __forceinline__ uint32_t fp2p_xchg(uint32_t v) {
   const int a = __builtin_amdgcn_update_dpp((int)v, (int)v, 0x104, 0xF, 0x5, false);
   return (uint32_t)__builtin_amdgcn_update_dpp(a, (int)v, 0x114, 0xF, 0xA, false);
 }
+__device__ __forceinline__ uint32_t fp2p_bfi(uint32_t m, uint32_t a, uint32_t b) {  // m ? a : b (v_bfi_b32, gcd30::bfi)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
 #endif
 #define BLS_ASM_CALL(fn)                                                                           \
   "s_getpc_b64 s[16:17]\n\ts_add_u32 s16, s16, " fn "@rel32@lo+4\n\ts_addc_u32 s17, s17, " fn \
@@ -379,7 +384,52 @@ BLS_HD BLS_INLINE void fp_sqr(fp& r, const fp& a) { r = fp_sqr_v(a); }
 #ifndef BLS_POW_W
 #define BLS_POW_W 5
 #endif
+#if BLS_FP2_PAIR && defined(__HIP_DEVICE_COMPILE__)
+// The split-Fp2 build: right to left over the twin lanes.  Both lanes carry s = a^(2^i) and square it together while
+// bit i is clear; at a set bit lane l (c0 side) squares while its twin l ^ 4 multiplies the accumulator by the same
+// s, and one exchange gives the twin the new s.  One product of latency per exponent bit (top_bit + 1) instead of the
+// window form's ~top_bit squarings + ~80 products on one lane, with the exchange only at set bits.  The accumulator
+// lives on the c1 side and is exchanged once at the end.  All eight lanes of a group must be active (the twin
+// products of this build require the same).
+__device__ __forceinline__ void fp_pow_twin(fp& r, const fp& a, const uint32_t* e, int top_bit) {
+  const uint32_t mul_lane = fp2p_mask();
+  fp s = a, acc;
+  bool started = false;
+#pragma unroll 1
+  for (int i = 0; i <= top_bit; ++i) {
+#ifdef BLS_RACE_POLL
+    if ((i & 63) == 63) BLS_RACE_POLL();
+#endif
+    const bool set = (e[i >> 5] >> (i & 31)) & 1u;  // wave-uniform
+    if (set && started) {
+      fp x, p, o;
+#pragma unroll
+      for (int k = 0; k < 12; ++k) x.v[k] = fp2p_bfi(mul_lane, acc.v[k], s.v[k]);
+      fp_mul(p, x, s);  // c0 side: s^2 | c1 side: acc s
+#pragma unroll
+      for (int k = 0; k < 12; ++k) o.v[k] = fp2p_xchg(p.v[k]);
+      acc = p;  // meaningful on the c1 side
+#pragma unroll
+      for (int k = 0; k < 12; ++k) s.v[k] = fp2p_bfi(mul_lane, o.v[k], p.v[k]);
+    } else {
+      if (set) {
+        acc = s;
+        started = true;
+      }
+      fp t;
+      fp_mul(t, s, s);
+      s = t;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 12; ++k) r.v[k] = fp2p_bfi(mul_lane, acc.v[k], fp2p_xchg(acc.v[k]));
+}
+#endif
 BLS_HD BLS_CALL void fp_pow(fp& r, const fp& a, const uint32_t* e, int top_bit) {
+#if BLS_FP2_PAIR && defined(__HIP_DEVICE_COMPILE__)
+  fp_pow_twin(r, a, e, top_bit);
+  return;
+#endif
   constexpr int W = BLS_POW_W;
   fp tbl[1 << (W - 1)];
   fp a2;

@@ -148,8 +148,87 @@ BLS_HD BLS_CALL void sha256_segs(uint32_t out[8], const byte_segs& m) {
   for (int i = 0; i < 8; ++i) out[i] = s.h[i];
 }
 
+BLS_HD BLS_INLINE uint32_t be32(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return (a << 24) | (b << 16) | (c << 8) | d;
+}
+
+// expand_message_xmd_256 for a 32-byte message (a signing root) and a 43-byte DST (the POP suite's): every byte's
+// block and position is a compile-time constant, so the blocks are assembled as words in registers.  msg_prime is
+// 143 bytes (Z_pad, msg, 0x01 0x00 0x00, DST, 43): three blocks, the first all zero; each b_i message is 77 bytes
+// ((b_0 ^ b_(i-1)), i, DST, 43): two blocks.  18 compressions from words, no byte arrays (the general form below
+// assembles every block byte by byte from segment lists in scratch: 266 -> <60 us at the n = 1 placement,
+// charon_amd/tools/lat_parts_probe.hip).  Same output as the general form (tests/test_host_arith.py).
+BLS_HD BLS_CALL void expand_message_xmd_256_m32_d43(uint32_t out[64], const uint8_t* msg, const uint8_t* dst) {
+  uint32_t D[44];
+#pragma unroll
+  for (int i = 0; i < 43; ++i) D[i] = dst[i];
+  D[43] = 43;
+  uint32_t mw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mw[i] = be32(msg[4 * i], msg[4 * i + 1], msg[4 * i + 2], msg[4 * i + 3]);
+  uint32_t w[16];
+  sha256_state s;
+  sha256_init(s);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = 0;
+  sha256_compress(s, w);  // Z_pad
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = mw[i];
+  w[8] = be32(0x01, 0x00, 0x00, D[0]);
+#pragma unroll
+  for (int i = 9; i < 16; ++i) w[i] = be32(D[4 * i - 35], D[4 * i - 34], D[4 * i - 33], D[4 * i - 32]);  // D[1..28]
+  sha256_compress(s, w);
+  w[0] = be32(D[29], D[30], D[31], D[32]);
+  w[1] = be32(D[33], D[34], D[35], D[36]);
+  w[2] = be32(D[37], D[38], D[39], D[40]);
+  w[3] = be32(D[41], D[42], D[43], 0x80);
+#pragma unroll
+  for (int i = 4; i < 15; ++i) w[i] = 0;
+  w[15] = 143 * 8;
+  sha256_compress(s, w);
+  uint32_t b0[8], prev[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    b0[i] = s.h[i];
+    prev[i] = 0;
+  }
+  // the b_i messages' DST words: block 1 ends with D[0..30] after (x, i); block 2 holds D[31..43] and the padding
+  uint32_t t1[7], t2[4];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) t1[i] = be32(D[4 * i + 3], D[4 * i + 4], D[4 * i + 5], D[4 * i + 6]);  // D[3..30]
+  t2[0] = be32(D[31], D[32], D[33], D[34]);
+  t2[1] = be32(D[35], D[36], D[37], D[38]);
+  t2[2] = be32(D[39], D[40], D[41], D[42]);
+  t2[3] = be32(D[43], 0x80, 0, 0);
+#pragma unroll 1
+  for (int idx = 1; idx <= 8; ++idx) {
+    sha256_init(s);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = b0[i] ^ prev[i];
+    w[8] = be32((uint32_t)idx, D[0], D[1], D[2]);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) w[9 + i] = t1[i];
+    sha256_compress(s, w);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = t2[i];
+#pragma unroll
+    for (int i = 4; i < 15; ++i) w[i] = 0;
+    w[15] = 77 * 8;
+    sha256_compress(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      prev[i] = s.h[i];
+      out[(idx - 1) * 8 + i] = s.h[i];
+    }
+  }
+}
+
 BLS_HD BLS_CALL void expand_message_xmd_256(uint32_t out[64], const uint8_t* msg, uint32_t msg_len,
                                                 const uint8_t* dst, uint32_t dst_len) {
+  if (msg_len == 32 && dst_len == 43) {
+    expand_message_xmd_256_m32_d43(out, msg, dst);
+    return;
+  }
   // msg_prime = Z_pad(64) || msg || I2OSP(256, 2) || I2OSP(0, 1) || DST || I2OSP(len(DST), 1)
   uint8_t mid[3] = {0x01, 0x00, 0x00};  // l_i_b_str = 0x0100, then 0x00
   uint8_t dst_tail[1] = {(uint8_t)dst_len};

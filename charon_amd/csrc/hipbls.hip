@@ -57,6 +57,13 @@ __global__ void k_rlcb_final8(const uint32_t* Ftot, const uint32_t* Fs, int32_t*
 __global__ void k_g1m_miller8(uint64_t nl_max, const uint32_t* meta, const uint32_t* lmsg, const uint32_t* Wv,
                               const uint32_t* H, uint64_t hstride, const uint32_t* hslot, uint32_t* F, uint64_t col0,
                               uint64_t fstride);
+}  // namespace bls_fp2p
+// The sixteen-lane check for batches of at most four items (verify_hex.hip: BLS_FP2_PAIR + BLS_HEX, namespace bls_hex).
+namespace bls_hex {
+__global__ void k_verify_pair_lq16(const uint32_t* ws, uint64_t n, int32_t* status, uint32_t replicas, uint32_t* race,
+                                   uint32_t epoch);
+}  // namespace bls_hex
+namespace bls_fp2p {
 // LDS the S-factor workgroup reserves at launch and never touches: the chunk kernel's 36 KiB per workgroup (four per
 // CU), so a CU that hosts the S-factor wave takes at most three chunk waves and no SIMD runs two (a shared SIMD
 // stretched the 1,023-wave chunk kernel by the S factor's run time: 34.9 -> 40.5 ms).
@@ -307,6 +314,7 @@ struct KernelRef {
 };
 #define KREF(k) {#k, reinterpret_cast<const void*>(&k)}
 #define KREF8(k) {#k, reinterpret_cast<const void*>(&bls_fp2p::k)}
+#define KREF16(k) {#k, reinterpret_cast<const void*>(&bls_hex::k)}
 // Every kernel the library launches (tests/test_kernel_resources.py: the same set as both code objects hold, minus the
 // reserve kernels).
 const KernelRef kKernels[] = {
@@ -322,6 +330,7 @@ const KernelRef kKernels[] = {
     KREF(k_verify_fused), KREF(k_verify_keys), KREF(k_verify_pair_lg2), KREF(k_verify_pair_lq4),
     KREF(k_verify_pair_single), KREF(k_verify_prep), KREF(k_zero_sig_status), KREF8(k_g1m_miller8),
     KREF8(k_rlcb_final8), KREF8(k_rlcb_sfactor8), KREF8(k_verify_pair_lq8), KREF8(k_verify_prep8),
+    KREF16(k_verify_pair_lq16),
 };
 #define RES(s) reinterpret_cast<const void*>(&k_scratch_reserve<s>)
 // 8 KiB to the per-lane budget (charon_amd/codeobj.py PRIVATE_SEGMENT_BUDGET, 13,104 B) in 256-byte steps: at most
@@ -844,6 +853,15 @@ bool use_quads(uint64_t n) {
   if (mode == HIPBLS_PAIR_QUADS || mode == HIPBLS_PAIR_OCTETS) return true;
   return mode == HIPBLS_PAIR_AUTO && n <= kLq4MaxVerify;
 }
+// The octet path's check on sixteen lanes per item (verify_hex.hip) for batches of at most four items: AUTO only (the
+// forced OCTETS mode keeps eight lanes, so the layout-parity tests compare the two), HIPBLS_LAT_HEX=0 turns it off.
+constexpr uint64_t kLq16MaxVerify = 4;
+bool initial_lat_hex() {
+  const char* e = getenv("HIPBLS_LAT_HEX");
+  return !(e && e[0] == '0');
+}
+const bool g_lat_hex = initial_lat_hex();
+bool use_hex(uint64_t n) { return g_lat_hex && g_pair_mode.load() == HIPBLS_PAIR_AUTO && n <= kLq16MaxVerify; }
 // Verify only (the drop-in latency path, verify_lat.hip); sigagg's check and the RLC stages keep quads / pairs.
 bool use_octets(uint64_t n) {
   const int mode = g_pair_mode.load();
@@ -883,13 +901,17 @@ int launch_verify(Context& c, const uint8_t* d_pks, const uint8_t* d_msgs, const
                          d_sigs, n, (uint32_t*)ws.p, d_status, reps, race, epoch);
     });
     if (rc) return rc;
-    return timed(c, "verify_pair_lq8", s, [&] {
+    return timed(c, use_hex(n) ? "verify_pair_lq16" : "verify_pair_lq8", s, [&] {
 #if defined(BLS_LQ8_XCD_PROBE) && BLS_LQ8_XCD_PROBE
       hipLaunchKernelGGL(bls_fp2p::k_verify_pair_lq8, dim3(8 * g8), dim3(kBlock), 0, s, (const uint32_t*)ws.p, n,
                          d_status, 1u, race, 0u);  // experiment build: every workgroup once per XCD (verify_lat.hip)
 #else
-      hipLaunchKernelGGL(bls_fp2p::k_verify_pair_lq8, dim3(g8 * reps), dim3(kBlock), 0, s, (const uint32_t*)ws.p, n,
-                         d_status, reps, race, epoch);
+      if (use_hex(n))  // n <= 4: one workgroup of sixteen lanes per item, like g8 == 1
+        hipLaunchKernelGGL(bls_hex::k_verify_pair_lq16, dim3(g8 * reps), dim3(kBlock), 0, s, (const uint32_t*)ws.p, n,
+                           d_status, reps, race, epoch);
+      else
+        hipLaunchKernelGGL(bls_fp2p::k_verify_pair_lq8, dim3(g8 * reps), dim3(kBlock), 0, s, (const uint32_t*)ws.p, n,
+                           d_status, reps, race, epoch);
 #endif
     });
   }

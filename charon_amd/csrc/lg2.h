@@ -22,6 +22,10 @@
 #pragma once
 #include "rlc.h"
 
+#ifndef BLS_HEX
+#define BLS_HEX 0
+#endif
+
 namespace bls {
 
 #if defined(__HIPCC__)
@@ -65,6 +69,69 @@ __device__ __forceinline__ fp6 sel(uint32_t m, const fp6& if_odd, const fp6& if_
   sel_words<72>(&r.c0.c0.v[0], m, &if_odd.c0.c0.v[0], &if_even.c0.c0.v[0]);
   return r;
 }
+
+// ---------------------------------------------------------------- sixteen lanes per item (verify_hex.hip, BLS_HEX)
+// The split-Fp2 build run on sixteen lanes per item: lanes 0-7 and 8-15 of each group hold the same octet state and
+// run the same code; the Fp6 products and the compressed squarings' Fp2 squarings are dealt out over the two halves
+// (lane ^ 8, one DPP row_ror:8 per dword).  Every other step runs redundantly on both halves.  All sixteen lanes must
+// be active.
+#if BLS_HEX
+__device__ __forceinline__ uint32_t hx_mask() {  // ~0 on lanes 8-15 of each group of sixteen
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  return (lane & 8u) ? ~0u : 0u;
+}
+__device__ __forceinline__ uint32_t hx_xchg(uint32_t v) {  // lane ^ 8 within the row of sixteen
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128 /* row_ror:8 */, 0xF, 0xF, false);
+#else
+  return v;
+#endif
+}
+__device__ __forceinline__ fp2 hx_xchg(const fp2& s) {
+  fp2 d;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) (&d.c0.v[0])[i] = hx_xchg((&s.c0.v[0])[i]);
+  return d;
+}
+// tower.h fp6_mul (Karatsuba, six Fp2 products) with the products dealt out: the low half forms a0 b0, a1 b1, a2 b2,
+// the high half (a1 + a2)(b1 + b2), (a0 + a1)(b0 + b1), (a0 + a2)(b0 + b2); one exchange, then both halves combine
+// them as fp6_mul does.  Three products of latency instead of six; the same canonical result.
+__device__ __forceinline__ void fp6_mul_hx(fp6& r, const fp6& a_in, const fp6& b_in) {
+  const fp6 a = a_in, b = b_in;
+  const uint32_t h = hx_mask();
+  fp2 s0, s1, p0, p1, p2;
+  fp2_add_lazy(s0, a.c1, a.c2);
+  fp2_add_lazy(s1, b.c1, b.c2);
+  fp2_mul(p0, sel(h, s0, a.c0), sel(h, s1, b.c0));
+  fp2_add_lazy(s0, a.c0, a.c1);
+  fp2_add_lazy(s1, b.c0, b.c1);
+  fp2_mul(p1, sel(h, s0, a.c1), sel(h, s1, b.c1));
+  fp2_add_lazy(s0, a.c0, a.c2);
+  fp2_add_lazy(s1, b.c0, b.c2);
+  fp2_mul(p2, sel(h, s0, a.c2), sel(h, s1, b.c2));
+  const fp2 o0 = hx_xchg(p0), o1 = hx_xchg(p1), o2 = hx_xchg(p2);
+  const fp2 t0 = sel(h, o0, p0), t1 = sel(h, o1, p1), t2 = sel(h, o2, p2);
+  const fp2 m12 = sel(h, p0, o0), m01 = sel(h, p1, o1), m02 = sel(h, p2, o2);
+  fp2 u0, u1, u2, x2;
+  fp2_sub(u0, m12, t1);
+  fp2_sub(u0, u0, t2);
+  fp2_mul_xi(u0, u0);
+  fp2_add(u0, u0, t0);
+  fp2_sub(u1, m01, t0);
+  fp2_sub(u1, u1, t1);
+  fp2_mul_xi(x2, t2);
+  fp2_add(u1, u1, x2);
+  fp2_sub(u2, m02, t0);
+  fp2_sub(u2, u2, t2);
+  fp2_add(u2, u2, t1);
+  r.c0 = u0;
+  r.c1 = u1;
+  r.c2 = u2;
+}
+#define LG2_FP6_MUL fp6_mul_hx
+#else
+#define LG2_FP6_MUL fp6_mul
+#endif
 
 // ---------------------------------------------------------------- split Fp12 (own half h)
 // Own half of the product of two FULL Fp12 values a, b (both known to the lane): even lane c0 = a0 b0 + v a1 b1,
@@ -449,7 +516,7 @@ __device__ __forceinline__ void fp12h_sqr_split(fp6& h, uint32_t m) {
   fp6_add(s1, a, vb);
   const fp6 x = sel(m, a, s0), y = sel(m, b, s1);  // odd: a b | even: (a + b)(a + v b)
   fp6 p;
-  fp6_mul(p, x, y);
+  LG2_FP6_MUL(p, x, y);
   fp6 t;
   pair_swap(t, p);  // even receives t = a b
   fp6 vt, c0, c1;
@@ -615,7 +682,7 @@ BLS_FP12Q_MUL_ATTR __device__ void fp12q_mul(fp12& r, const fp12& a_in, const fp
   const fp6 x = sel(qm.odd, a.c1, a.c0);    // a0 | a1 | a0 | a1
   const fp6 y = sel(qm.cross, b.c1, b.c0);  // b0 | b1 | b1 | b0
   fp6 p, o, vp, vo, t0, t1, t2;
-  fp6_mul(p, x, y);
+  LG2_FP6_MUL(p, x, y);
   pair_swap(o, p);
   fp6_mul_v(vp, p);
   fp6_mul_v(vo, o);
@@ -653,8 +720,20 @@ __device__ __forceinline__ void cyc_sqr_compressed_quad(cyc_c& c, const quad_m& 
   fp2_add(s45, c.z4, c.z5);
   const fp2 xb = sel(qm.odd, s45, s23);
   fp2 ra, rb;
+#if BLS_HEX
+  // both rounds at once: the low half squares xa, the high half xb; one exchange gives each half the other's
+  {
+    const uint32_t h = hx_mask();
+    fp2 r;
+    BLS_KAR_FP2_SQR(r, sel(h, xb, xa));
+    const fp2 o = hx_xchg(r);
+    ra = sel(h, o, r);
+    rb = sel(h, r, o);
+  }
+#else
   BLS_KAR_FP2_SQR(ra, xa);
   BLS_KAR_FP2_SQR(rb, xb);
+#endif
   const fp2 X = quad_perm<0x0A>(ra);  // [2, 2, 0, 0]: z4^2 | z4^2 | z2^2 | z2^2
   const fp2 Y = quad_perm<0x5F>(ra);  // [3, 3, 1, 1]: z5^2 | z5^2 | z3^2 | z3^2
   const fp2 W = quad_perm<0x05>(rb);  // [1, 1, 0, 0]: (z4 + z5)^2 on lane 0, (z2 + z3)^2 on lane 3
@@ -730,6 +809,7 @@ BLS_CALL __device__ bool fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, cons
   if (fp2_is_zero(pre[5])) return true;  // the same on all four lanes
   fp2 inv;
   fp2_inv(inv, pre[5]);
+  BLS_RACE_POLL();
   fp2 is[6];  // 1 / den[s] by back-substitution
 #pragma unroll
   for (s = 5; s > 0; --s) {
@@ -756,6 +836,7 @@ BLS_CALL __device__ bool fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, cons
     fp12 x = acc;
     fp12q_mul(acc, x, d, qm);
   }
+  BLS_RACE_POLL();
   quad_bcast12<2>(d, xA);
   {
     fp12 x = acc;
@@ -766,6 +847,7 @@ BLS_CALL __device__ bool fp12q_exp_xabs_karabina(fp12& r, const fp12& a_in, cons
     fp12 x = acc;
     fp12q_mul(acc, x, d, qm);
   }
+  BLS_RACE_POLL();
   quad_bcast12<0>(d, xA);
   {
     fp12 x = acc;
@@ -805,6 +887,7 @@ BLS_CALL __device__ void final_exponentiation_quad(fp12& r, const fp12& f_in, co
     fp12_frobenius(t1, t0, 1);
     fp12q_mul(t1, t1, u, qm);
   }
+  BLS_RACE_POLL();
   fp12 t2;
   {
     fp12 u;
@@ -815,6 +898,7 @@ BLS_CALL __device__ void final_exponentiation_quad(fp12& r, const fp12& f_in, co
     fp12_conj(u, t1);
     fp12q_mul(t2, t2, u, qm);
   }
+  BLS_RACE_POLL();
   {
     fp12 u;
     fp12_cyclotomic_sqr(u, m);

@@ -16,55 +16,7 @@
 #define bls bls_fp2p
 #include <hip/hip_runtime.h>
 
-// ---------------------------------------------------------------- replica races (the n = 1 drop-in path)
-// The octet check of one item takes 7.2 to 9.8 ms depending on where its single wave runs: eight copies of the same
-// work in one launch, one per XCD, finished 7.2-9.8 ms apart with no XCD consistently fast
-// (profiles/r05/r05_xcd_lq8.txt).  So a batch of at most 8 items runs as `replicas` copies of its workgroups; every
-// copy computes the same result, polls its race word at coarse steps (BLS_RACE_POLL in lg2.h and below), and the
-// first to finish sets the word to this launch's epoch, which ends the others.  The word lives in LDS per workgroup
-// (nullptr: not raced); EVERY kernel of this translation unit sets it at entry, since LDS is not zero-initialized.
-namespace bls_race {
-__shared__ uint32_t* s_word;
-__shared__ uint32_t s_epoch;
-__device__ __forceinline__ void init(uint32_t* word, uint32_t epoch) {
-  s_word = word;
-  s_epoch = epoch;
-}
-__device__ __forceinline__ uint32_t* word_u() {  // wave-uniform copy of the LDS pointer; nullptr unless 4-aligned
-  const uint64_t w = (uint64_t)s_word;
-  // readfirstlane returns int: each half goes through uint32_t, or a low half with bit 31 set (half of all buffer
-  // addresses) sign-extends over the high half -- round 5's first race build read a wild address (an illegal access in
-  // one run, a hung queue worker in the next)
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)w);
-  const uint64_t u = ((uint64_t)hi << 32) | lo;
-  return (u & 3) ? nullptr : (uint32_t*)u;  // the words are race[0..3]: the launch checks race's 64-B alignment
-}
-// The word is written by a wave on another XCD: the poll is a `global_load_dword ... sc1` (past this CU's L1, served
-// coherently across the XCDs' L2s) and the winner's store a write-through `global_store_dword ... sc1`
-// (MI355X_MICROARCH.md, inter-workgroup visibility: flag polls by global/buffer sc1 loads, never flat; the generic
-// pointer made __hip_atomic_load/store flat_ forms).  The second race build also asked each word for 64-byte alignment,
-// which only race[0] has: no polled stage was raced, and every raced kernel took as long as its slowest copy
-// (profiles/r05/race_trace_flat.json).
-__device__ __forceinline__ void poll() {
-  uint32_t* w = word_u();
-  if (!w) return;
-  uint32_t v;
-  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(w) : "memory");
-  if ((uint32_t)__builtin_amdgcn_readfirstlane(v) == (uint32_t)__builtin_amdgcn_readfirstlane(s_epoch))
-    asm volatile("s_endpgm");
-}
-// After this copy's results are stored: the race is won (the other copies end at their next poll).
-__device__ __forceinline__ void finish() {
-  uint32_t* w = word_u();
-  if (w && threadIdx.x == 0) {
-    const uint32_t e = s_epoch;
-    asm volatile("s_waitcnt vmcnt(0)\n\tglobal_store_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : : "v"(w), "v"(e)
-                 : "memory");
-  }
-}
-}  // namespace bls_race
-#define BLS_RACE_POLL() ::bls_race::poll()
+#include "race.h"
 
 #include "lg2.h"
 #include "rlcb.h"
@@ -108,42 +60,111 @@ __device__ __forceinline__ void g2_dbl_quad(g2j& r, const g2j& p, int q) {
   r.x = x3;
 }
 
-// [|x|] p with the doublings on the quad (the additions, at |x|'s six set bits, on every lane)
+// G2 addition (curve.h jac_add_body, add-2007-bl: 11 products + 5 squarings) dealt out over the quad in five levels
+// of one product per lane, each level broadcast to the quad:
+//   1: Z1^2 | Z2^2 | Y1 Z2 | Y2 Z1          2: U1 = X1 Z2^2 | U2 = X2 Z1^2 | S1 = Y1 Z2^3 | S2 = Y2 Z1^3
+//   3: I = (2H)^2 | R^2 | (Z1 + Z2)^2        4: J = H I | V = U1 I | Z3 = ((Z1 + Z2)^2 - Z1^2 - Z2^2) H
+//   5: R (V - X3) | S1 J
+// Five products of latency instead of sixteen; squarings as products of equal operands (the same canonical values).
+// The exceptional cases (an input at infinity, H = 0) take jac_add on every lane: the values are the same on all
+// four lanes, so those branches are quad-uniform.  All four lanes (and their Fp2 twins) must be active.
+__device__ __forceinline__ void g2_add_quad(g2j& r, const g2j& p, const g2j& qp, int q) {
+  if (jac_is_inf(p) || jac_is_inf(qp)) {
+    jac_add(r, p, qp);
+    return;
+  }
+  const uint32_t q1 = q == 1 ? ~0u : 0u, q2 = q == 2 ? ~0u : 0u, q3 = q == 3 ? ~0u : 0u;
+  fp2 x, y, o;
+  x = sel(q3, qp.y, sel(q2, p.y, sel(q1, qp.z, p.z)));
+  y = sel(q3, p.z, sel(q2, qp.z, sel(q1, qp.z, p.z)));
+  fp2_mul(o, x, y);
+  const fp2 z1z1 = quad_bcast<0>(o), z2z2 = quad_bcast<1>(o), s1a = quad_bcast<2>(o), s2a = quad_bcast<3>(o);
+  x = sel(q3, s2a, sel(q2, s1a, sel(q1, qp.x, p.x)));
+  y = sel(q3, z1z1, sel(q2, z2z2, sel(q1, z1z1, z2z2)));
+  fp2_mul(o, x, y);
+  const fp2 u1 = quad_bcast<0>(o), u2 = quad_bcast<1>(o), s1 = quad_bcast<2>(o), s2 = quad_bcast<3>(o);
+  fp2 h, rr;
+  fp2_sub(h, u2, u1);
+  fp2_sub(rr, s2, s1);
+  if (fp2_is_zero(h)) {  // the same on all four lanes
+    if (fp2_is_zero(rr))
+      jac_dbl(r, p);
+    else
+      jac_set_inf(r);
+    return;
+  }
+  fp2_add(rr, rr, rr);
+  fp2 h2, zs;
+  fp2_add(h2, h, h);
+  fp2_add(zs, p.z, qp.z);
+  x = sel(q2, zs, sel(q1, rr, h2));
+  fp2_mul(o, x, x);
+  const fp2 i = quad_bcast<0>(o), r2 = quad_bcast<1>(o), zz = quad_bcast<2>(o);
+  fp2 zc;
+  fp2_sub(zc, zz, z1z1);
+  fp2_sub(zc, zc, z2z2);
+  x = sel(q2, zc, sel(q1, u1, h));
+  y = sel(q2, h, i);
+  fp2_mul(o, x, y);
+  const fp2 j = quad_bcast<0>(o), v = quad_bcast<1>(o), z3 = quad_bcast<2>(o);
+  fp2 x3, t;
+  fp2_sub(x3, r2, j);
+  fp2_sub(x3, x3, v);
+  fp2_sub(x3, x3, v);
+  fp2_sub(t, v, x3);
+  x = sel(q1, s1, rr);
+  y = sel(q1, j, t);
+  fp2_mul(o, x, y);
+  const fp2 y3a = quad_bcast<0>(o), s1j = quad_bcast<1>(o);
+  fp2 y3, s1j2;
+  fp2_add(s1j2, s1j, s1j);
+  fp2_sub(y3, y3a, s1j2);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;
+}
+
+// [|x|] p with the doublings and the additions (at |x|'s five set bits below the top) on the quad
 __device__ void g2_mul_xabs_quad(g2j& r, const g2j& p_in, int q) {
   const g2j p = p_in;
   g2j acc = p;
   for (int i = 62; i >= 0; --i) {
-    if ((i & 7) == 7) BLS_RACE_POLL();
+    if ((i & 3) == 3) BLS_RACE_POLL();
     g2j t;
     g2_dbl_quad(t, acc, q);
     acc = t;
     if ((X_ABS >> i) & 1ull) {
       g2j u = acc;
-      jac_add(acc, u, p);
+      g2_add_quad(acc, u, p, q);
     }
   }
   r = acc;
 }
 
-// curve.h g2_clear_cofactor (Budroni-Pintore) with its two [x] multiplications on the quad
+// curve.h g2_clear_cofactor (Budroni-Pintore) with its two [x] multiplications, its doubling and its additions on the
+// quad
 __device__ void g2_clear_cofactor_quad(g2j& r, const g2j& p_in, int q) {
   const g2j p = p_in;
-  g2j t1, t2, t3, np, nt1, nt2;
+  g2j t1, t2, t3, np, nt1, nt2, u;
   g2_mul_xabs_quad(t1, p, q);
   jac_neg(t1, t1);  // [x] P
   g2_psi(t2, p);
-  jac_dbl(t3, p);
+  g2_dbl_quad(t3, p, q);
   g2_psi2(t3, t3);
   jac_neg(nt2, t2);
-  jac_add(t3, t3, nt2);  // psi^2(2P) - psi(P)
-  jac_add(t2, t1, t2);   // [x] P + psi(P)
+  u = t3;
+  g2_add_quad(t3, u, nt2, q);  // psi^2(2P) - psi(P)
+  u = t2;
+  g2_add_quad(t2, t1, u, q);   // [x] P + psi(P)
   g2_mul_xabs_quad(t2, t2, q);
   jac_neg(t2, t2);
-  jac_add(t3, t3, t2);
+  u = t3;
+  g2_add_quad(t3, u, t2, q);
   jac_neg(nt1, t1);
-  jac_add(t3, t3, nt1);
+  u = t3;
+  g2_add_quad(t3, u, nt1, q);
   jac_neg(np, p);
-  jac_add(r, t3, np);
+  g2_add_quad(r, t3, np, q);
 }
 
 // Stage 1, eight lanes per item (t >> 3), three roles per set of workgroups (uniform per workgroup, so they run side
@@ -175,6 +196,7 @@ __global__ void __launch_bounds__(kOctBlock) k_verify_prep8(const uint8_t* __res
     g2j sum, hj;
     hash_to_g2_pair_sum(sum, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43, m);
     g2_clear_cofactor_quad(hj, sum, (int)(t & 3));
+    BLS_RACE_POLL();
     g2a hm;
     jac_to_aff(hm, hj);
     if (lead) soa_store<48>(ws + 24 * n, n, i, &hm.x.c0.v[0]);

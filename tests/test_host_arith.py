@@ -65,6 +65,15 @@ def test_expand_message(L):
     for msg in [b"", b"abc", b"a" * 200]:
         L.ht_expand_message(msg, len(msg), dst, len(dst), out)
         assert out.raw == bls.expand_message_xmd(msg, dst, 256)
+    # 32-byte messages with a 43-byte DST take the word-assembled form (h2c.h expand_message_xmd_256_m32_d43): the
+    # POP suite's DST and another 43-byte one (the DST bytes are read, not assumed)
+    rng = random.Random(11)
+    pop = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_POP_"
+    assert len(pop) == 43
+    for d in (pop, bytes(rng.randrange(256) for _ in range(43))):
+        for msg in [bytes(32), b"\xff" * 32] + [bytes(rng.randrange(256) for _ in range(32)) for _ in range(6)]:
+            L.ht_expand_message(msg, 32, d, 43, out)
+            assert out.raw == bls.expand_message_xmd(msg, d, 256)
 
 
 def test_map_to_curve(L):
