@@ -468,8 +468,8 @@ def main():
         latency = {"calls": k, "p50_ms": round(1000 * lat[k // 2], 3), "p90_ms": round(1000 * lat[(9 * k) // 10], 3),
                    "min_ms": round(1000 * lat[0], 3), "serial_verifies_per_s": round(k / tot, 1),
                    "seconds_per_1000_serial": round(1000 * tot / k, 2),
-                   "path": "hipbls_verify (submission queue, n = 1 batch: eight-lane prep + pairing check, "
-                           "verify_lat.hip; each stage raced by 8 replicas, one per XCD)"}
+                   "path": "hipbls_verify (submission queue, n = 1 batch: eight-lane prep (verify_lat.hip) + "
+                           "sixteen-lane pairing check (verify_hex.hip); each stage raced by 8 replicas, one per XCD)"}
         # the same calls without the replica race (hipbls_set_latency_replicas(1)), for comparison
         k1 = min(200, k)
         prev = lib.hipbls_set_latency_replicas(1)
