@@ -223,3 +223,31 @@ def test_raced_small_batches_across_workspace_growth(impl):
                     assert got == [want[i] for i in idx], (grow, reps, idx)
     finally:
         impl.lib.hipbls_set_latency_replicas(prev)
+
+
+def test_sixteen_lane_check_takes_small_batches(impl):
+    """AUTO runs batches of at most four items on the sixteen-lane check (verify_hex.hip), five to eight on the octet
+    check; the forced OCTETS mode keeps eight lanes.  Statuses agree everywhere (the layout-parity tests in
+    tests/test_gpu_lg2.py compare the modes on mixed batches and the fixtures)."""
+    import bench
+    from charon_amd.tbls import PAIR_AUTO, PAIR_OCTETS
+
+    def launches(name):
+        a, c = ctypes.c_double(), ctypes.c_uint64()
+        impl.lib.hipbls_kernel_timing(name, ctypes.byref(a), ctypes.byref(c))
+        return c.value
+
+    pks, roots, sigs, bad = bench.make_c2(impl, bench.share_keys(impl, 64, "c2hex"), 0, 64)
+    want = impl.batch_verify_status(pks, roots, sigs)
+    impl.lib.hipbls_set_timing(1)
+    try:
+        for mode, n, lq16, lq8 in ((PAIR_AUTO, 1, 1, 0), (PAIR_AUTO, 4, 1, 0), (PAIR_AUTO, 5, 0, 1),
+                                   (PAIR_OCTETS, 3, 0, 1)):
+            impl.set_pair_mode(mode)
+            b16, b8 = launches(b"verify_pair_lq16"), launches(b"verify_pair_lq8")
+            lo = 7 * n
+            assert impl.batch_verify_status(pks[lo:lo + n], roots[lo:lo + n], sigs[lo:lo + n]) == want[lo:lo + n]
+            assert (launches(b"verify_pair_lq16") - b16, launches(b"verify_pair_lq8") - b8) == (lq16, lq8), (mode, n)
+    finally:
+        impl.set_pair_mode(PAIR_AUTO)
+        impl.lib.hipbls_set_timing(0)
