@@ -457,6 +457,9 @@ def main():
         k = min(args.latency_calls, n)
         assert impl.verify_queued(pks[0], roots[0], sigs[0]) == st[0]  # starts the queue worker
         lat = []
+        w0, b0 = ctypes.c_uint64(), ctypes.c_uint64()
+        lib.hipbls_queue_worker_stats(ctypes.byref(w0), ctypes.byref(b0))
+        cpu0 = time.process_time()
         t0 = time.perf_counter()
         for j in range(k):
             a = time.perf_counter()
@@ -464,12 +467,19 @@ def main():
             lat.append(time.perf_counter() - a)
             assert got == st[j], "queued Verify differs from the batch call"
         tot = time.perf_counter() - t0
+        cpu = time.process_time() - cpu0
+        w1, b1 = ctypes.c_uint64(), ctypes.c_uint64()
+        lib.hipbls_queue_worker_stats(ctypes.byref(w1), ctypes.byref(b1))
         lat.sort()
         latency = {"calls": k, "p50_ms": round(1000 * lat[k // 2], 3), "p90_ms": round(1000 * lat[(9 * k) // 10], 3),
                    "min_ms": round(1000 * lat[0], 3), "serial_verifies_per_s": round(k / tot, 1),
                    "seconds_per_1000_serial": round(1000 * tot / k, 2),
                    "path": "hipbls_verify (submission queue, n = 1 batch: eight-lane prep (verify_lat.hip) + "
-                           "sixteen-lane pairing check (verify_hex.hip); each stage raced by 8 replicas, one per XCD)"}
+                           "sixteen-lane pairing check (verify_hex.hip); each stage raced by 8 replicas, one per XCD)",
+                   # the queue worker's completion polls per batch (CPU inside the charon process) and the
+                   # whole process's CPU time per call (the calling thread's ctypes round trip included)
+                   "worker_polls_per_batch": round((w1.value - w0.value) / max(1, b1.value - b0.value), 1),
+                   "process_cpu_ms_per_call": round(1000 * cpu / k, 3)}
         # the same calls without the replica race (hipbls_set_latency_replicas(1)), for comparison
         k1 = min(200, k)
         prev = lib.hipbls_set_latency_replicas(1)

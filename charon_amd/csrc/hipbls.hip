@@ -153,6 +153,11 @@ struct VerifyQueue {
   uint64_t batches = 0, items = 0, keyed = 0, overlapped = 0;
   uint64_t wakeups = 0;   // completion polls of the worker (hipbls_queue_worker_stats)
   double batch_us[26] = {};  // running estimate of a wire batch's launch-to-completion time, per log2(batch size)
+  // running mean of the items per launched batch: below 1.5 the callers are serial (each waits for its own result
+  // before the next call), so an idle worker launches at once instead of waiting gather_us for company that cannot
+  // come; concurrent callers raise it (items that arrive while a batch runs coalesce into the next one) and turn the
+  // gather window back on
+  double batch_mean = 2.0;
   hipStream_t stream = nullptr;  // the keyed path's stream
   QSlot slot[kSlots];
   std::deque<int> inflight;  // slots in launch order
@@ -1747,8 +1752,9 @@ int rlc_range(Context& c, const uint8_t* pks, const uint32_t* key_idx, const uin
 // partials or by a committee is hashed once, and once across batches while it stays cached.  Statuses are exactly
 // the per-item Verify's (rlc.h).  Batches with a key outside the table take the wire-format Verify.
 std::atomic<uint64_t> g_q_max_batch{65536};
-// 50 us: a lone synchronous call (the parsigex loop) pays at most this before its launch; callers arriving while a
-// batch runs coalesce into the next one regardless (two batches in flight).
+// 50 us: what an idle worker waits for company before launching a small batch; callers arriving while a batch runs
+// coalesce into the next one regardless (two batches in flight).  Serial callers (the parsigex loop: a running mean
+// below 1.5 items per batch, VerifyQueue::batch_mean) skip it.
 std::atomic<uint32_t> g_q_gather_us{50};
 constexpr uint64_t kQueueKeyedMin = 8;  // without the H(m) cache, batches below this take the lane-pair Verify
 
@@ -1903,13 +1909,14 @@ void queue_worker(Context* cp) {
     if (pending && (int)q.inflight.size() < VerifyQueue::kSlots) {
       const uint64_t max_batch = g_q_max_batch.load();
       const uint32_t gather_us = g_q_gather_us.load();
-      if (q.inflight.empty() && gather_us && q.open.front()->n() < max_batch && !q.stop) {
+      if (q.inflight.empty() && gather_us && q.open.front()->n() < max_batch && !q.stop && q.batch_mean >= 1.5) {
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(gather_us);
         q.cv_work.wait_until(lk, until, [&] { return q.stop || q.open.front()->n() >= max_batch; });
       }
       std::shared_ptr<VBatch> b = q.open.front();
       q.open.pop_front();
       q.items += b->n();
+      q.batch_mean = 0.75 * q.batch_mean + 0.25 * (double)b->n();
       lk.unlock();
       b->status.assign(b->n(), HIPBLS_ERR_DEVICE);
       int rc = HIPBLS_ERR_DEVICE;

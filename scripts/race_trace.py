@@ -1,6 +1,6 @@
 """n = 1 Verify with the replica race off (1) and on (8), in alternating blocks of direct batch calls: host-side p50
 per block, and (under rocprofv3 --kernel-trace) the octet kernels' durations per block, in launch order.
-Usage: python scripts/race_trace.py [calls_per_block] > out.json"""
+Usage: python scripts/race_trace.py [calls_per_block] [replicas per block, e.g. 1,8,1,8,2,4] > out.json"""
 import json
 import statistics
 import sys
@@ -16,7 +16,8 @@ good = [i for i in range(64) if i not in bad]
 for i in good[:8]:
     assert impl.batch_verify_status([pks[i]], [roots[i]], [sigs[i]]) == [0]
 out = []
-for b, reps in enumerate((1, 8, 1, 8, 2, 4)):
+BLOCKS = tuple(int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,8,1,8,2,4").split(","))
+for b, reps in enumerate(BLOCKS):
     impl.lib.hipbls_set_latency_replicas(reps)
     ts = []
     for k in range(K):
