@@ -27,14 +27,33 @@ def build(force=False, verbose=True, extra=(), out=LIB):
     measurements (loaded with HIPBLS_LIB=<path>); the product is the default in-tree build."""
     if not force and out == LIB and not stale():
         return LIB
-    cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I" + CSRC, "-I" + os.path.join(ROOT, "include"),
-           "-o", out + ".tmp", os.path.join(CSRC, "hipbls.hip"), os.path.join(CSRC, "verify_lat.hip"),
-           os.path.join(CSRC, "verify_hex.hip"),
-           "-L/opt/rocm/lib", "-lhsa-runtime64"] + list(extra)
+    # the three translation units compile in parallel (each a separate code object; the link combines them), then link
+    srcs = [os.path.join(CSRC, f) for f in ("hipbls.hip", "verify_lat.hip", "verify_hex.hip")]
+    flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I" + CSRC, "-I" + os.path.join(ROOT, "include")]
+    flags += list(extra)
+    objs = [out + "." + os.path.splitext(os.path.basename(src))[0] + ".o" for src in srcs]
+    procs = []
+    for src, obj in zip(srcs, objs):
+        cmd = ["hipcc"] + flags + ["-c", "-o", obj, src]
+        if verbose:
+            print("[hipbls] " + " ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+    rcs = [p.wait() for p in procs]
+    if any(rcs):
+        for obj in objs:
+            if os.path.exists(obj):
+                os.remove(obj)
+        raise subprocess.CalledProcessError(max(rcs), "hipcc")
+    cmd = ["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out + ".tmp"] + objs + [
+        "-L/opt/rocm/lib", "-lhsa-runtime64"]
     if verbose:
         print("[hipbls] " + " ".join(cmd), flush=True)
-    subprocess.check_call(cmd)
+    try:
+        subprocess.check_call(cmd)
+    finally:
+        for obj in objs:
+            if os.path.exists(obj):
+                os.remove(obj)
     # scratch budget per lane (charon_amd/codeobj.py, DESIGN.md 5.1.1): a deeper kernel fails the build here instead of
     # exhausting the hardware queues' scratch under load (HSA_STATUS_ERROR_OUT_OF_RESOURCES aborts the process)
     from charon_amd import codeobj
