@@ -62,14 +62,20 @@ def _padded(impl, so, n_honest, seed):
     return [list(x) for x in zip(*items)]
 
 
-@pytest.mark.parametrize("mode", ["auto", "single", "lanes", "quads"])
+@pytest.mark.parametrize("mode", ["auto", "single", "lanes", "quads", "octets"])
 def test_small_order_batch_verify_every_layout(impl, so, mode):
-    from charon_amd.tbls import PAIR_AUTO, PAIR_LANES, PAIR_QUADS, PAIR_SINGLE
-    m = {"auto": PAIR_AUTO, "single": PAIR_SINGLE, "lanes": PAIR_LANES, "quads": PAIR_QUADS}[mode]
+    from charon_amd.tbls import PAIR_AUTO, PAIR_LANES, PAIR_OCTETS, PAIR_QUADS, PAIR_SINGLE
+    m = {"auto": PAIR_AUTO, "single": PAIR_SINGLE, "lanes": PAIR_LANES, "quads": PAIR_QUADS,
+         "octets": PAIR_OCTETS}[mode]
     pks, msgs, sigs, want = _cases(so)
     prev = impl.set_pair_mode(m)
     try:
         assert impl.batch_verify_status(pks, msgs, sigs) == want
+        if mode in ("auto", "octets"):
+            # one case per call: AUTO takes the sixteen-lane check (verify_hex.hip) at n <= 4, OCTETS the octet one,
+            # both raced by replicas
+            for p, msg, s, w in zip(pks, msgs, sigs, want):
+                assert impl.batch_verify_status([p], [msg], [s]) == [w]
         # the same cases at odd positions of a larger batch (pairs straddling wave edges)
         P, M, S, W = _padded(impl, so, 200, 1)
         assert impl.batch_verify_status(P, M, S) == W
