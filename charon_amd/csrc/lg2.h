@@ -911,6 +911,152 @@ BLS_CALL __device__ void final_exponentiation_quad(fp12& r, const fp12& f_in, co
 #define BLS_LQ4_FE_QUAD 1
 #endif
 
+// ---------------------------------------------------------------- one Miller accumulator for both pairs (round 5)
+// lq4_verify's two Miller loops share ONE accumulator held in full on the quad: f <- f^2 lA lB, where each pair's
+// doubling / addition step leaves its line on both of its lanes (miller_dbl_step_split, miller_add_step_inl) and one
+// exchange across the pairs gives every lane both lines.  Per bit: the two doubling steps side by side on the pairs
+// (as before), the Fp12 squaring as two Fp6 products with their Fp2 products split over a pair (fp12q_sqr), the
+// product of the two lines (eight Fp2 products in two slots over the quad) and one quad Fp12 product (fp12q_mul)
+// -- instead of each pair squaring its own split value and multiplying it by its own line.  f_A f_B is the same
+// element either way (the squarings distribute over the product), so the final exponentiation's input and every
+// status are unchanged.  BLS_LQ4_SHARED=0 builds the two split loops.  Measured (profiles/r05/lq4_shared_ab.json):
+// sigagg's quad check (the main translation unit) gains, C3 489k -> 501k aggregates/s with one call in flight and
+// 589k -> 606k on two streams; the split-Fp2 builds (octet and sixteen-lane n = 1 checks) lose (check 6.41 -> 6.57
+// ms: there the split loop's Fp12 squaring is already shared by the twin halves), so they keep the split loops.
+#ifndef BLS_LQ4_SHARED
+#if BLS_FP2_PAIR
+#define BLS_LQ4_SHARED 0
+#else
+#define BLS_LQ4_SHARED 1
+#endif
+#endif
+#if BLS_LQ4_SHARED
+// tower.h fp6_mul (Karatsuba) with its six Fp2 products dealt over a lane pair: the even lane forms a0 b0, a1 b1,
+// a2 b2, the odd lane (a1 + a2)(b1 + b2), (a0 + a1)(b0 + b1), (a0 + a2)(b0 + b2); one exchange; both combine them as
+// fp6_mul does.  Both lanes of the pair must be active and hold the same operands.
+__device__ __forceinline__ void fp6_mul_pair(fp6& r, const fp6& a_in, const fp6& b_in, uint32_t odd) {
+  const fp6 a = a_in, b = b_in;
+  fp2 s0, s1, p0, p1, p2;
+  fp2_add_lazy(s0, a.c1, a.c2);
+  fp2_add_lazy(s1, b.c1, b.c2);
+  fp2_mul(p0, sel(odd, s0, a.c0), sel(odd, s1, b.c0));
+  fp2_add_lazy(s0, a.c0, a.c1);
+  fp2_add_lazy(s1, b.c0, b.c1);
+  fp2_mul(p1, sel(odd, s0, a.c1), sel(odd, s1, b.c1));
+  fp2_add_lazy(s0, a.c0, a.c2);
+  fp2_add_lazy(s1, b.c0, b.c2);
+  fp2_mul(p2, sel(odd, s0, a.c2), sel(odd, s1, b.c2));
+  fp2 o0, o1, o2;
+  pair_swap(o0, p0);
+  pair_swap(o1, p1);
+  pair_swap(o2, p2);
+  const fp2 t0 = sel(odd, o0, p0), t1 = sel(odd, o1, p1), t2 = sel(odd, o2, p2);
+  const fp2 m12 = sel(odd, p0, o0), m01 = sel(odd, p1, o1), m02 = sel(odd, p2, o2);
+  fp2 u0, u1, u2, x2;
+  fp2_sub(u0, m12, t1);
+  fp2_sub(u0, u0, t2);
+  fp2_mul_xi(u0, u0);
+  fp2_add(u0, u0, t0);
+  fp2_sub(u1, m01, t0);
+  fp2_sub(u1, u1, t1);
+  fp2_mul_xi(x2, t2);
+  fp2_add(u1, u1, x2);
+  fp2_sub(u2, m02, t0);
+  fp2_sub(u2, u2, t2);
+  fp2_add(u2, u2, t1);
+  r.c0 = u0;
+  r.c1 = u1;
+  r.c2 = u2;
+}
+// f = f^2 for f in full on the quad: X = (a + b)(a + v b) on lanes 0, 1 and Y = a b on lanes 2, 3, each split over its
+// pair, one exchange across the pairs, then f^2 = (X - Y - v Y) + 2 Y w (fp12h_sqr_split's formula).
+__device__ __forceinline__ void fp12q_sqr(fp12& f, const quad_m& qm) {
+  const fp6 a = f.c0, b = f.c1;
+  fp6 s0, vb, s1;
+  fp6_add(s0, a, b);
+  fp6_mul_v(vb, b);
+  fp6_add(s1, a, vb);
+  const fp6 x = sel(qm.hi, a, s0), y = sel(qm.hi, b, s1);
+  fp6 p, o;
+  fp6_mul_pair(p, x, y, qm.odd);
+  quad_swap(o, p);
+  const fp6 X = sel(qm.hi, o, p), Y = sel(qm.hi, p, o);
+  fp6 vY, c0;
+  fp6_mul_v(vY, Y);
+  fp6_sub(c0, X, Y);
+  fp6_sub(c0, c0, vY);
+  fp6_add(f.c1, Y, Y);
+  f.c0 = c0;
+}
+// f = f lA lB (f = lA lB when `first`): this pair's line (g0, g1, h1) on both of its lanes, the other pair's by one
+// exchange; M = lA lB = (a0 b0 + xi ah bh, a0 b1 + a1 b0, a1 b1) + (0, a0 bh + ah b0, a1 bh + ah b1) w for
+// l = (g0 + g1 v) + (h1 v) w, its eight Fp2 products as two slots over the quad.
+__device__ __forceinline__ void fp12q_mul_two_lines(fp12& f, bool first, const fp2& g0, const fp2& g1, const fp2& h1,
+                                                    const quad_m& qm) {
+  fp2 og0, og1, oh1;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) {
+    (&og0.c0.v[0])[i] = quad_swap((&g0.c0.v[0])[i]);
+    (&og1.c0.v[0])[i] = quad_swap((&g1.c0.v[0])[i]);
+    (&oh1.c0.v[0])[i] = quad_swap((&h1.c0.v[0])[i]);
+  }
+  const fp2 a0 = sel(qm.hi, og0, g0), a1 = sel(qm.hi, og1, g1), ah = sel(qm.hi, oh1, h1);  // pair A's line
+  const fp2 b0 = sel(qm.hi, g0, og0), b1 = sel(qm.hi, g1, og1), bh = sel(qm.hi, h1, oh1);  // pair B's line
+  fp2 sa, sb, x, y, o1, o2;
+  fp2_add_lazy(sa, a0, a1);
+  fp2_add_lazy(sb, b0, b1);
+  x = sel(qm.hi, sel(qm.odd, ah, sa), sel(qm.odd, a1, a0));  // a0 b0 | a1 b1 | (a0 + a1)(b0 + b1) | ah bh
+  y = sel(qm.hi, sel(qm.odd, bh, sb), sel(qm.odd, b1, b0));
+  fp2_mul(o1, x, y);
+  x = sel(qm.hi, sel(qm.odd, ah, a1), sel(qm.odd, ah, a0));  // a0 bh | ah b0 | a1 bh | ah b1
+  y = sel(qm.hi, sel(qm.odd, b1, bh), sel(qm.odd, b0, bh));
+  fp2_mul(o2, x, y);
+  const fp2 p00 = quad_bcast<0>(o1), p11 = quad_bcast<1>(o1), s01 = quad_bcast<2>(o1), phh = quad_bcast<3>(o1);
+  const fp2 q0 = quad_bcast<0>(o2), q1 = quad_bcast<1>(o2), q2 = quad_bcast<2>(o2), q3 = quad_bcast<3>(o2);
+  fp12 M;
+  fp2 t;
+  fp2_mul_xi(t, phh);
+  fp2_add(M.c0.c0, p00, t);
+  fp2_sub(t, s01, p00);
+  fp2_sub(M.c0.c1, t, p11);
+  M.c0.c2 = p11;
+  fp2_set_zero(M.c1.c0);
+  fp2_add(M.c1.c1, q0, q1);
+  fp2_add(M.c1.c2, q2, q3);
+  if (first) {
+    f = M;
+  } else {
+    fp12 x12 = f;
+    fp12q_mul(f, x12, M, qm);
+  }
+}
+// f_{|x|,Q_A}(P_A) f_{|x|,Q_B}(P_B), conjugated (x < 0), in full on every lane of the quad; lanes 0, 1 carry pair A's
+// (P, Q) and T, lanes 2, 3 pair B's.  T_out: this pair's final T (pair B's gives the signature's G2 membership).
+BLS_CALL __device__ void miller_loop_shared_quad(fp12& f_out, const g1a& P_in, const g2a& Q_in, const quad_m& qm,
+                                                 uint32_t m, g2j* T_out) {
+  const g1a P = P_in;
+  const g2a Q = Q_in;
+  g2j T;
+  T.x = Q.x;
+  T.y = Q.y;
+  fp2_set_one(T.z);
+  fp12 f;
+  for (int bit = 62; bit >= 0; --bit) {
+    if ((bit & 7) == 7) BLS_RACE_POLL();
+    if (bit != 62) fp12q_sqr(f, qm);
+    fp2 g0, g1, h1;
+    miller_dbl_step_split(T, g0, g1, h1, P.x, P.y, m);
+    fp12q_mul_two_lines(f, bit == 62, g0, g1, h1, qm);
+    if ((X_ABS >> bit) & 1ull) {
+      miller_add_step_inl(T, g0, g1, h1, Q, P.x, P.y);
+      fp12q_mul_two_lines(f, false, g0, g1, h1, qm);
+    }
+  }
+  fp12_conj(f_out, f);
+  if (T_out) *T_out = T;
+}
+#endif
+
 // Verify's pairing check on a lane quad: lanes 0, 1 run e(pk, H(m))'s Miller loop split, lanes 2, 3 e(-g1, sig)'s;
 // the quad forms the product's halves (each pair multiplies its split value by the other pair's, the same
 // product on both pairs) and both pairs run the split final exponentiation.  The signature's G2 membership comes
@@ -929,13 +1075,26 @@ __device__ int lq4_verify(const g1a& pk, const g2a& hm, const g2a& sig, int q) {
     P = pk;
     Q = hm;
   }
+#if BLS_LQ4_SHARED && BLS_LQ4_FE_QUAD
+  const quad_m qm(q);
+  fp12 r, e;
+  g2j T;
+  miller_loop_shared_quad(r, P, Q, qm, m, &T);
+  const uint32_t mine = g2_subgroup_from_miller(T, Q) ? 1u : 0u;  // meaningful on the second pair
+  const uint32_t other = quad_swap(mine);
+  const uint32_t sig_in_g2 = second ? mine : other;
+  final_exponentiation_quad(e, r, qm);
+  const bool ok = fp12_is_one(e);
+#else
   fp6 h;
   g2j T;
   miller_loop_split(h, P, Q, m, &T);
   const uint32_t mine = g2_subgroup_from_miller(T, Q) ? 1u : 0u;  // meaningful on the second pair
   const uint32_t other = quad_swap(mine);
   const uint32_t sig_in_g2 = second ? mine : other;
-#if BLS_LQ4_FE_QUAD
+#endif
+#if BLS_LQ4_SHARED && BLS_LQ4_FE_QUAD
+#elif BLS_LQ4_FE_QUAD
   // full values: this pair's loop (gathered over the pair), the other pair's (one exchange across the pairs)
   fp12 fm, fo, f0, f1, r, e;
   fp12h_gather(fm, h, m);
