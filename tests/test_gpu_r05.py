@@ -251,3 +251,41 @@ def test_sixteen_lane_check_takes_small_batches(impl):
     finally:
         impl.set_pair_mode(PAIR_AUTO)
         impl.lib.hipbls_set_timing(0)
+
+
+def test_raced_calls_from_many_threads(impl):
+    """Raced small batches from eight threads at once, direct batch calls (the context's workspace) mixed with queued
+    n = 1 calls (the queue's slot workspaces): every call's race words and epochs are its own, so every status equals
+    the one large call's."""
+    import random
+    import threading
+
+    import bench
+    N = 512
+    pks, roots, sigs, bad = bench.make_c2(impl, bench.share_keys(impl, 256, "c2thr"), 0, N)
+    want = impl.batch_verify_status(pks, roots, sigs)
+    errors = []
+
+    def worker(seed):
+        rng = random.Random(seed)
+        try:
+            for _ in range(12):
+                n = rng.randint(1, 8)
+                lo = rng.randrange(0, N - n)
+                if rng.random() < 0.5:
+                    got = impl.batch_verify_status(pks[lo:lo + n], roots[lo:lo + n], sigs[lo:lo + n])
+                    if got != want[lo:lo + n]:
+                        errors.append(("batch", lo, n, got))
+                else:
+                    got = impl.verify_queued(pks[lo], roots[lo], sigs[lo])
+                    if got != want[lo]:
+                        errors.append(("queued", lo, got))
+        except Exception as e:  # noqa: BLE001 -- reported by the assertion below
+            errors.append(("exception", repr(e)))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]
