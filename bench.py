@@ -218,12 +218,16 @@ def c4_node_bad(tag, v_node, nk, shares=4, corrupt=True):
     return {v * shares + j for v in range(v_node) for j in range(shares) if c4_item(tag, v, j, nk, corrupt)[1]}
 
 
-def pmc_summary(path=os.path.join(ROOT, "profiles", "r04", "pmc_verify.json")):
+def pmc_summary(path=None):
     """k_verify_fused counters from the committed rocprofv3 --pmc passes over this build's bench (scripts/gpu_pmc_r04.sh
     WL=c2, scripts/pmc_commit_r04.py): HBM bytes per launch (FETCH_SIZE + WRITE_SIZE), their ratio to the 188 B/verify
     of algorithmic input, VALU utilisation (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES at one wave per SIMD), the fraction
     of wave cycles spent waiting, VALU and 64-bit integer VALU (the v_mad_u64_u32 stream) instructions per wave, and
-    the commit the counters were taken at.  {} when absent."""
+    the commit the counters were taken at.  {} when absent.  The newest round's passes are read."""
+    if path is None:
+        path = os.path.join(ROOT, "profiles", "r05", "pmc_verify.json")
+        if not os.path.exists(path):
+            path = os.path.join(ROOT, "profiles", "r04", "pmc_verify.json")
     try:
         with open(path) as f:
             d = json.load(f)

@@ -3,7 +3,8 @@ profiles: profiles/r04/pmc_<wl>.json (per kernel: VALU and integer-VALU instruct
 wait fraction, HBM bytes per launch, L2 hit rate) and profiles/r04/pmc_verify.json (k_verify_fused in the form
 bench.py's roofline reads, with the commit the counters were taken at).
 
-Run:  python3 scripts/pmc_commit_r04.py <git rev of the profiled build>
+Run:  python3 scripts/pmc_commit_r04.py <git rev of the profiled build> [round dir, default r04] [input prefix, default
+      pmc_ (gpurun_out/pmc_<wl>); round 5: r05 pmc5_ (scripts/gpu_pmc_r05.sh)]
 """
 import json
 import os
@@ -18,26 +19,27 @@ C2_ITEMS = 65536  # scripts/gpu_pmc_r04.sh WL=c2: the default bench, 65,536 Veri
 IN_BYTES_PER_VERIFY = 188  # pk 48 + sig 96 + message 32 + offsets 8 + status 4
 
 
-def main(rev):
-    os.makedirs(os.path.join(ROOT, "profiles", "r04"), exist_ok=True)
+def main(rev, rnd="r04", prefix="pmc_"):
+    os.makedirs(os.path.join(ROOT, "profiles", rnd), exist_ok=True)
     for wl in ("c2", "c3", "c4"):
-        src = os.path.join(ROOT, "gpurun_out", "pmc_" + wl, "summary.json")
+        src = os.path.join(ROOT, "gpurun_out", prefix + wl, "summary.json")
         if not os.path.exists(src):
             continue
         d = json.load(open(src))
-        out = {"taken_at": rev, "workload": wl, "source": "scripts/gpu_pmc_r04.sh WL=%s" % wl, "kernels": {}}
+        script = "scripts/gpu_pmc_r04.sh" if rnd == "r04" else "scripts/gpu_pmc_%s.sh" % rnd
+        out = {"taken_at": rev, "workload": wl, "source": "%s WL=%s" % (script, wl), "kernels": {}}
         for k, v in sorted(d.items()):
             if isinstance(v, dict) and v.get("valu_insts_per_wave"):
                 out["kernels"][k] = {kk: (round(v[kk], 4) if isinstance(v.get(kk), float) else v.get(kk))
                                      for kk in KEYS if kk in v}
-        with open(os.path.join(ROOT, "profiles", "r04", "pmc_%s.json" % wl), "w") as f:
+        with open(os.path.join(ROOT, "profiles", rnd, "pmc_%s.json" % wl), "w") as f:
             json.dump(out, f, indent=1)
         if wl == "c2" and "k_verify_fused" in d:
             v = d["k_verify_fused"]
             hbm = v.get("hbm_bytes_per_launch_raw")
             ver = {"kernel": "k_verify_fused", "taken_at": rev,
                    "note": "rocprofv3 --pmc passes over the default bench's C2 step at this commit "
-                           "(scripts/gpu_pmc_r04.sh WL=c2); FETCH_SIZE + WRITE_SIZE in KiB x 1024",
+                           "(%s WL=c2); FETCH_SIZE + WRITE_SIZE in KiB x 1024" % script,
                    "counters_per_launch": v.get("counters_per_launch"),
                    "hbm_bytes_per_launch_raw": hbm,
                    "hbm_bytes_per_launch_fetch_x2": v.get("hbm_bytes_per_launch_fetch_x2"),
@@ -46,10 +48,10 @@ def main(rev):
                    "int64_valu_insts_per_wave": v.get("sq_insts_valu_int64_per_wave"),
                    "int32_valu_insts_per_wave": v.get("sq_insts_valu_int32_per_wave"),
                    "wait_any_frac": v.get("wait_any_frac"), "valu_util": v.get("valu_util")}
-            with open(os.path.join(ROOT, "profiles", "r04", "pmc_verify.json"), "w") as f:
+            with open(os.path.join(ROOT, "profiles", rnd, "pmc_verify.json"), "w") as f:
                 json.dump(ver, f, indent=1)
-        print("wrote profiles/r04/pmc_%s.json (%d kernels)" % (wl, len(out["kernels"])))
+        print("wrote profiles/%s/pmc_%s.json (%d kernels)" % (rnd, wl, len(out["kernels"])))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "unknown")
+    main(sys.argv[1] if len(sys.argv) > 1 else "unknown", *(sys.argv[2:4]))
