@@ -143,3 +143,28 @@ def test_every_implementation_method_bound():
     for m in ("BatchVerify", "BatchVerifyRLC", "BatchThresholdAggregate", "BatchVerifyAggregate",
               "BatchThresholdAggregateVerify"):
         assert re.search(r"^func \((?:\w+ )?HipBLS\) " + m + r"\(", batch, flags=re.M), m
+
+
+def test_error_texts_are_herumis():
+    """The error texts the cgo package returns for a Verify status (hipbls.go verifyErr / deserErr) and the Python
+    mirror's (charon_amd/tbls.py VERIFY_ERRORS) are the strings tbls.Herumi wraps and returns for the same input
+    (tbls/herumi.go Verify): the Go package cannot be compiled here, so its mapping is pinned textually."""
+    from charon_amd import tbls
+    go = open(os.path.join(INT, "charon", "tbls", "hipbls", "hipbls.go")).read()
+    want = {tbls.ERR_PUBKEY: "cannot set compressed public key in Herumi format",
+            tbls.ERR_SIGNATURE: "cannot unmarshal signature into Herumi signature",
+            tbls.ERR_VERIFY: "signature not verified"}
+    assert tbls.VERIFY_ERRORS == want
+    for text in want.values():
+        assert '"%s"' % text in go, text
+    # verifyErr: OK -> nil, VERIFY -> the plain error, anything else -> the deserialization wrap
+    m = re.search(r"func verifyErr\(.*?\n}\n", go, flags=re.S)
+    assert m and "case C.HIPBLS_OK:\n\t\treturn nil" in m.group(0)
+    assert 'case C.HIPBLS_ERR_VERIFY:\n\t\treturn errors.New("signature not verified")' in m.group(0)
+    m = re.search(r"func deserErr\(.*?\n}\n", go, flags=re.S)
+    assert m and "status == C.HIPBLS_ERR_PUBKEY" in m.group(0)
+    if os.path.isdir(REF):
+        herumi = open(os.path.join(REF, "tbls", "herumi.go")).read()
+        v = re.search(r"func \(Herumi\) Verify\(.*?\n}\n", herumi, flags=re.S).group(0)
+        for text in want.values():
+            assert '"%s"' % text in v, text
