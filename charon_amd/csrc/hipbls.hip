@@ -968,7 +968,8 @@ constexpr uint64_t kLg2FallbackLanes = 32768;
 int launch_fallback(Context& c, hipStream_t s, const uint32_t* list, const uint32_t* cnt, uint64_t cap,
                     uint64_t concurrent, const uint8_t* d_pks, const uint8_t* d_sigs, const uint32_t* d_midx,
                     const uint32_t* d_H, uint64_t hstride, const uint32_t* d_hslot, int32_t* d_status,
-                    const uint32_t* d_kidx, uint64_t T, const uint32_t* tab) {
+                    const uint32_t* d_kidx, uint64_t T, const uint32_t* tab, const uint32_t* rpk,
+                    const uint32_t* rsig, uint64_t n) {
   const int mode = g_pair_mode.load();
   const uint64_t pair_upto = mode == HIPBLS_PAIR_SINGLE ? 0
                              : (mode == HIPBLS_PAIR_AUTO ? kLg2FallbackLanes / (concurrent ? concurrent : 1)
@@ -978,13 +979,14 @@ int launch_fallback(Context& c, hipStream_t s, const uint32_t* list, const uint3
   if (pairs > 0)
     rc = timed(c, "rlc_fallback_lg2", s, [&] {
       hipLaunchKernelGGL(k_rlc_fallback_lg2, dim3((unsigned)grid_for(2 * pairs)), dim3(kBlock), 0, s, list, cnt, cap,
-                         d_pks, d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab, pair_upto);
+                         d_pks, d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab, pair_upto, rpk, rsig,
+                         n);
     });
   if (rc) return rc;
   if (pair_upto < cap)
     rc = timed(c, "rlc_fallback", s, [&] {
       hipLaunchKernelGGL(k_rlc_fallback, dim3((unsigned)grid_for(cap)), dim3(kBlock), 0, s, list, cnt, cap, d_pks,
-                         d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab, pair_upto);
+                         d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab, pair_upto, rpk, rsig, n);
     });
   return rc;
 }
@@ -1084,7 +1086,7 @@ int launch_rlc(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const ui
     // next sub-batch's windows); off by default until measured on its own.
     static const bool tail_pairs = getenv("HIPBLS_RLC_TAIL_PAIRS") && getenv("HIPBLS_RLC_TAIL_PAIRS")[0] == '1';
     rc = launch_fallback(c, ss, list + i0, cnt + k, i1 - i0, tail_pairs && k + 1 == nsub ? 1 : nsub, d_pks, d_sigs,
-                         d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
+                         d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab, rpk, rsig, n);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c.ev_join[k], ss));
     HIP_TRY(hipStreamWaitEvent(s, c.ev_join[k], 0));
@@ -1396,7 +1398,8 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
                          d_status, win, list, cnt);
     });
   if (rc) return rc;
-  rc = launch_fallback(c, s, list, cnt, n, 1, d_pks, d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab);
+  rc = launch_fallback(c, s, list, cnt, n, 1, d_pks, d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab,
+                       (const uint32_t*)rpk, (const uint32_t*)rsig, n);
   if (rc) return rc;
   c.r_windows = n_win;
   return ws_end(c, s, WS_RLC);

@@ -867,13 +867,15 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback(const uint32_t* __restr
                                                          const uint32_t* __restrict__ hslot,
                                                          int32_t* __restrict__ status,
                                                          const uint32_t* __restrict__ key_idx, uint64_t T,
-                                                         const uint32_t* __restrict__ tab, uint64_t pair_upto) {
+                                                         const uint32_t* __restrict__ tab, uint64_t pair_upto,
+                                                         const uint32_t* __restrict__ rpk,
+                                                         const uint32_t* __restrict__ rsig, uint64_t n) {
   const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t len = *list_len;
   if (len <= pair_upto) return;  // k_rlc_fallback_lg2 takes short lists
   if (j >= len || j >= cap) return;
   BLS_LANE_F12(F);
-  rlc_fallback_lane(F, list[j], pks, sigs, msg_idx, H, hstride, hslot, status, key_idx, T, tab);
+  rlc_fallback_lane(F, list[j], pks, sigs, msg_idx, H, hstride, hslot, status, key_idx, T, tab, rpk, rsig, n);
 }
 
 // The lane-pair layout (lg2.h): the even lane decodes the key and takes e(pk, H(m)), the odd lane decodes the
@@ -887,7 +889,9 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback_lg2(const uint32_t* __r
                                                              const uint32_t* __restrict__ hslot,
                                                              int32_t* __restrict__ status,
                                                              const uint32_t* __restrict__ key_idx, uint64_t T,
-                                                             const uint32_t* __restrict__ tab, uint64_t pair_upto) {
+                                                             const uint32_t* __restrict__ tab, uint64_t pair_upto,
+                                                             const uint32_t* __restrict__ rpk,
+                                                             const uint32_t* __restrict__ rsig, uint64_t n) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   const uint64_t j = t >> 1;
   const uint32_t m = (t & 1) ? ~0u : 0u;
@@ -896,9 +900,14 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback_lg2(const uint32_t* __r
   if (j >= len || j >= cap) return;
   const uint64_t i = list[j];
   if (status[i] != RLC_PENDING) return;
+  g1a spk;
+  g2a ssig;
+  const bool scaled = rlc_scaled_pair(spk, ssig, rpk, rsig, n, i);  // the same decision on both lanes
   const bool ok = pairing_check_lg2<1>(2, m, [&](int k, g1a& P, g2a& Q) {
     if (k == 0) {
-      if (pks)
+      if (scaled)
+        P = spk;
+      else if (pks)
         g1_decompress(P, pks + 48 * i, false);
       else
         soa_load<24>(&P.x.v[0], tab, T, key_idx[i]);
@@ -906,7 +915,10 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback_lg2(const uint32_t* __r
     } else {
       P.x = G1_GEN_X;
       P.y = G1_NEG_GEN_Y;
-      g2_decompress(Q, sigs + 96 * i, false);
+      if (scaled)
+        Q = ssig;
+      else
+        g2_decompress(Q, sigs + 96 * i, false);
     }
   });
   if (!m) status[i] = ok ? HIPBLS_OK : HIPBLS_ERR_VERIFY;

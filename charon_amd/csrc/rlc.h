@@ -464,19 +464,40 @@ BLS_HD BLS_INLINE int rlc_window_lane(const f12l<S>& F, uint64_t w, uint64_t n, 
 // Stage 4, item i: still pending after its window failed -> tbls.Verify of the item alone.  Both
 // points already passed decoding and the subgroup tests in stage 1 and H(m) is in the table, so this
 // is the bare pairing check: e(pk, H(m)) * e(-g1, sig) == 1 (about half of a full op_verify).
+// The fallback's points from stage 1 instead of the wire bytes: an item pending in a failed window has [r] pk and
+// [r] sig stored (rlc_item_decoded; the batch-wide path's k_rlcb_mark stores the same), and for r != 0 mod the group
+// order e([r] pk, H) == e(g1, [r] sig) exactly when e(pk, H) == e(g1, sig), so the re-check needs two inversions
+// (to affine) instead of three square-root powers of decompression.  r = a + b x with a, b < 2^32 is 0 only for
+// a = b = 0, which leaves both points at infinity: then (and without stored points) the caller decodes as before.
+BLS_HD BLS_INLINE bool rlc_scaled_pair(g1a& pk, g2a& sig, const uint32_t* rpk, const uint32_t* rsig, uint64_t n,
+                                       uint64_t i) {
+  if (!rpk || !rsig) return false;
+  g1j rp;
+  g2j rs;
+  soa_load<36>(&rp.x.v[0], rpk, n, i);
+  soa_load<72>(&rs.x.c0.v[0], rsig, n, i);
+  if (jac_is_inf(rp) || jac_is_inf(rs)) return false;
+  jac_to_aff(pk, rp);
+  jac_to_aff(sig, rs);
+  return true;
+}
+
 template <int S>
 BLS_HD BLS_INLINE void rlc_fallback_lane(const f12l<S>& F, uint64_t i, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
                                          const uint32_t* H, uint64_t hstride, const uint32_t* hslot, int32_t* status,
                                          const uint32_t* key_idx = nullptr, uint64_t T = 0,
-                                         const uint32_t* tab = nullptr) {
+                                         const uint32_t* tab = nullptr, const uint32_t* rpk = nullptr,
+                                         const uint32_t* rsig = nullptr, uint64_t n = 0) {
   if (status[i] != RLC_PENDING) return;
   g1a pk;
   g2a sig, hm;
-  if (pks)
-    g1_decompress(pk, pks + 48 * i, false);
-  else
-    soa_load<24>(&pk.x.v[0], tab, T, key_idx[i]);
-  g2_decompress(sig, sigs + 96 * i, false);
+  if (!rlc_scaled_pair(pk, sig, rpk, rsig, n, i)) {
+    if (pks)
+      g1_decompress(pk, pks + 48 * i, false);
+    else
+      soa_load<24>(&pk.x.v[0], tab, T, key_idx[i]);
+    g2_decompress(sig, sigs + 96 * i, false);
+  }
   soa_load<48>(&hm.x.c0.v[0], H, hstride, h_col(hslot, msg_idx[i]));
   status[i] = pairing_check_verify_l(pk, hm, sig, F) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
 }

@@ -406,7 +406,9 @@ extern "C" int ht_rlc_verify(const uint8_t* pks, const uint8_t* sigs, const uint
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
   mark(2);
-  for (uint32_t i : list) rlc_fallback_lane(host_f12_slot(), i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status);
+  for (uint32_t i : list)
+    rlc_fallback_lane(host_f12_slot(), i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status, nullptr, 0, nullptr,
+                      rpk.data(), rsig.data(), n);
   mark(3);
   stats3[0] = n_win;
   stats3[1] = stats3[2] = 0;
@@ -442,7 +444,9 @@ extern "C" int ht_rlc_verify_keys(const uint8_t* tab_pks, uint64_t T, const uint
     if (rlc_window_lane(host_f12_slot(), w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
-  for (uint32_t i : list) rlc_fallback_lane(host_f12_slot(), i, nullptr, sigs, msg_idx, H.data(), n_msgs, nullptr, status, key_idx, T, tab.data());
+  for (uint32_t i : list)
+    rlc_fallback_lane(host_f12_slot(), i, nullptr, sigs, msg_idx, H.data(), n_msgs, nullptr, status, key_idx, T, tab.data(),
+                      rpk.data(), rsig.data(), n);
   stats3[0] = n_win;
   stats3[1] = stats3[2] = 0;
   for (int32_t x : win)
@@ -625,7 +629,9 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
     if (rlc_window_lane(host_f12_slot(), w, n, msg_idx, rpk.data(), rsig.data(), H.data(), n_msgs, nullptr, status, win.data()))
       for (uint64_t i = w * RLC_W; i < n && i < (w + 1) * RLC_W; ++i)
         if (status[i] == RLC_PENDING) list.push_back((uint32_t)i);
-  for (uint32_t i : list) rlc_fallback_lane(host_f12_slot(), i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status);
+  for (uint32_t i : list)
+    rlc_fallback_lane(host_f12_slot(), i, pks, sigs, msg_idx, H.data(), n_msgs, nullptr, status, nullptr, 0, nullptr,
+                      rpk.data(), rsig.data(), n);
   mark(5);
   return 0;
 }
