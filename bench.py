@@ -37,7 +37,7 @@ MADS_PER_FPMUL = 300
 # RLC BatchVerify stages (charon_amd/csrc/rlc.h), same unit and source (tests/test_work_counts.py):
 # stage 1 per item, stage 2 per distinct message, stage 3 per window of 8 with 2 messages (one per
 # 4-partial validator) or 1 message (committee root), stage 4 per item re-checked after a failed window.
-RLC_FPMUL = {"item": 5495, "hash": 4790, "window_2msg": 21906, "window_1msg": 17485, "fallback": 18394}
+RLC_FPMUL = {"item": 5495, "hash": 4790, "window_2msg": 21906, "window_1msg": 17485, "fallback": 17021}
 # Batch-wide check (charon_amd/csrc/rlcb.h), same unit and source: stage 1 per item, the Pippenger MSM per item
 # (2 points x 2 windows of mixed additions; the bucket/segment folds add ~15 per item at 1M items and are left
 # out), and one multi-Miller loop per 16-item chunk with 4 message runs (one root per 4-partial validator) or with one
