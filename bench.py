@@ -34,6 +34,9 @@ METRIC = "verified BLS partial sigs/sec (node) + threshold aggregates/sec, 1/2/4
 # counted: ~33k VALU each, about 49 products' worth of issue time.  See DESIGN.md "Roofline".
 FPMUL_PER_VERIFY = 24247
 MADS_PER_FPMUL = 300
+# HIPBLS_RLC_AUTO after a failed batch-wide check: kRlcbBackoff (8) calls on windows only, then the check again
+# (charon_amd/csrc/hipbls.hip use_rlc_batch), so a stream with invalid partials pays one failed check per 9 calls
+RLC_AUTO_PERIOD = 9
 # RLC BatchVerify stages (charon_amd/csrc/rlc.h), same unit and source (tests/test_work_counts.py):
 # stage 1 per item, stage 2 per distinct message, stage 3 per window of 8 with 2 messages (one per
 # 4-partial validator) or 1 message (committee root), stage 4 per item re-checked after a failed window.
@@ -790,6 +793,18 @@ def main():
                 tel_auto = timed_loop(rstep, args.rlc_steps, dev, barrier, world)
                 assert {i for i, x in enumerate(d_st4.cpu().tolist()) if x != 0} == bad4, "RLC bitmap mismatch (auto)"
                 rlc[variant]["auto_mode_ms_per_batch"] = round(1000 * tel_auto / args.rlc_steps, 3)
+                # a batch-wide check that fails (what AUTO pays once every RLC_AUTO_PERIOD calls of such a stream:
+                # the check, then the windows and fallback over the same items)
+                impl.set_rlc_mode(RLC_BATCH)
+                rstep()
+                torch.cuda.synchronize(dev)
+                tel_fb = timed_loop(rstep, args.rlc_steps, dev, barrier, world)
+                assert {i for i, x in enumerate(d_st4.cpu().tolist()) if x != 0} == bad4, "RLC bitmap mismatch (batch)"
+                fb_ms = 1000 * tel_fb / args.rlc_steps
+                rlc[variant]["failed_batch_check_ms_per_batch"] = round(fb_ms, 3)
+                rlc[variant]["auto_mode_amortized_ms_per_batch"] = round(
+                    ((RLC_AUTO_PERIOD - 1) * 1000 * tel / args.rlc_steps + fb_ms) / RLC_AUTO_PERIOD, 3)
+                impl.set_rlc_mode(RLC_AUTO)
             if args.keys and variant in ("i_root_per_validator", "i_all_valid"):
                 table4 = list(dict.fromkeys(pks4))
                 pos4 = {k: j for j, k in enumerate(table4)}
@@ -875,6 +890,15 @@ def main():
         assert {i for i, x in enumerate(d_st5.cpu().tolist()) if x != 0} == bad5, "C5 bitmap mismatch"
         if rank == 0 and c5_fav:
             assert d_sst.cpu().tolist() == [0], "sync-committee FastAggregateVerify failed"
+        # the slot when AUTO retries its batch-wide check (once every RLC_AUTO_PERIOD calls of a stream with invalid
+        # partials), and the average over that period
+        impl.set_rlc_mode(RLC_BATCH)
+        c5step()
+        torch.cuda.synchronize()
+        t5b = timed_loop(c5step, args.rlc_steps, dev, barrier, world)
+        torch.cuda.synchronize()
+        impl.set_rlc_mode(RLC_AUTO)
+        assert {i for i, x in enumerate(d_st5.cpu().tolist()) if x != 0} == bad5, "C5 bitmap mismatch (batch)"
         if world > 1:  # node-wide failure count == construction
             rows = node5[0]
             fails = sum(int((~unpack_bitmap(rows[r], c5_rows[r])).sum()) for r in range(world))
@@ -885,7 +909,10 @@ def main():
                           "of its root) overlapped on rank 0" % args.rlc_node_validators,
               "node_partials": n5_node, "partials_this_gpu": n5, "ms_per_slot": round(1000 * t5 / args.rlc_steps, 3),
               "verified_partial_sigs_per_s": round(n5_node * args.rlc_steps / t5, 1),
-              "sync_aggregate_verifies_per_s": round(args.rlc_steps / t5, 3)}
+              "sync_aggregate_verifies_per_s": round(args.rlc_steps / t5, 3),
+              "failed_batch_check_ms_per_slot": round(1000 * t5b / args.rlc_steps, 3),
+              "auto_mode_amortized_ms_per_slot": round(1000 * ((RLC_AUTO_PERIOD - 1) * t5 + t5b)
+                                                       / (RLC_AUTO_PERIOD * args.rlc_steps), 3)}
         del d_pk5, d_sig5, d_midx5, d_msg5, d_off5, d_st5
 
     if rank == 0:

@@ -57,11 +57,15 @@ __global__ void k_rlcb_final8(const uint32_t* Ftot, const uint32_t* Fs, int32_t*
 __global__ void k_g1m_miller8(uint64_t nl_max, const uint32_t* meta, const uint32_t* lmsg, const uint32_t* Wv,
                               const uint32_t* H, uint64_t hstride, const uint32_t* hslot, uint32_t* F, uint64_t col0,
                               uint64_t fstride);
+__global__ void k_fav_prep8(const uint8_t* pks, uint64_t nkeys, const uint8_t* sigs, const uint8_t* msgs,
+                            const uint64_t* moffs, uint64_t G, uint32_t* pts, int32_t* kcode, uint32_t* ws);
 }  // namespace bls_fp2p
 // The sixteen-lane check for batches of at most four items (verify_hex.hip: BLS_FP2_PAIR + BLS_HEX, namespace bls_hex).
 namespace bls_hex {
 __global__ void k_verify_pair_lq16(const uint32_t* ws, uint64_t n, int32_t* status, uint32_t replicas, uint32_t* race,
                                    uint32_t epoch);
+__global__ void k_fav_pair_lq16(const uint32_t* pts, const int32_t* kcode, uint64_t nkeys, const uint64_t* goff,
+                                const uint32_t* ws, uint64_t G, int32_t* status);
 }  // namespace bls_hex
 namespace bls_fp2p {
 // LDS the S-factor workgroup reserves at launch and never touches: the chunk kernel's 36 KiB per workgroup (four per
@@ -177,6 +181,7 @@ struct Context {
   DevBuf b_pk, b_msg, b_off, b_sig, b_st, b_out, b_ids, b_pts, b_pst, b_aux, b_part, b_bad;
   DevBuf r_pk, r_sig, r_h, r_win, r_midx, r_list, r_cnt, r_slot, r_mlist;  // RLC BatchVerify workspaces
   DevBuf t_code, t_tab, b_kidx;                                            // resident pubshare table + key indices
+  DevBuf f_ws;  // FastAggregateVerify on the octet / sixteen-lane layouts: per-group H(m), signature, codes
   DevBuf v_ws;                                                             // lane-pair Verify points (SoA)
   // sigagg in one call (launch_tagg_verify): two workspace sets used alternately, each with the completion event of
   // the call that last used it
@@ -335,7 +340,7 @@ const KernelRef kKernels[] = {
     KREF(k_verify_fused), KREF(k_verify_keys), KREF(k_verify_pair_lg2), KREF(k_verify_pair_lq4),
     KREF(k_verify_pair_single), KREF(k_verify_prep), KREF(k_zero_sig_status), KREF8(k_g1m_miller8),
     KREF8(k_rlcb_final8), KREF8(k_rlcb_sfactor8), KREF8(k_verify_pair_lq8), KREF8(k_verify_prep8),
-    KREF16(k_verify_pair_lq16),
+    KREF16(k_verify_pair_lq16), KREF8(k_fav_prep8), KREF16(k_fav_pair_lq16),
 };
 #define RES(s) reinterpret_cast<const void*>(&k_scratch_reserve<s>)
 // 8 KiB to the per-lane budget (charon_amd/codeobj.py PRIVATE_SEGMENT_BUDGET, 13,104 B) in 256-byte steps: at most
@@ -1525,6 +1530,16 @@ int launch_tagg_verify(Context& c, const uint8_t* d_sigs, const int64_t* d_ids, 
   return rc;  // tv_end records tv_done[p]
 }
 
+// A few groups (the sync committee's one aggregate per slot) take the drop-in path's layouts: keys, signatures and
+// messages decoded / hashed on octets (verify_lat.hip k_fav_prep8), then the key sum and the sixteen-lane check per
+// group (verify_hex.hip k_fav_pair_lq16), instead of k_fav_batch's one workgroup per group with its hash and pairing
+// at one or two lanes' speed.  AUTO pair mode only, so PAIR_SINGLE / PAIR_LANES keep k_fav_batch for the layout-parity
+// tests; HIPBLS_LAT_HEX=0 turns it off with the n = 1 check.
+constexpr uint64_t kFavHexMaxGroups = 16;
+bool use_fav_hex(uint64_t n_groups) {
+  return g_lat_hex && g_pair_mode.load() == HIPBLS_PAIR_AUTO && n_groups <= kFavHexMaxGroups;
+}
+
 int launch_fav(Context& c, const uint8_t* d_pks, uint64_t nkeys, const uint64_t* d_goff, uint64_t n_groups,
                const uint8_t* d_sigs, const uint8_t* d_msgs, const uint64_t* d_moffs, int32_t* d_status,
                hipStream_t s) {
@@ -1533,6 +1548,24 @@ int launch_fav(Context& c, const uint8_t* d_pks, uint64_t nkeys, const uint64_t*
   HIP_TRY(c.b_pst.ensure((nkeys ? nkeys : 1) * 4));
   int rc = ws_begin(c, s);
   if (rc) return rc;
+  if (use_fav_hex(n_groups)) {
+    HIP_TRY(c.f_ws.ensure(n_groups * 122 * 4));
+    // the kernel derives the same role boundaries from nkeys and n_groups
+    const uint64_t nbk = (8 * nkeys + kBlock - 1) / kBlock, nbg = (8 * n_groups + kBlock - 1) / kBlock;
+    rc = timed(c, "fav_prep8", s, [&] {
+      hipLaunchKernelGGL(bls_fp2p::k_fav_prep8, dim3((unsigned)(nbk + 2 * nbg)), dim3(kBlock), 0, s, d_pks, nkeys,
+                         d_sigs, d_msgs, d_moffs, n_groups, (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p,
+                         (uint32_t*)c.f_ws.p);
+    });
+    if (rc) return rc;
+    rc = timed(c, "fav_lq16", s, [&] {
+      hipLaunchKernelGGL(bls_hex::k_fav_pair_lq16, dim3((unsigned)n_groups), dim3(kBlock), 0, s,
+                         (const uint32_t*)c.b_pts.p, (const int32_t*)c.b_pst.p, nkeys, d_goff,
+                         (const uint32_t*)c.f_ws.p, n_groups, d_status);
+    });
+    if (rc) return rc;
+    return ws_end(c, s);
+  }
   if (nkeys)
     hipLaunchKernelGGL(k_g1_decode, dim3((unsigned)grid_for(nkeys)), dim3(kBlock), 0, s, d_pks, nkeys,
                        (uint32_t*)c.b_pts.p, (int32_t*)c.b_pst.p);

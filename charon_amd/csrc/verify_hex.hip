@@ -59,4 +59,91 @@ __global__ void __launch_bounds__(kHexBlock) k_verify_pair_lq16(const uint32_t* 
   bls_race::finish();
 }
 
+// FastAggregateVerify's check for a few groups (tbls/herumi.go:315-339), one workgroup per group g over the keys
+// [goff[g], goff[g + 1]) that verify_lat.hip k_fav_prep8 decoded: the 64 lanes sum them (strided mixed additions, then
+// an LDS tree, as kernels.h k_fav_batch), then lanes 0-15 run lq4_verify on the aggregate key in the sixteen-lane
+// layout.  Status order as k_fav_batch: the signature's error first (its encoding, or G2 membership, which comes from
+// lq4_verify's Miller loop, so the check runs whenever the signature decoded, with -g1 standing in for a key sum that
+// cannot be used), then a key's encoding error, then "verification failed" (also for an empty key list, an infinity
+// key or signature, a key sum at infinity).
+__global__ void __launch_bounds__(kHexBlock) k_fav_pair_lq16(const uint32_t* __restrict__ pts,
+                                                             const int32_t* __restrict__ kcode, uint64_t nkeys,
+                                                             const uint64_t* __restrict__ goff,
+                                                             const uint32_t* __restrict__ ws, uint64_t G,
+                                                             int32_t* __restrict__ status) {
+  __shared__ uint32_t red[kHexBlock * 36];
+  __shared__ int sh_bad, sh_inf;
+  bls_race::init(nullptr, 0u);
+  const uint64_t g = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint64_t k0 = goff[g], k1 = goff[g + 1];
+  if (tid == 0) {
+    sh_bad = 0;
+    sh_inf = 0;
+  }
+  __syncthreads();
+  {
+    g1j acc;
+    jac_set_inf(acc);
+    int bad = 0, inf = 0;
+    for (uint64_t k = k0 + tid; k < k1; k += kHexBlock) {
+      const int c = kcode[k];
+      if (c == DEC_BAD) {
+        bad = 1;
+      } else if (c == DEC_INF) {
+        inf = 1;
+      } else {
+        g1a a;
+        soa_load<24>(&a.x.v[0], pts, nkeys, k);
+        jac_add_aff(acc, acc, a);
+      }
+    }
+    if (bad) atomicOr(&sh_bad, 1);
+    if (inf) atomicOr(&sh_inf, 1);
+    for (int w = 0; w < 36; ++w) red[w * kHexBlock + tid] = (&acc.x.v[0])[w];
+  }
+  __syncthreads();
+  for (int half = kHexBlock / 2; half >= 1; half >>= 1) {  // every thread reaches every barrier
+    if (tid < half) {
+      g1j x, y;
+      for (int w = 0; w < 36; ++w) {
+        (&x.x.v[0])[w] = red[w * kHexBlock + tid];
+        (&y.x.v[0])[w] = red[w * kHexBlock + tid + half];
+      }
+      jac_add(x, x, y);
+      for (int w = 0; w < 36; ++w) red[w * kHexBlock + tid] = (&x.x.v[0])[w];
+    }
+    __syncthreads();
+  }
+  if (tid >= 16) return;  // lanes 0-15: the check, every branch below on shared values only
+  const int ds = ((const int32_t*)(ws + 120 * G))[2 * g + 1];
+  g1j sum;
+  for (int w = 0; w < 36; ++w) (&sum.x.v[0])[w] = red[w * kHexBlock];
+  const bool sum_ok = !sh_bad && !sh_inf && k1 > k0 && !jac_is_inf(sum);
+  int chk = HIPBLS_OK;
+  if (ds == DEC_OK) {
+    g1a pk;
+    if (sum_ok) {
+      jac_to_aff(pk, sum);
+    } else {
+      pk.x = G1_GEN_X;
+      pk.y = G1_NEG_GEN_Y;
+    }
+    g2a hm, sig;
+    soa_load<48>(&hm.x.c0.v[0], ws + 24 * G, G, g);
+    soa_load<48>(&sig.x.c0.v[0], ws + 72 * G, G, g);
+    chk = lq4_verify(pk, hm, sig, tid & 3);
+  }
+  int st;
+  if (ds == DEC_BAD || chk == HIPBLS_ERR_SIGNATURE)
+    st = HIPBLS_ERR_SIGNATURE;
+  else if (sh_bad)
+    st = HIPBLS_ERR_PUBKEY;
+  else if (!sum_ok || ds == DEC_INF)
+    st = HIPBLS_ERR_VERIFY;  // KeyValidate rejects the identity key; the empty set is false
+  else
+    st = chk;
+  if (tid == 0) status[g] = st;
+}
+
 }  // namespace bls

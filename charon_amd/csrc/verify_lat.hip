@@ -222,6 +222,60 @@ __global__ void __launch_bounds__(kOctBlock) k_verify_prep8(const uint8_t* __res
   bls_race::finish();
 }
 
+// FastAggregateVerify's stage 1 for a few groups (tbls/herumi.go:315-339; hipbls.hip launch_fav, the sync committee's
+// one aggregate per slot), eight lanes per unit: every key of every group decoded + subgroup-tested (pts: affine SoA
+// with stride nkeys, kcode: DEC_* per key), beside each group's signature decode and message hash exactly as
+// k_verify_prep8's roles 1 and 2 (ws: H(m) at 24 G, sig at 72 G, the signature's code at word 2 g + 1 of 120 G).
+// Workgroups: the key blocks, then the signature blocks, then the hash blocks.  Not raced.
+__global__ void __launch_bounds__(kOctBlock) k_fav_prep8(const uint8_t* __restrict__ pks, uint64_t nkeys,
+                                                         const uint8_t* __restrict__ sigs,
+                                                         const uint8_t* __restrict__ msgs,
+                                                         const uint64_t* __restrict__ moffs, uint64_t G,
+                                                         uint32_t* __restrict__ pts, int32_t* __restrict__ kcode,
+                                                         uint32_t* __restrict__ ws) {
+  bls_race::init(nullptr, 0u);
+  const uint64_t nbk = (8 * nkeys + kOctBlock - 1) / kOctBlock;
+  const uint64_t nbg = (8 * G + kOctBlock - 1) / kOctBlock;
+  uint64_t b = blockIdx.x;
+  int role = 0;  // 0 key, 1 signature, 2 hash: uniform per workgroup
+  if (b >= nbk) {
+    b -= nbk;
+    role = b < nbg ? 1 : 2;
+    if (role == 2) b -= nbg;
+  }
+  const uint64_t t = b * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t i = t >> 3;
+  const bool lead = (t & 7) == 0;
+  if (role == 0) {
+    if (i >= nkeys) return;  // the same on all eight lanes
+    g1a pk;
+    const int dp = g1_decompress(pk, pks + 48 * i, true);
+    if (lead) {
+      kcode[i] = dp;
+      if (dp == DEC_OK) soa_store<24>(pts, nkeys, i, &pk.x.v[0]);
+    }
+    return;
+  }
+  if (i >= G) return;
+  if (role == 2) {
+    const uint32_t m = (t & 1) ? ~0u : 0u;
+    const uint64_t o0 = moffs[i], o1 = moffs[i + 1];
+    g2j sum, hj;
+    hash_to_g2_pair_sum(sum, msgs + o0, (uint32_t)(o1 - o0), DST_POP, 43, m);
+    g2_clear_cofactor_quad(hj, sum, (int)(t & 3));
+    g2a hm;
+    jac_to_aff(hm, hj);
+    if (lead) soa_store<48>(ws + 24 * G, G, i, &hm.x.c0.v[0]);
+    return;
+  }
+  g2a sig;
+  const int ds = g2_decompress(sig, sigs + 96 * i, false);  // G2 membership: from the check's Miller loop
+  if (lead) {
+    ((int32_t*)(ws + 120 * G))[2 * i + 1] = ds;
+    if (ds == DEC_OK) soa_store<48>(ws + 72 * G, G, i, &sig.x.c0.v[0]);
+  }
+}
+
 #ifndef BLS_LQ8_XCD_PROBE
 #define BLS_LQ8_XCD_PROBE 0
 #endif

@@ -289,3 +289,65 @@ def test_raced_calls_from_many_threads(impl):
     for t in th:
         t.join()
     assert not errors, errors[:5]
+
+
+def test_fav_octet_and_sixteen_lane_layouts_match_fav_batch(impl):
+    """FastAggregateVerify for at most 16 groups runs on the drop-in path's layouts (verify_lat.hip k_fav_prep8, then
+    verify_hex.hip k_fav_pair_lq16); PAIR_SINGLE keeps k_fav_batch.  Same statuses on: honest groups, a wrong message,
+    a signature / key encoding error, empty, identity key, keys summing to infinity (P, -P), small-order signatures
+    (alone and with a bad key: the signature's error wins), a small-order key, a 512-key sync-committee group, and a
+    17-group batch (over the limit: k_fav_batch in AUTO too)."""
+    import json
+    import random
+
+    from charon_amd.tbls import PAIR_AUTO, PAIR_SINGLE
+
+    def launches(name):
+        a, c = ctypes.c_double(), ctypes.c_uint64()
+        impl.lib.hipbls_kernel_timing(name, ctypes.byref(a), ctypes.byref(c))
+        return c.value
+
+    with open(os.path.join(ROOT, "tests", "golden", "fixtures.json")) as f:
+        so = json.load(f)["small_order"]
+    h = bytes.fromhex
+    rng = random.Random(55)
+    sks = [rng.randrange(1, 2 ** 254).to_bytes(32, "big") for _ in range(512)]
+    pks, st = impl.secret_to_public_key_batch(sks)
+    assert set(st) == {0}
+    msg = b"sync committee root".ljust(32, b"\0")
+    sigs, _ = impl.sign_batch(sks, [msg] * 512)
+    agg3, agg512 = impl.aggregate(sigs[:3]), impl.aggregate(sigs)
+    bad_sig = bytearray(agg3)
+    bad_sig[0] &= 0x7F
+    neg0 = bytearray(pks[0])
+    neg0[0] ^= 0x20  # the sign flag: -P
+    small_sig, small_pk = h(so["verify"][0]["sig"]), h(so["verify"][16]["pk"])
+    groups = [
+        (pks[:3], agg3, msg),                        # 0
+        (pks[:3], agg3, msg[::-1]),                  # 3
+        (pks[:3], bytes(bad_sig), msg),              # 2
+        ([pks[0], bytes(48), pks[2]], agg3, msg),    # 1
+        ([], agg3, msg),                             # 3
+        (pks[:3] + [bytes([0xC0]) + bytes(47)], agg3, msg),  # 3
+        ([pks[0], bytes(neg0)], agg3, msg),          # 3: the key sum is the identity
+        (pks[:3], small_sig, msg),                   # 2
+        ([pks[0], bytes(48)], small_sig, msg),       # 2: the signature's membership error before the key's
+        (pks[:3] + [small_pk], agg3, msg),           # 1
+        (pks, agg512, msg),                          # 0
+        (pks[:511], agg512, msg),                    # 3
+    ]
+    want = [0, 3, 2, 1, 3, 3, 3, 2, 2, 1, 0, 3]
+    impl.lib.hipbls_set_timing(1)
+    try:
+        for mode, batch, hexl in ((PAIR_SINGLE, groups, 0), (PAIR_AUTO, groups, 1), (PAIR_AUTO, groups * 2, 0)):
+            impl.set_pair_mode(mode)
+            before = launches(b"fav_lq16")
+            assert impl.batch_verify_aggregate_status(batch) == want * (len(batch) // len(groups)), (mode, len(batch))
+            assert launches(b"fav_lq16") - before == hexl, (mode, len(batch))
+        impl.set_pair_mode(PAIR_AUTO)
+        for g, w in zip(groups, want):  # one group per call, as the sync-committee duty sends it
+            assert impl.batch_verify_aggregate_status([g]) == [w]
+    finally:
+        impl.set_pair_mode(PAIR_AUTO)
+        impl.lib.hipbls_set_timing(0)
+

@@ -3,6 +3,7 @@
 instrumented host build of the same per-lane code the kernels run (tests/native/host_ops.cpp).
 This test recomputes it on a seeded sample and keeps bench.py honest."""
 import ctypes
+import os
 import random
 
 from oracle import bls12381 as bls
@@ -137,3 +138,13 @@ def test_bench_tagg_counts_match():
     want = bench.TAGG_FPMUL
     for k, got in zip(("scale_7", "sum", "unscale", "key_prep", "pairing"), tot):
         assert abs(got / N - want[k]) / want[k] < 0.03, (k, got / N)
+
+
+def test_bench_auto_period_matches_library():
+    """bench.RLC_AUTO_PERIOD = the library's back-off after a failed batch-wide check + the retried call."""
+    import re
+    import bench
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "charon_amd", "csrc",
+                            "hipbls.hip")).read()
+    backoff = int(re.search(r"constexpr int kRlcbBackoff = (\d+);", src).group(1))
+    assert bench.RLC_AUTO_PERIOD == backoff + 1
