@@ -1046,6 +1046,22 @@ int launch_rlc(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const ui
   if (nsub > Context::kSub) nsub = Context::kSub;
   if (nsub < 1) nsub = 1;
   const uint64_t win_per = (n_win + nsub - 1) / nsub;
+  // The sub-batches' window launches run side by side at one lane per window.  When their partial last waves push the
+  // total into one more round of waves than their full waves need (C5: 131,088 windows = 2 x 1,024.1 waves on 1,024
+  // SIMDs, a third ~30 ms round for 16 windows), those windows' items go straight to the per-item checks instead
+  // (k_rlc_window wdirect), which run in the fallback's tail.
+  bool direct = false;
+  {
+    uint64_t full = 0, all = 0;
+    for (int k = 0; k < nsub; ++k) {
+      const uint64_t w0 = win_per * k, w1 = w0 + win_per < n_win ? w0 + win_per : n_win;
+      if (w0 >= w1 || use_pairs(w1 - w0, kLg2MaxWindows)) continue;
+      full += (w1 - w0) / kBlock;
+      all += grid_for(w1 - w0);
+    }
+    const uint64_t S = wave_slots(c);
+    direct = all > S && (full + S - 1) / S < (all + S - 1) / S;
+  }
 
   rc = ws_begin(c, s, WS_RLC);
   if (rc) return rc;
@@ -1079,9 +1095,10 @@ int launch_rlc(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, const ui
       });
     else
       rc = timed(c, "rlc_window", ss, [&] {
+        const uint64_t wdirect = direct ? w0 + (w1 - w0) / kBlock * kBlock : w1;
         hipLaunchKernelGGL(k_rlc_window, dim3((unsigned)grid_for(w1 - w0)), dim3(kBlock), 0, ss, w0, w1, n, d_midx,
                            (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
-                           d_status, win, list + i0, cnt + k);
+                           d_status, win, list + i0, cnt + k, wdirect);
       });
     if (rc) return rc;
     // The list length is only known on the device: launch for the worst case, idle lanes exit.  The list is short
@@ -1398,9 +1415,12 @@ int launch_rlc_batch(Context& c, const uint8_t* d_pks, const uint8_t* d_sigs, co
     });
   else
     rc = timed(c, "rlc_window", s, [&] {
+      // as in launch_rlc: a partial last wave that would start another round goes straight to the per-item checks
+      const uint64_t S = wave_slots(c), full = n_win / kBlock, all = grid_for(n_win);
+      const uint64_t wdirect = all > S && (full + S - 1) / S < (all + S - 1) / S ? full * kBlock : n_win;
       hipLaunchKernelGGL(k_rlc_window, dim3((unsigned)grid_for(n_win)), dim3(kBlock), 0, s, (uint64_t)0, n_win, n,
                          d_midx, (const uint32_t*)rpk, (const uint32_t*)rsig, (const uint32_t*)d_H, hstride, d_hslot,
-                         d_status, win, list, cnt);
+                         d_status, win, list, cnt, wdirect);
     });
   if (rc) return rc;
   rc = launch_fallback(c, s, list, cnt, n, 1, d_pks, d_sigs, d_midx, d_H, hstride, d_hslot, d_status, d_kidx, T, tab,
@@ -3103,6 +3123,8 @@ int hipbls_rlc_stats(uint64_t* windows, uint64_t* windows_failed, uint64_t* item
       if (x > 0) {
         *windows_failed += 1;
         *items_fallback += (uint64_t)x;
+      } else if (x < 0) {  // a window sent straight to the per-item checks (k_rlc_window wdirect)
+        *items_fallback += (uint64_t)-x;
       }
   }
   return HIPBLS_OK;

@@ -799,6 +799,9 @@ __global__ void __launch_bounds__(kBlock) k_rlc_hash(const uint8_t* __restrict__
 // Stage 3: one lane per window of RLC_W items -> one multi-pairing check.  The items a failed window
 // leaves pending are appended to this sub-batch's fallback list (one atomic per failed window), so
 // stage 4 runs on a dense list instead of waking a wave for every scattered pending item.
+// Windows from wdirect on (the launches' partial last waves, when those would start another round of waves on a full
+// device: hipbls.hip launch_rlc) skip the check and send their pending items straight to stage 4, recorded as
+// win_fail[w] = -(items sent) so the statistics count them as re-checked items, not failed windows.
 __global__ void __launch_bounds__(kBlock) k_rlc_window(uint64_t w0, uint64_t w1, uint64_t n,
                                                        const uint32_t* __restrict__ msg_idx,
                                                        const uint32_t* __restrict__ rpk,
@@ -806,14 +809,22 @@ __global__ void __launch_bounds__(kBlock) k_rlc_window(uint64_t w0, uint64_t w1,
                                                        const uint32_t* __restrict__ H, uint64_t hstride,
                                                        const uint32_t* __restrict__ hslot,
                                                        int32_t* __restrict__ status, int32_t* __restrict__ win_fail,
-                                                       uint32_t* __restrict__ list, uint32_t* __restrict__ list_len) {
+                                                       uint32_t* __restrict__ list, uint32_t* __restrict__ list_len,
+                                                       uint64_t wdirect) {
   const uint64_t w = w0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (w >= w1) return;
-  BLS_LANE_F12(F);
-  const int left = rlc_window_lane(F, w, n, msg_idx, rpk, rsig, H, hstride, hslot, status, win_fail);
+  const uint64_t i1 = w * RLC_W + RLC_W < n ? w * RLC_W + RLC_W : n;
+  int left;
+  if (w >= wdirect) {
+    left = 0;
+    for (uint64_t i = w * RLC_W; i < i1; ++i) left += status[i] == RLC_PENDING ? 1 : 0;
+    win_fail[w] = -left;
+  } else {
+    BLS_LANE_F12(F);
+    left = rlc_window_lane(F, w, n, msg_idx, rpk, rsig, H, hstride, hslot, status, win_fail);
+  }
   if (left == 0) return;
   uint32_t at = atomicAdd(list_len, (uint32_t)left);
-  const uint64_t i1 = w * RLC_W + RLC_W < n ? w * RLC_W + RLC_W : n;
   for (uint64_t i = w * RLC_W; i < i1; ++i)
     if (status[i] == RLC_PENDING) list[at++] = (uint32_t)i;
 }

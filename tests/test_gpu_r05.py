@@ -351,3 +351,28 @@ def test_fav_octet_and_sixteen_lane_layouts_match_fav_batch(impl):
         impl.set_pair_mode(PAIR_AUTO)
         impl.lib.hipbls_set_timing(0)
 
+
+@pytest.mark.parametrize("rlc_mode", ["windows", "batch"])
+def test_c5_partial_wave_windows_go_to_item_checks(impl, rlc_mode):
+    """C5's 131,088 windows are 2 x 1,024.1 waves at one lane per window on 1,024 SIMDs: the two partial last waves'
+    windows (8 per sub-batch) skip the window check and their items go straight to the per-item checks
+    (kernels.h k_rlc_window wdirect), on the windows path and on a failed batch-wide check's windows.  Bitmap ==
+    construction; the statistics count those items as re-checked, not their windows as failed."""
+    import bench
+    from charon_amd.tbls import RLC_BATCH, RLC_WINDOWS
+    keys4 = bench.share_keys(impl, 4096, "c4")
+    pks, sigs, midx, roots, bad = bench.make_c4(impl, keys4, "c4i", 0, V, V, 0)
+    ppks, psigs, pmidx, proots, pbad = bench.make_c4(impl, bench.share_keys(impl, 128, "c5p"), "c5p", 0, 32, 32)
+    base, off = len(pks), len(roots)
+    pks, sigs, roots = pks + ppks, sigs + psigs, roots + proots
+    midx = midx + [m + off for m in pmidx]
+    bad = bad | {base + i for i in pbad}
+    prev = impl.set_rlc_mode({"windows": RLC_WINDOWS, "batch": RLC_BATCH}[rlc_mode])
+    try:
+        st = impl.batch_verify_rlc_status(pks, [roots[m] for m in midx], sigs, seed=bytes(range(32)))
+        assert {i for i, s in enumerate(st) if s != 0} == bad
+        w, wf, fb = impl.rlc_stats()
+        assert w == (len(pks) + 7) // 8
+        assert fb >= wf + 96  # >= 1 item per failed window + the direct windows' (16 windows, 128 items, few invalid)
+    finally:
+        impl.set_rlc_mode(prev)
