@@ -43,7 +43,8 @@ def test_patch_series_targets():
     touched = [f for p in PATCHES for f in _patched_files(p)]
     for f in ("tbls/tbls.go", "core/parsigex/parsigex.go", "core/validatorapi/validatorapi.go", "core/sigagg/sigagg.go",
               "core/eth2signeddata.go", "app/app.go", "app/featureset/featureset.go", "tbls/hipbls/hipbls.go",
-              "tbls/hipbls/batch.go", "tbls/hipbls_suite_test.go", "eth2util/signing/signing.go", "cluster/lock.go"):
+              "tbls/hipbls/batch.go", "tbls/hipbls_suite_test.go", "eth2util/signing/signing.go", "cluster/lock.go",
+              "dkg/dkg.go", "dkg/bulkverify.go"):
         assert f in touched, f
 
 
@@ -94,6 +95,24 @@ def test_patch_series_applies_to_reference(tmp_path):
         assert "c.verifyPartialSig(" not in body, fn
         assert "core.VerifyEth2SignedData(" not in body and "signing.VerifyAggregateAndProofSelection(" not in body, fn
         assert body.count("core.FirstFailure(ctx, c.eth2Cl, steps)") == 1, fn
+    # SubmitValidatorRegistrations: one StepErrors batch, no per-registration verify left
+    body = va[va.index("func (c Component) SubmitValidatorRegistrations("):]
+    body = body[:body.index("\n}\n")]
+    assert "c.verifyPartialSig(" not in body and "submitRegistration(" not in body
+    assert body.count("core.StepErrors(ctx, c.eth2Cl, steps)") == 1 and "c.registrationStep(ctx, registration)" in body
+    assert "func (c Component) submitRegistration(" not in va
+    step = va[va.index("func (c Component) registrationStep("):]
+    step = step[:step.index("\n}\n")]
+    assert "c.verifyPartialSig(" not in step and "c.partialSigStep(ctx, signedData, pubkey)" in step
+    # the single-signature requests are the only verifyPartialSig callers left
+    callers = set()
+    for m in re.finditer(r"^func \(c Component\) (\w+)\(", va, flags=re.M):
+        fbody = va[m.start():]
+        fbody = fbody[:fbody.index("\n}\n")]
+        if "c.verifyPartialSig(" in fbody:
+            callers.add(m.group(1))
+    assert callers == {"BeaconBlockProposal", "SubmitBeaconBlock", "BlindedBeaconBlockProposal",
+                       "SubmitBlindedBeaconBlock", "SubmitVoluntaryExit"}, callers
     # app: the resident pubshare table loaded from the lock's shares, fused sigagg
     app = open(tmp_path / "app" / "app.go").read()
     assert "tbls.LoadPubShares(pubShareTable)" in app and "sigagg.NewFused(" in app
@@ -101,6 +120,22 @@ def test_patch_series_applies_to_reference(tmp_path):
     lk = open(tmp_path / "cluster" / "lock.go").read()
     assert "tbls.BatchVerifyAggregate(aggKeys, aggSigs, aggMsgs)" in lk and "func VerifyLocksSignatures(" in lk
     assert "tbls.BatchVerify(regs.pks, regs.msgs, regs.sigs)" in lk
+    # the bulk lock check has a behavioural Go test against the serial VerifySignatures
+    lt = open(tmp_path / "cluster" / "lock_bulk_test.go").read()
+    assert "cluster.VerifyLocksSignatures(cases)" in lt and "lock.VerifySignatures()" in lt
+    # DKG: no per-partial tbls.Verify / per-DV ThresholdAggregate left in the three loops; one
+    # BatchVerifyRLC of every partial and one BatchThresholdAggregateVerify of every DV
+    dkg = open(tmp_path / "dkg" / "dkg.go").read()
+    for fn in ("aggLockHashSig", "aggDepositData", "aggValidatorRegistrations"):
+        body = dkg[dkg.index("func %s(" % fn):]
+        body = body[:body.index("\n}\n")]
+        assert "tbls.Verify(" not in body and "tbls.ThresholdAggregate(" not in body, fn
+        assert body.count("firstFailure(steps)") + body.count("aggregateVerified(steps, dvs,") == 1, fn
+    bv = open(tmp_path / "dkg" / "bulkverify.go").read()
+    assert bv.count("tbls.BatchVerifyRLC(pks, sigs, msgIdx, msgs)") == 1
+    assert bv.count("tbls.BatchThresholdAggregateVerify(groups, dvPks, msgs)") == 1
+    assert "aggDepositData(partials(bad, depositRoot), shares, msgs, network)" in open(
+        tmp_path / "dkg" / "bulkverify_internal_test.go").read()
 
 
 # gofmt'd reference files the indentation rule does not model (a multi-value return of two function literals)
