@@ -399,7 +399,9 @@ def main():
             dist.init_process_group(backend=backend)
 
     from charon_amd.shard import gather_aggregates, gather_bitmap_rows, gather_node_bitmap, shard_range, unpack_bitmap
+    from charon_amd import build as hb
     from charon_amd.tbls import RLC_AUTO, RLC_BATCH, RLC_WINDOWS, HipBLS, load_library
+    build_src = hb.verify()  # the binary measured is the one built from the sources beside it
     impl = HipBLS(device=local_dev)
     lib = load_library()
     lib.hipbls_set_timing(1)  # per-kernel HIP events for the roofline (off by default in the library)
@@ -935,6 +937,7 @@ def main():
                                    "distinct messages" % args.n,
                        "items_per_gpu": args.n, "node_items": n_node,
                        "parallelism": "shard-by-validator-index x %d (RCCL all-gather of the verify bitmaps)" % world},
+            "build_src_sha": build_src,
             "pairings_per_s": round(2 * value, 1),
             "drop_in_latency": latency,
             "host_path": host_path,

@@ -439,7 +439,13 @@ int scratch_reserve(const hipStream_t* ss, int n, uint64_t per_lane) {
       break;
     }
   }
-  if (!fn) return HIPBLS_OK;  // deeper than the largest reserve kernel: blocks grow on first use as before
+  if (!fn) {
+    // deeper than the largest reserve kernel: the queues' blocks would grow on first use, the round-4 abort's
+    // precondition, so refuse the device (the build budget, charon_amd/codeobj.py, keeps this from happening)
+    g_last_error = "scratch: the deepest kernel needs " + std::to_string(per_lane) +
+                   " B per lane, more than the largest reserve kernel";
+    return HIPBLS_ERR_DEVICE;
+  }
   void* args[2];
   uint32_t* none = nullptr;
   uint32_t zero = 0;
@@ -508,6 +514,13 @@ int init_locked(const std::vector<int>& ids) {
     // GPU_MAX_HW_QUEUES normal-priority queues that could all carry the library's kernels through callers' streams
     // must fit as well; otherwise every *_device call runs on the library's own streams (StreamJoin).
     if (sb.limit && (uint64_t)sb.queues * sb.per_queue > sb.limit) g_join_all = true;
+    if (!sb.limit) {
+      // no scratch limit to check against (no HSA query on this runtime): fail safe, and say so
+      g_join_all = true;
+      g_last_error = "scratch: device " + std::to_string(kv.first) +
+                     " reports no scratch limit; every *_device call runs on the library's streams";
+      fprintf(stderr, "hipbls: %s\n", g_last_error.c_str());
+    }
     const char* rs = getenv("HIPBLS_SCRATCH_RESERVE");
     if (!(rs && rs[0] == '0')) {
       rc = scratch_reserve(kv.second.data(), kStreamsPerDevice, sb.per_lane);
@@ -2499,6 +2512,18 @@ int hipbls_plan_ranges(uint64_t n, uint32_t parts, const uint32_t* run_keys, uin
 }
 
 const char* hipbls_last_error(void) { return g_last_error.c_str(); }
+
+// Build identity (charon_amd/build.py source_digest / flags_digest): a marker string the build script and the test,
+// smoke and bench entry points read from the .so's bytes and compare with the shipped sources.
+#ifndef HIPBLS_SRC_SHA
+#define HIPBLS_SRC_SHA "none"
+#endif
+#ifndef HIPBLS_FLAGS_SHA
+#define HIPBLS_FLAGS_SHA "none"
+#endif
+extern "C" __attribute__((used, visibility("default"))) const char hipbls_build_id_mark[] =
+    "HIPBLS_BUILD_ID src=" HIPBLS_SRC_SHA " flags=" HIPBLS_FLAGS_SHA;
+const char* hipbls_build_id(void) { return hipbls_build_id_mark + sizeof("HIPBLS_BUILD_ID ") - 1; }
 
 int hipbls_set_timing(int enabled) {
   g_timing = enabled != 0;

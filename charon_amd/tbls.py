@@ -122,6 +122,7 @@ def load_library(path: str = _LIB_PATH) -> ctypes.CDLL:
         "hipbls_kernel_names": ([], ctypes.c_char_p),
         "hipbls_queue_worker_stats": ([u64p, u64p], ctypes.c_int),
         "hipbls_set_latency_replicas": ([ctypes.c_uint32], ctypes.c_int),
+        "hipbls_build_id": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -150,8 +151,14 @@ def exported_symbols() -> List[str]:
         "hipbls_threshold_aggregate_verify_batch_device", "hipbls_init_devices", "hipbls_device_slots",
         "hipbls_plan_ranges", "hipbls_queue_keyed_batches", "hipbls_deserialize_status", "hipbls_device_streams",
         "hipbls_rlc_set_g1_msm_min", "hipbls_scratch_budget", "hipbls_stream_joins", "hipbls_kernel_names",
-        "hipbls_queue_worker_stats", "hipbls_set_latency_replicas",
+        "hipbls_queue_worker_stats", "hipbls_set_latency_replicas", "hipbls_build_id",
     ]
+
+
+def build_id() -> dict:
+    """The digests compiled into the loaded library (hipbls_build_id): {"src": sha256, "flags": sha256}."""
+    raw = load_library().hipbls_build_id().decode()
+    return dict(kv.split("=", 1) for kv in raw.split())
 
 
 def plan_ranges(n: int, parts: int, run_keys: Optional[Sequence[int]] = None) -> List[int]:

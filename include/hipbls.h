@@ -98,8 +98,12 @@ int hipbls_scratch_budget(int device, uint64_t* per_lane, uint64_t* per_queue, u
 int hipbls_stream_joins(uint64_t* calls);
 /* Space-separated names of every kernel the library can launch (no GPU needed; the scratch budget's kernel set). */
 const char* hipbls_kernel_names(void);
-/* Thread-local text of the last HIPBLS_ERR_DEVICE / HIPBLS_ERR_ARG. */
+/* Thread-local text of the last HIPBLS_ERR_DEVICE / HIPBLS_ERR_ARG (and, after an init on a runtime without a
+ * scratch-limit query, the note that every *_device call runs on the library's streams). */
 const char* hipbls_last_error(void);
+/* "src=<sha256> flags=<sha256>": digests of the sources and compile flags the library was built from
+ * (charon_amd/build.py); smoke(), the GPU test session and bench.py compare them with the shipped sources. */
+const char* hipbls_build_id(void);
 /* Device index the library is bound to (-1 before the first call). */
 int hipbls_current_device(void);
 /* Per-kernel HIP-event timing (hipbls_kernel_timing); off by default, or HIPBLS_TIMING=1 in the environment. */

@@ -33,20 +33,25 @@ func (HipBLS) BatchVerify(pks []tbls.PublicKey, msgs [][]byte, sigs []tbls.Signa
 	flat, offs := flatten(msgs)
 	status := make([]int32, n)
 	var rc C.int
-	if kidx, ok := tableIndices(pks); ok { // keys by resident table index: no per-call decode or subgroup test
+	path := "batch_verify"
+	kidx, keyed, release := lockTable(pks) // held across the call: a reload cannot swap the table under the indices
+	if keyed { // keys by resident table index: no per-call decode or subgroup test
+		path = "batch_verify_keys"
 		rc = C.hipbls_verify_batch_keys((*C.uint32_t)(unsafe.Pointer(&kidx[0])), u8(flat), u64(offs),
 			(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), C.uint64_t(n), i32(status))
 	} else {
 		rc = C.hipbls_verify_batch((*C.uint8_t)(unsafe.Pointer(&pks[0][0])), u8(flat), u64(offs),
 			(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), C.uint64_t(n), i32(status))
 	}
+	release()
 	if rc != C.HIPBLS_OK {
-		return nil, devErr(rc)
+		return nil, observeFailure(path, n, devErr(rc))
 	}
 	errs := make([]error, n)
 	for i, s := range status {
 		errs[i] = verifyErr(s, pks[i][:], sigs[i][:])
 	}
+	observe(path, errs)
 
 	return errs, nil
 }
@@ -70,7 +75,10 @@ func (HipBLS) BatchVerifyRLC(pks []tbls.PublicKey, sigs []tbls.Signature, msgIdx
 	}
 	status := make([]int32, n)
 	var rc C.int
-	if kidx, ok := tableIndices(pks); ok { // keys by resident table index
+	path := "batch_verify_rlc"
+	kidx, keyed, release := lockTable(pks) // held across the call, as in BatchVerify
+	if keyed { // keys by resident table index
+		path = "batch_verify_rlc_keys"
 		rc = C.hipbls_batch_verify_rlc_keys((*C.uint32_t)(unsafe.Pointer(&kidx[0])),
 			(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), (*C.uint32_t)(unsafe.Pointer(&msgIdx[0])), C.uint64_t(n), u8(flat),
 			u64(offs), C.uint64_t(len(msgs)), u8(seed[:]), i32(status))
@@ -79,13 +87,16 @@ func (HipBLS) BatchVerifyRLC(pks []tbls.PublicKey, sigs []tbls.Signature, msgIdx
 			(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), (*C.uint32_t)(unsafe.Pointer(&msgIdx[0])), C.uint64_t(n), u8(flat),
 			u64(offs), C.uint64_t(len(msgs)), u8(seed[:]), i32(status))
 	}
+	release()
 	if rc != C.HIPBLS_OK {
-		return nil, devErr(rc)
+		return nil, observeFailure(path, n, devErr(rc))
 	}
 	errs := make([]error, n)
 	for i, s := range status {
 		errs[i] = verifyErr(s, pks[i][:], sigs[i][:])
 	}
+	observe(path, errs)
+	observeRLC()
 
 	return errs, nil
 }
@@ -130,12 +141,13 @@ func (HipBLS) BatchThresholdAggregate(groups []map[int]tbls.Signature) ([]tbls.S
 	rc := C.hipbls_threshold_aggregate_batch(u8(sigs), i64(ids), u64(offs), C.uint64_t(len(groups)),
 		(*C.uint8_t)(unsafe.Pointer(&out[0][0])), i32(status))
 	if rc != C.HIPBLS_OK {
-		return nil, nil, devErr(rc)
+		return nil, nil, observeFailure("threshold_aggregate", len(groups), devErr(rc))
 	}
 	errs := make([]error, len(groups))
 	for g, s := range status {
 		errs[g] = aggErr(s)
 	}
+	observe("threshold_aggregate", errs)
 
 	return out, errs, nil
 }
@@ -163,7 +175,7 @@ func (h HipBLS) BatchVerifyAggregate(keys [][]tbls.PublicKey, sigs []tbls.Signat
 	rc := C.hipbls_verify_aggregate_batch(u8(flatKeys), u64(koffs), C.uint64_t(g),
 		(*C.uint8_t)(unsafe.Pointer(&sigs[0][0])), u8(flat), u64(moffs), i32(status))
 	if rc != C.HIPBLS_OK {
-		return nil, devErr(rc)
+		return nil, observeFailure("batch_verify_aggregate", g, devErr(rc))
 	}
 	errs := make([]error, g)
 	for i, s := range status {
@@ -177,6 +189,7 @@ func (h HipBLS) BatchVerifyAggregate(keys [][]tbls.PublicKey, sigs []tbls.Signat
 			errs[i] = errors.New("signature verification failed")
 		}
 	}
+	observe("batch_verify_aggregate", errs)
 
 	return errs, nil
 }
@@ -204,7 +217,7 @@ func (HipBLS) BatchThresholdAggregateVerify(groups []map[int]tbls.Signature, dvP
 		(*C.uint8_t)(unsafe.Pointer(&dvPks[0][0])), u8(flat), u64(moffs), (*C.uint8_t)(unsafe.Pointer(&out[0][0])),
 		i32(ast), i32(vst))
 	if rc != C.HIPBLS_OK {
-		return nil, nil, nil, devErr(rc)
+		return nil, nil, nil, observeFailure("fused_sigagg", n, devErr(rc))
 	}
 	aggErrs := make([]error, n)
 	verErrs := make([]error, n)
@@ -216,6 +229,7 @@ func (HipBLS) BatchThresholdAggregateVerify(groups []map[int]tbls.Signature, dvP
 			verErrs[g] = verifyErr(vst[g], dvPks[g][:], out[g][:])
 		}
 	}
+	observe("fused_sigagg", verErrs)
 
 	return out, aggErrs, verErrs, nil
 }

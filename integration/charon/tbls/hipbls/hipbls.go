@@ -151,23 +151,25 @@ func (HipBLS) LoadPubShares(pubshares []tbls.PublicKey) error {
 	return nil
 }
 
-// tableIndices returns every key's index in the resident pubshare table, or false when one is not in it.
-func tableIndices(pks []tbls.PublicKey) ([]uint32, bool) {
+// lockTable returns every key's index in the resident pubshare table (ok false when one is not in it) and holds the
+// table's read lock until release is called.  The keyed C call must run before release: a concurrent LoadPubShares
+// replaces the device table, and an index resolved against the old table would then name another key (ADVICE r05).
+// Readers share the lock, so batch calls still run side by side; only a reload waits for them.
+func lockTable(pks []tbls.PublicKey) (kidx []uint32, ok bool, release func()) {
 	pubShareIndex.RLock()
-	defer pubShareIndex.RUnlock()
 	if len(pubShareIndex.idx) == 0 {
-		return nil, false
+		return nil, false, pubShareIndex.RUnlock
 	}
 	out := make([]uint32, len(pks))
 	for i, k := range pks {
-		j, ok := pubShareIndex.idx[k]
-		if !ok {
-			return nil, false
+		j, found := pubShareIndex.idx[k]
+		if !found {
+			return nil, false, pubShareIndex.RUnlock
 		}
 		out[i] = j
 	}
 
-	return out, true
+	return out, true, pubShareIndex.RUnlock
 }
 
 func devErr(rc C.int) error {
@@ -394,10 +396,12 @@ func (HipBLS) Sign(privateKey tbls.PrivateKey, data []byte) (tbls.Signature, err
 func (HipBLS) Verify(pk tbls.PublicKey, data []byte, sig tbls.Signature) error {
 	var status C.int32_t
 	if rc := C.hipbls_verify(u8(pk[:]), u8(data), C.uint64_t(len(data)), u8(sig[:]), &status); rc != C.HIPBLS_OK {
-		return devErr(rc)
+		return observeFailure("verify", 1, devErr(rc))
 	}
+	err := verifyErr(int32(status), pk[:], sig[:])
+	observeOne("verify", err)
 
-	return verifyErr(int32(status), pk[:], sig[:])
+	return err
 }
 
 // ThresholdAggregate (tbls/herumi.go:244-283): ids are the map keys as Fr elements (int64 mod r); one group of the
@@ -429,8 +433,9 @@ func (HipBLS) VerifyAggregate(shares []tbls.PublicKey, sig tbls.Signature, data 
 	status := make([]int32, 1)
 	if rc := C.hipbls_verify_aggregate(u8(keys), C.uint64_t(len(shares)), u8(sig[:]), u8(data), C.uint64_t(len(data)),
 		i32(status)); rc != C.HIPBLS_OK {
-		return devErr(rc)
+		return observeFailure("verify_aggregate", 1, devErr(rc))
 	}
+	observeStatus("verify_aggregate", 1, status[0] != C.HIPBLS_OK)
 	switch C.int32_t(status[0]) {
 	case C.HIPBLS_OK:
 		return nil
@@ -457,8 +462,9 @@ func (HipBLS) Aggregate(signs []tbls.Signature) (tbls.Signature, error) {
 	var out tbls.Signature
 	status := make([]int32, 1)
 	if rc := C.hipbls_aggregate(u8(flat), C.uint64_t(len(signs)), u8(out[:]), i32(status)); rc != C.HIPBLS_OK {
-		return tbls.Signature{}, devErr(rc)
+		return tbls.Signature{}, observeFailure("aggregate", len(signs), devErr(rc))
 	}
+	observeStatus("aggregate", len(signs), status[0] != C.HIPBLS_OK)
 	if status[0] != C.HIPBLS_OK {
 		i := firstBad(flat, len(signs), 2)
 		if i < 0 {

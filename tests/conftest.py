@@ -38,6 +38,13 @@ def pytest_collection_modifyitems(session, config, items):
     seen once after the RLC tests ran first).  Initializing torch up front gives every GPU session bench.py's order."""
     if not any(item.get_closest_marker("gpu") for item in items):
         return
+    # the library the GPU tests load must be built from the sources beside it (VERDICT r05 next 3): the box runs the
+    # pushed binary, so a stale one would test other code than HEAD's
+    from charon_amd import build
+    try:
+        build.verify()
+    except RuntimeError as e:
+        raise pytest.UsageError(str(e))
     try:
         import torch
         if torch.cuda.is_available():

@@ -11,6 +11,11 @@ and cites the reference file:line it was taken from.
              (cluster/lock.go:144-189 FastAggregateVerify over all pubshares on lock_hash;
               cluster/lock.go:228-274 builder registrations = ThresholdAggregate outputs, Verify
               against the DV root key)
+  manifest   cluster/manifest/testdata/lock2.json, lock.json via cluster/manifest/load_test.go:31,77
+             (lock2: FastAggregateVerify of signature_aggregate over its 12 pubshares on lock_hash;
+              lock: the deposit_data signatures, threshold-aggregated by the DKG (dkg/dkg.go aggDepositData),
+              verified under each DV key with the deposit domain of the definition's fork version.  lock.json's own
+              aggregate and registrations do not verify and no reference test says they should: not vectors)
 """
 import base64
 import json
@@ -79,6 +84,23 @@ def main():
                       "lock_hash": _b(d["lock_hash"]), "signature_aggregate": _b(d["signature_aggregate"]),
                       "validators": vals})
     kat["locks"] = locks
+
+    # 5. cluster/manifest testdata (round 6)
+    path = "cluster/manifest/testdata/lock2.json"
+    d = json.load(open(os.path.join(REF, path)))
+    man = {"lock2": {"cite": path + " (cluster/manifest/load_test.go:77)",
+                     "lock_hash": _b(d["lock_hash"]), "signature_aggregate": _b(d["signature_aggregate"]),
+                     "public_shares": [_b(s) for v in d["distributed_validators"] for s in v["public_shares"]]}}
+    path = "cluster/manifest/testdata/lock.json"
+    d = json.load(open(os.path.join(REF, path)))
+    man["lock_deposits"] = {"cite": path + " (cluster/manifest/load_test.go:31)",
+                            "fork_version": d["cluster_definition"]["fork_version"][2:],
+                            "deposit_data": [{"pubkey": _b(v["deposit_data"]["pubkey"]),
+                                              "withdrawal_credentials": _b(v["deposit_data"]["withdrawal_credentials"]),
+                                              "amount": int(v["deposit_data"]["amount"]),
+                                              "signature": _b(v["deposit_data"]["signature"])}
+                                             for v in d["distributed_validators"]]}
+    kat["manifest"] = man
 
     with open(OUT, "w") as f:
         json.dump(kat, f, indent=1)

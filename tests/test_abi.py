@@ -99,3 +99,25 @@ def test_plan_ranges_tiles_exactly():
         keys4 = [i // 4 for i in range(4 * 1000)]
         b4 = plan_ranges(4000, 8, keys4)
         assert all(x % 4 == 0 for x in b4)
+
+
+def test_build_id_is_the_shipped_sources():
+    """The in-tree library carries the digests of the sources and default flags it was built from (VERDICT r05 next
+    3), both in its bytes (read without loading) and through hipbls_build_id()."""
+    from charon_amd import build, tbls
+    assert build.embedded_id() == (build.source_digest(), build.flags_digest())
+    assert tbls.build_id() == {"src": build.source_digest(), "flags": build.flags_digest()}
+    assert build.verify() == build.source_digest()
+
+
+def test_build_id_detects_other_sources(tmp_path, monkeypatch):
+    from charon_amd import build
+    fake = tmp_path / "lib.so"
+    fake.write_bytes(b"\x7fELF...HIPBLS_BUILD_ID src=" + b"0" * 64 + b" flags=" + b"1" * 64 + b"\0tail")
+    assert build.embedded_id(str(fake)) == ("0" * 64, "1" * 64)
+    assert build.stale(str(fake))
+    with pytest.raises(RuntimeError, match="other sources"):
+        build.verify(str(fake))
+    (tmp_path / "none.so").write_bytes(b"\x7fELF no id")
+    with pytest.raises(RuntimeError, match="no build id"):
+        build.verify(str(tmp_path / "none.so"))

@@ -226,6 +226,27 @@ def test_every_implementation_method_bound():
         assert re.search(r"^func \((?:\w+ )?HipBLS\) " + m + r"\(", batch, flags=re.M), m
 
 
+def test_engine_metrics_registered_and_observed():
+    """SURVEY §5 / VERDICT r05 next 6: promauto metrics in the binding, and every batch entry point records its call."""
+    d = os.path.join(INT, "charon", "tbls", "hipbls")
+    m = open(os.path.join(d, "metrics.go")).read()
+    for name in ("items_total", "failed_items_total", "batch_size", "device_errors_total", "rlc_windows_total",
+                 "rlc_windows_failed_total", "rlc_fallback_items_total"):
+        assert re.search(r'promauto\.New\w+\(prometheus\.\w+Opts\{\n(?:\t\t[^\n]*\n)*?\t\tName:\s+"%s"' % name, m), name
+    assert '"github.com/obolnetwork/charon/app/promauto"' in m
+    assert "C.hipbls_rlc_stats(" in m
+    src = open(os.path.join(d, "batch.go")).read() + open(os.path.join(d, "hipbls.go")).read()
+    for fn in ("BatchVerify", "BatchVerifyRLC", "BatchThresholdAggregate", "BatchVerifyAggregate",
+               "BatchThresholdAggregateVerify", "Verify", "VerifyAggregate", "Aggregate"):
+        body = src[re.search(r"^func \((?:\w+ )?HipBLS\) %s\(" % fn, src, flags=re.M).start():]
+        body = body[:body.index("\n}\n")]
+        assert re.search(r"\bobserve(One|Status)?\(", body), fn  # results recorded
+        assert body.count("devErr(rc)") == body.count("observeFailure("), fn  # every device failure counted
+    assert "observeRLC()" in src
+    t = open(os.path.join(d, "internal_test.go")).read()
+    assert "func TestMetricsCountEveryEntryPoint(" in t and "func TestReloadWaitsForKeyedCalls(" in t
+
+
 def test_error_texts_are_herumis():
     """The error texts the cgo package returns for a Verify status (hipbls.go verifyErr / deserErr) and the Python
     mirror's (charon_amd/tbls.py VERIFY_ERRORS) are the strings tbls.Herumi wraps and returns for the same input

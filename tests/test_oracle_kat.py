@@ -99,3 +99,26 @@ def test_threshold_roundtrip_matches_sign():
     parts = {i: bls.sign(shares[i], msg) for i in (1, 3, 5)}
     assert bls.threshold_aggregate(parts) == full
     assert bls.recover_secret({i: shares[i] for i in (2, 4, 5)}) == bls.sk_serialize(secret)
+
+
+def test_manifest_lock2_fast_aggregate_verify(kat):
+    """cluster/manifest/testdata/lock2.json (load_test.go:77): its aggregate over the 12 pubshares on lock_hash."""
+    m = kat["manifest"]["lock2"]
+    pks = [h(s) for s in m["public_shares"]]
+    assert len(pks) == 12
+    bls.verify_aggregate(pks, h(m["signature_aggregate"]), h(m["lock_hash"]))
+    with pytest.raises(bls.BLSError):
+        bls.verify_aggregate(pks[1:], h(m["signature_aggregate"]), h(m["lock_hash"]))
+
+
+def test_manifest_lock_deposit_signatures(kat):
+    """cluster/manifest/testdata/lock.json (load_test.go:31): the DKG's threshold-aggregated deposit signatures verify
+    under the DV keys over the deposit domain of fork 0x00001020."""
+    m = kat["manifest"]["lock_deposits"]
+    domain = ssz.compute_domain(ssz.DOMAIN_DEPOSIT, h(m["fork_version"]))
+    assert len(m["deposit_data"]) == 2
+    for dd in m["deposit_data"]:
+        root = ssz.signing_data_root(ssz.deposit_message_root(h(dd["pubkey"]), h(dd["withdrawal_credentials"]),
+                                                              dd["amount"]), domain)
+        assert bls.verify_status(h(dd["pubkey"]), root, h(dd["signature"])) == 0
+        assert bls.verify_status(h(dd["pubkey"]), root[::-1], h(dd["signature"])) == 3
