@@ -259,7 +259,9 @@ __device__ __attribute__((used, noinline)) static void bls_fp_asm_routines() {
 #define BLS_LAZY_FP6 0
 #endif
 #if BLS_LAZY_FP6 && !BLS_FP2_PAIR
-// The lazy-reduction experiment's routines (tools/gen_fp_asm.py gen_fp2_mul2 / gen_fp2_mul3).
+// The lazy-reduction experiment's routines (tools/gen_fp_asm.py gen_fp2_mul2 / gen_fp2_mul3),
+// generated on demand: `python3 charon_amd/tools/gen_fp_asm.py --lazy` writes the header below.
+#include "../tools/fp_asm_lazy_gfx950.h"
 __device__ __attribute__((used, noinline)) static void bls_fp2_lazy_routines() {
   asm volatile("s_endpgm\n.p2align 6\n.type bls_fp2_mul2_rt,@function\nbls_fp2_mul2_rt:\n\t" BLS_FP2_MUL2_ASM_BODY
                "\n\ts_setpc_b64 s[30:31]\n"

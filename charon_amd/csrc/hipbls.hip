@@ -2026,7 +2026,10 @@ void queue_worker(Context* cp) {
       if (sl.rc == HIPBLS_OK) {
         const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - sl.launched).count();
         double& e = q.batch_us[size_class(sl.b->n())];
-        e = e > 0 ? 0.75 * e + 0.25 * us : us;
+        // The estimate follows a faster batch of the class at once and drifts up slowly: a measured time includes the
+        // slack of a poll deferred past the batch's real end, so an average of those kept serial n = 1 callers late
+        // for many batches after a change to a faster layout, fewer replicas or a race won early.
+        e = (e <= 0 || us < e) ? us : e + 0.05 * (us - e);
       }
       lk.unlock();
       const int rc = wire_finish(sl);
@@ -2209,9 +2212,31 @@ int tagg_verify_host(Context& c, const uint8_t* sigs, const int64_t* share_idx, 
   const int p = (int)(c.tvh_seq.fetch_add(1) & 1);
   Context::TvHostSlot& h = c.tvh[p];
   std::lock_guard<std::mutex> slot_lock(h.mu);
+  // The slot's pinned result buffers grow under the slot lock only, not the context lock: hipHostFree may wait for
+  // the device, and the other slot's call must keep enqueueing meanwhile.  This slot's previous call has
+  // completed (its event was waited on before the slot lock was released).
+  if (h.h_groups < n_groups) {
+    if (h.h_out) HIP_TRY(hipHostFree(h.h_out));
+    if (h.h_st) HIP_TRY(hipHostFree(h.h_st));
+    h.h_out = nullptr;
+    h.h_st = nullptr;
+    h.h_groups = 0;
+    HIP_TRY(hipHostMalloc((void**)&h.h_out, n_groups * 96, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&h.h_st, n_groups * 8, hipHostMallocDefault));
+    h.h_groups = n_groups;
+  }
   {
     std::lock_guard<std::mutex> lk(c.mu);
     const hipStream_t s = c.sub[p];
+    // Every early return below drains the slot's stream: nothing this call enqueued may still read the caller's host
+    // arrays once it returns (a failing copy after the first one used to return without a wait).
+    struct Drain {
+      hipStream_t s;
+      bool on;
+      ~Drain() {
+        if (on) (void)hipStreamSynchronize(s);
+      }
+    } drain{s, true};
     if (!h.done) HIP_TRY(hipEventCreateWithFlags(&h.done, hipEventDisableTiming));
     HIP_TRY(h.sig.ensure((n_parts ? n_parts : 1) * 96));
     HIP_TRY(h.ids.ensure((n_parts ? n_parts : 1) * 8));
@@ -2221,16 +2246,6 @@ int tagg_verify_host(Context& c, const uint8_t* sigs, const int64_t* share_idx, 
     HIP_TRY(h.moff.ensure((n_groups + 1) * 8));
     HIP_TRY(h.out.ensure(n_groups * 96));
     HIP_TRY(h.st.ensure(n_groups * 8));  // aggregate statuses, then verify statuses
-    if (h.h_groups < n_groups) {
-      if (h.h_out) HIP_TRY(hipHostFree(h.h_out));
-      if (h.h_st) HIP_TRY(hipHostFree(h.h_st));
-      h.h_out = nullptr;
-      h.h_st = nullptr;
-      h.h_groups = 0;
-      HIP_TRY(hipHostMalloc((void**)&h.h_out, n_groups * 96, hipHostMallocDefault));
-      HIP_TRY(hipHostMalloc((void**)&h.h_st, n_groups * 8, hipHostMallocDefault));
-      h.h_groups = n_groups;
-    }
     if (n_parts) {
       HIP_TRY(hipMemcpyAsync(h.sig.p, sigs, n_parts * 96, hipMemcpyHostToDevice, s));
       HIP_TRY(hipMemcpyAsync(h.ids.p, share_idx, n_parts * 8, hipMemcpyHostToDevice, s));
@@ -2244,13 +2259,11 @@ int tagg_verify_host(Context& c, const uint8_t* sigs, const int64_t* share_idx, 
     const int rc = launch_tagg_verify(c, (const uint8_t*)h.sig.p, (const int64_t*)h.ids.p, (const uint64_t*)h.off.p,
                                       n_groups, n_parts, (const uint8_t*)h.pk.p, (const uint8_t*)h.msg.p,
                                       (const uint64_t*)h.moff.p, (uint8_t*)h.out.p, ast, vst, s);
-    if (rc) {
-      (void)hipStreamSynchronize(s);  // nothing the failed call enqueued may still read the caller's host arrays
-      return rc;
-    }
+    if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(h.h_out, h.out.p, n_groups * 96, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(h.h_st, h.st.p, n_groups * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(h.done, s));
+    drain.on = false;  // the wait below (no lock held) covers the enqueued work
   }
   HIP_TRY(hipEventSynchronize(h.done));
   memcpy(out_sigs, h.h_out, n_groups * 96);

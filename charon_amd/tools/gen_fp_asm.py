@@ -943,9 +943,6 @@ def emit_header(path, bodies, extra=()):
     lines.append("#define BLS_FP2_MUL_HALF_ASM_CLOBBERS %s" % clob4)
     clob5 = ", ".join('"v%d"' % r for r in range(36, 76)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
     lines.append("#define BLS_FP2_SQR_HALF_ASM_CLOBBERS %s" % clob5)
-    clob6 = ", ".join('"v%d"' % r for r in list(range(48, 52)) + list(range(76, 88))) + ', "vcc", ' + \
-        ", ".join('"s%d"' % r for r in range(16, 29))
-    lines.append("#define BLS_FP2_MUL2_ASM_CLOBBERS %s" % clob6)
     for name, body in extra:
         lines.append("")
         lines.append("// %s: %d instructions, positional operands (see tools/gen_fp_asm.py)" % (name, len(body)))
@@ -958,20 +955,45 @@ def emit_header(path, bodies, extra=()):
         f.write("\n".join(lines) + "\n")
 
 
-def main():
+def emit_lazy_header(path):
+    """The lazy-reduction experiment's routines (gen_fp2_mul2 / gen_fp2_mul3; VERDICT r04 item 7, measured -1.8 % in
+    round 5 and off): ~7,300 lines that only a BLS_LAZY_FP6=1 build reads, so they are generated on demand
+    (`gen_fp_asm.py --lazy`) instead of shipping in the product header."""
+    lines = ["// GENERATED by charon_amd/tools/gen_fp_asm.py --lazy -- do not edit (BLS_LAZY_FP6=1 builds only).",
+             "#pragma once"]
+    for name, body in (("BLS_FP2_MUL2_ASM_BODY", gen_fp2_mul2()), ("BLS_FP2_MUL3_ASM_BODY", gen_fp2_mul3())):
+        lines.append("// %s: %d instructions" % (name, len(body)))
+        lines.append("#define %s \\" % name)
+        for k, ins in enumerate(body):
+            sep = "\\n\\t" if k + 1 < len(body) else ""
+            lines.append('  "%s%s" \\' % (ins, sep))
+        lines.append("")
+    clob6 = ", ".join('"v%d"' % r for r in list(range(48, 52)) + list(range(76, 88))) + ', "vcc", ' + \
+        ", ".join('"s%d"' % r for r in range(16, 29))
+    lines.append("#define BLS_FP2_MUL2_ASM_CLOBBERS %s" % clob6)
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def main(lazy=False):
     mul = gen_mul()
     check(mul, mont=1 << 384, canonical=True)
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "fp_asm_gfx950.h")
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(pkg, "csrc", "fp_asm_gfx950.h")
     fp2 = gen_fp2_mul()
     fp2s = gen_fp2_sqr()
     emit_header(path, [("BLS_FP_MUL_ASM_BODY", mul), ("BLS_FP2_MUL_ASM_BODY", fp2), ("BLS_FP2_SQR_ASM_BODY", fp2s),
                        ("BLS_FP2_MUL_HALF_ASM_BODY", gen_fp2_mul_half()),
-                       ("BLS_FP2_SQR_HALF_ASM_BODY", gen_fp2_sqr_half()),
-                       ("BLS_FP2_MUL2_ASM_BODY", gen_fp2_mul2()), ("BLS_FP2_MUL3_ASM_BODY", gen_fp2_mul3())],
+                       ("BLS_FP2_SQR_HALF_ASM_BODY", gen_fp2_sqr_half())],
                 extra=[("BLS_FP_ADD_ASM", gen_add()), ("BLS_FP_SUB_ASM", gen_sub()), ("BLS_FP_NEG_ASM", gen_sub(neg=True)),
                        ("BLS_FP_ADD_LAZY_ASM", gen_add_lazy()), ("BLS_FP_SUB_LAZY_ASM", gen_sub_lazy())])
     print("wrote %s: %d instructions" % (path, len(mul)))
+    if lazy:
+        lpath = os.path.join(pkg, "tools", "fp_asm_lazy_gfx950.h")
+        emit_lazy_header(lpath)
+        print("wrote %s" % lpath)
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    main(lazy="--lazy" in sys.argv)
