@@ -177,10 +177,16 @@ def make_c3(impl, g_lo, g_hi, t=7, n=10):
     return psigs, part_ids, offs, dv_pks, roots, secrets_
 
 
+# Invalid partials per 1,000 in the C4 / C5 batches (BASELINE's ~1 %: 10).  BENCH_C4_BAD_PER_MILLE changes it for the
+# fallback-size measurements of DESIGN.md 9 (round 6); the default line always uses 10.
+C4_BAD_PER_MILLE = int(os.environ.get("BENCH_C4_BAD_PER_MILLE", "10"))
+
+
 def c4_item(tag, v, j, nk, corrupt=True):
     """(owner key, bad?, kind) of partial j of validator v; corrupt=False: an all-valid node batch."""
     r = _hi(tag, v, j)
-    return r % nk, corrupt and (r >> 20) % 100 == 0, (r >> 40) & 1
+    bad = (r >> 20) % 100 == 0 if C4_BAD_PER_MILLE == 10 else (r >> 20) % 1000 < C4_BAD_PER_MILLE
+    return r % nk, corrupt and bad, (r >> 40) & 1
 
 
 def make_c4(impl, keys, tag, v_lo, v_hi, v_node, n_roots_node=0, shares=4, corrupt=True):
@@ -222,15 +228,16 @@ def c4_node_bad(tag, v_node, nk, shares=4, corrupt=True):
 
 
 def pmc_summary(path=None):
-    """k_verify_fused counters from the committed rocprofv3 --pmc passes over this build's bench (scripts/gpu_pmc_r04.sh
+    """k_verify_fused counters from the committed rocprofv3 --pmc passes over this build's bench (scripts/gpu_pmc.sh
     WL=c2, scripts/pmc_commit_r04.py): HBM bytes per launch (FETCH_SIZE + WRITE_SIZE), their ratio to the 188 B/verify
     of algorithmic input, VALU utilisation (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES at one wave per SIMD), the fraction
     of wave cycles spent waiting, VALU and 64-bit integer VALU (the v_mad_u64_u32 stream) instructions per wave, and
     the commit the counters were taken at.  {} when absent.  The newest round's passes are read."""
     if path is None:
-        path = os.path.join(ROOT, "profiles", "r05", "pmc_verify.json")
-        if not os.path.exists(path):
-            path = os.path.join(ROOT, "profiles", "r04", "pmc_verify.json")
+        for rnd in ("r06", "r05", "r04"):
+            path = os.path.join(ROOT, "profiles", rnd, "pmc_verify.json")
+            if os.path.exists(path):
+                break
     try:
         with open(path) as f:
             d = json.load(f)
@@ -241,6 +248,20 @@ def pmc_summary(path=None):
             "valu_insts_per_wave": d.get("valu_insts_per_wave"),
             "int64_valu_insts_per_wave": d.get("int64_valu_insts_per_wave"),
             "taken_at": d.get("taken_at"), "source": os.path.relpath(path, ROOT)}
+
+
+def attainable_products(path=None):
+    """The product routines' own rate on every SIMD (profiles/<round>/ceiling_probe.json, written from
+    charon_amd/tools/ceiling_probe's output); {} when absent."""
+    if path is None:
+        path = os.path.join(ROOT, "profiles", "r06", "ceiling_probe.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    d["source_file"] = os.path.relpath(path, ROOT)
+    return d
 
 
 def _cpu_model():
@@ -901,6 +922,30 @@ def main():
         torch.cuda.synchronize()
         impl.set_rlc_mode(RLC_AUTO)
         assert {i for i, x in enumerate(d_st5.cpu().tolist()) if x != 0} == bad5, "C5 bitmap mismatch (batch)"
+        t5k = None
+        if args.keys:  # the slot as charon runs it: every partial's key from the resident pubshare table (patch 0004)
+            table5 = list(dict.fromkeys(pks5))
+            pos5 = {k: j for j, k in enumerate(table5)}
+            assert set(impl.load_pubshares(table5)) <= {0}
+            d_k5 = torch.tensor([pos5[p] for p in pks5], dtype=torch.int32).to(dev)
+
+            def c5kstep():
+                if rank == 0 and c5_fav:
+                    rc = lib.hipbls_verify_aggregate_batch_device(d_spk.data_ptr(), 512, d_skoff.data_ptr(), 1,
+                                                                  d_ssig.data_ptr(), d_smsg.data_ptr(),
+                                                                  d_smoff.data_ptr(), d_sst.data_ptr(), sp_fav)
+                    assert rc == 0
+                rc = lib.hipbls_batch_verify_rlc_keys_device(d_k5.data_ptr(), d_sig5.data_ptr(), d_midx5.data_ptr(), n5,
+                                                             d_msg5.data_ptr(), d_off5.data_ptr(), len(roots5), seed5,
+                                                             d_st5.data_ptr(), sp)
+                assert rc == 0
+
+            c5kstep()
+            torch.cuda.synchronize()
+            t5k = timed_loop(c5kstep, args.rlc_steps, dev, barrier, world)
+            torch.cuda.synchronize()
+            assert {i for i, x in enumerate(d_st5.cpu().tolist()) if x != 0} == bad5, "C5 bitmap mismatch (table)"
+            del d_k5
         if world > 1:  # node-wide failure count == construction
             rows = node5[0]
             fails = sum(int((~unpack_bitmap(rows[r], c5_rows[r])).sum()) for r in range(world))
@@ -914,7 +959,8 @@ def main():
               "sync_aggregate_verifies_per_s": round(args.rlc_steps / t5, 3),
               "failed_batch_check_ms_per_slot": round(1000 * t5b / args.rlc_steps, 3),
               "auto_mode_amortized_ms_per_slot": round(1000 * ((RLC_AUTO_PERIOD - 1) * t5 + t5b)
-                                                       / (RLC_AUTO_PERIOD * args.rlc_steps), 3)}
+                                                       / (RLC_AUTO_PERIOD * args.rlc_steps), 3),
+              "ms_per_slot_pubshare_table": round(1000 * t5k / args.rlc_steps, 3) if t5k else None}
         del d_pk5, d_sig5, d_midx5, d_msg5, d_off5, d_st5
 
     if rank == 0:
@@ -985,6 +1031,18 @@ def main():
                 "kernel_avg_ms": round(k_ms, 3),
                 "kernel_launches": int(launches.value),
             }
+            # the attainable rate of this arithmetic on this chip: the shipped product
+            # routines alone on every SIMD at the kernel's occupancy, measured by charon_amd/tools/ceiling_probe.hip
+            ceil = attainable_products()
+            if ceil:
+                got = FPMUL_PER_VERIFY * n / (k_ms * 1e-3) / 1e9
+                out["roofline"]["attainable"] = {
+                    "g_products_per_s": ceil["attainable_g_products_per_s_one_wave"],
+                    "achieved_g_products_per_s": round(got, 2),
+                    "frac": round(got / ceil["attainable_g_products_per_s_one_wave"], 4),
+                    "note": "products/s of the product routines alone, one wave per SIMD (the kernel's occupancy); the "
+                            "nominal peak assumes every lane issues one 32x32->64 MAD per clock at 2.4 GHz",
+                    "source": ceil["source_file"]}
         if world == 1 and args.cpu_sample > 0:
             out["cpu_baseline"] = cpu_baseline(impl, (pks, roots, sigs, bad), args.cpu_sample, random.Random(SEED))
         print(json.dumps(out), flush=True)

@@ -8,6 +8,8 @@
 #   prof                  the default bench under rocprofv3 --kernel-trace --stats -> gpurun_out/<tag>_prof/
 #   rlc:<lib>:<name>      the C4(i) + C5 part of the bench with HIPBLS_LIB=<lib> (A/B of compile-time variants)
 #   pmc:<counters>:<name> one rocprofv3 --pmc pass over a short C2-only bench -> gpurun_out/<tag>_pmc_<name>/
+#   pmcset:<wl>           the five counter passes of scripts/gpu_pmc.sh for workload c2|c3|c4|lat -> gpurun_out/pmc6_<wl>/
+#   ceiling               charon_amd/tools/ceiling_probe (the product routines alone, every SIMD) -> <tag>_ceiling.txt
 #   py:<file>             python -u <file> (a probe script)                -> gpurun_out/<tag>_<basename>.log
 #
 # TAG (environment, default "run") prefixes every output.
@@ -54,6 +56,14 @@ for step in "$@"; do
         -d "$O/${T}_pmc_${name}" -o run -- python3 -u "$R/bench.py" $C2_ARGS \
         > "$O/${T}_pmc_${name}.json" 2> "$O/${T}_pmc_${name}.err") \
         || { echo "pmc pass failed"; tail -20 "$O/${T}_pmc_${name}.err"; exit 1; } ;;
+    pmcset:*)
+      WL=${step#pmcset:} bash scripts/gpu_pmc.sh > "$O/${T}_pmcset_${step#pmcset:}.log" 2>&1 \
+        || { echo "pmc set failed"; tail -20 "$O/${T}_pmcset_${step#pmcset:}.log"; exit 1; }
+      tail -1 "$O/${T}_pmcset_${step#pmcset:}.log" ;;
+    ceiling)
+      timeout -k 10 300 charon_amd/tools/ceiling_probe > "$O/${T}_ceiling.txt" 2>&1 \
+        || { echo "ceiling probe failed"; tail -20 "$O/${T}_ceiling.txt"; exit 1; }
+      cat "$O/${T}_ceiling.txt" ;;
     py:*)
       f=${step#py:}
       timeout -k 10 600 python -u "$f" > "$O/${T}_$(basename "$f" .py).log" 2>&1 \

@@ -26,7 +26,7 @@ def main(rev, rnd="r04", prefix="pmc_"):
         if not os.path.exists(src):
             continue
         d = json.load(open(src))
-        script = "scripts/gpu_pmc_r04.sh" if rnd == "r04" else "scripts/gpu_pmc_%s.sh" % rnd
+        script = {"r04": "scripts/gpu_pmc_r04.sh", "r05": "scripts/gpu_pmc_r05.sh"}.get(rnd, "scripts/gpu_pmc.sh")
         out = {"taken_at": rev, "workload": wl, "source": "%s WL=%s" % (script, wl), "kernels": {}}
         for k, v in sorted(d.items()):
             if isinstance(v, dict) and v.get("valu_insts_per_wave"):
