@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restri
   const uint64_t o0 = offs[i], o1 = offs[i + 1];
 #if BLS_VERIFY_LDS
   BLS_LANE_F12(F);
-  status[i] = op_verify_l(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i, F);
+  status[i] = op_verify_l_kernel(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i, F);
 #else
   status[i] = op_verify(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i);
 #endif

@@ -51,8 +51,9 @@ BLS_HD BLS_CALL int pairing_check_verify_sig(const g1a& pk, const g2a& hm, const
 #ifndef BLS_VERIFY_L_CALL
 #define BLS_VERIFY_L_CALL BLS_CALL
 #endif
-template <int S>
-BLS_HD BLS_VERIFY_L_CALL int pairing_check_verify_sig_l(const g1a& pk, const g2a& hm, const g2a& sig, const f12l<S> F) {
+// INL: the Miller loop inlined here (k_verify_fused's kernel-inlined chain, op_verify_l_kernel) or called.
+template <int S, bool INL>
+BLS_HD BLS_INLINE int pairing_check_verify_sig_l_body(const g1a& pk, const g2a& hm, const g2a& sig, const f12l<S> F) {
   g1a P1;
   P1.x = G1_GEN_X;
   P1.y = G1_NEG_GEN_Y;
@@ -60,12 +61,19 @@ BLS_HD BLS_VERIFY_L_CALL int pairing_check_verify_sig_l(const g1a& pk, const g2a
   bool in_g2;
   {
     g2j T1;
-    miller_loop_2_l<S, true>(f, F, pk, hm, P1, sig, &T1);
+    if (INL)
+      miller_loop_2_l_body<S, true>(f, F, pk, hm, P1, sig, &T1);
+    else
+      miller_loop_2_l<S, true>(f, F, pk, hm, P1, sig, &T1);
     in_g2 = g2_subgroup_from_miller(T1, sig);
   }
   final_exp_l(f, f, F);  // in place: one Fp12 less in this frame (final_exponentiation_l allows r == f_in)
   if (!in_g2) return HIPBLS_ERR_SIGNATURE;
   return fp12_is_one(f) ? HIPBLS_OK : HIPBLS_ERR_VERIFY;
+}
+template <int S>
+BLS_HD BLS_VERIFY_L_CALL int pairing_check_verify_sig_l(const g1a& pk, const g2a& hm, const g2a& sig, const f12l<S> F) {
+  return pairing_check_verify_sig_l_body<S, false>(pk, hm, sig, F);
 }
 
 // Statuses for the infinity cases (herumi: a valid infinity key or signature fails KeyValidate / the check), once the
@@ -289,9 +297,9 @@ BLS_HD BLS_CALL int op_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t 
 }
 
 // op_verify with the Miller loop's f in LDS (F: this lane's slot; pairing_lds.h).
-template <int S>
-BLS_HD BLS_VERIFY_L_CALL int op_verify_l(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96,
-                                const f12l<S> F) {
+template <int S, bool INL>
+BLS_HD BLS_INLINE int op_verify_l_body(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96,
+                                     const f12l<S> F) {
   g1a pk;
   const int dp = g1_decompress(pk, pk48, true);
   if (dp == DEC_BAD) return HIPBLS_ERR_PUBKEY;
@@ -303,7 +311,19 @@ BLS_HD BLS_VERIFY_L_CALL int op_verify_l(const uint8_t* pk48, const uint8_t* msg
   hash_to_g2(hj, msg, msg_len, DST_POP, 43);
   g2a hm;
   jac_to_aff(hm, hj);
-  return pairing_check_verify_sig_l(pk, hm, sig, F);
+  return pairing_check_verify_sig_l_body<S, INL>(pk, hm, sig, F);
+}
+template <int S>
+BLS_HD BLS_VERIFY_L_CALL int op_verify_l(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96,
+                                const f12l<S> F) {
+  return op_verify_l_body<S, false>(pk48, msg, msg_len, sig96, F);
+}
+// k_verify_fused's form: the whole chain down to the Miller loop inlined into the kernel (pairing_lds.h
+// miller_loop_2_l_body); the final exponentiation and the other callees stay out of line.
+template <int S>
+BLS_HD BLS_INLINE int op_verify_l_kernel(const uint8_t* pk48, const uint8_t* msg, uint32_t msg_len, const uint8_t* sig96,
+                                         const f12l<S> F) {
+  return op_verify_l_body<S, true>(pk48, msg, msg_len, sig96, F);
 }
 
 BLS_HD BLS_CALL int op_sign(uint8_t* out96, const uint8_t* sk32, const uint8_t* msg, uint32_t msg_len) {

@@ -376,9 +376,13 @@ BLS_HD BLS_INLINE void park_agpr(T& x) {
 #endif
 // P1_NEG_GEN: P1 is -g1 (Verify's second pair), so its coordinates are immediates rematerialized at each use instead
 // of 24 registers live across the loop.
+// The loop's body is an inline function: miller_loop_2_l below is its out-of-line form (the RLC and keyed kernels call
+// it), and k_verify_fused inlines the body into the kernel itself (ops.h op_verify_l_kernel), where no callee-saved
+// register set applies: the loop then spills to all 256 AGPRs before scratch (225 scratch instructions per doubling
+// iteration instead of 275, C2 +0.5 %).
 template <int S, bool P1_NEG_GEN = false>
-BLS_HD BLS_MILLER_L_CALL void miller_loop_2_l(fp12& f_out, const f12l<S> F, const g1a& P0_in, const g2a& Q0, const g1a& P1_in,
-                                     const g2a& Q1, g2j* T1_out) {
+BLS_HD BLS_INLINE void miller_loop_2_l_body(fp12& f_out, const f12l<S> F, const g1a& P0_in, const g2a& Q0,
+                                          const g1a& P1_in, const g2a& Q1, g2j* T1_out) {
   g1a P0 = P0_in;
   g1a P1;
   if (P1_NEG_GEN) {
@@ -434,6 +438,11 @@ BLS_HD BLS_MILLER_L_CALL void miller_loop_2_l(fp12& f_out, const f12l<S> F, cons
   F.ld12(f);
   fp12_conj(f_out, f);
   if (T1_out) *T1_out = T1;
+}
+template <int S, bool P1_NEG_GEN = false>
+BLS_HD BLS_MILLER_L_CALL void miller_loop_2_l(fp12& f_out, const f12l<S> F, const g1a& P0_in, const g2a& Q0, const g1a& P1_in,
+                                     const g2a& Q1, g2j* T1_out) {
+  miller_loop_2_l_body<S, P1_NEG_GEN>(f_out, F, P0_in, Q0, P1_in, Q1, T1_out);
 }
 
 // f <- f b in place, b dense in registers (fp12_mul_inl): t0 = F0 b0, t1 = F1 b1; F0 + F1 overwrites F1, c0 = t0 + v t1

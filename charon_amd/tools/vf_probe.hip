@@ -19,5 +19,5 @@ __global__ void __launch_bounds__(kBlock) k_verify_fused(const uint8_t* __restri
   const uint64_t o0 = offs[i], o1 = offs[i + 1];
   __shared__ u32x4 s_f12_[36 * kBlock];
   const f12l<kBlock> F{(BLS_LDS u32x4*)&s_f12_[threadIdx.x]};
-  status[i] = op_verify_l(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i, F);
+  status[i] = op_verify_l_kernel(pks + 48 * i, msgs + o0, (uint32_t)(o1 - o0), sigs + 96 * i, F);
 }

@@ -16,10 +16,12 @@ from charon_amd import codeobj  # noqa: E402
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 DYN = {}
+MILLER = [0]
 
 
 def build(extra, out):
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I" + os.path.join(PKG, "csrc"),
+    csrc = os.environ.get("VF_CSRC") or os.path.join(PKG, "csrc")  # a modified copy of the sources (experiments)
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I" + csrc,
            "-I" + os.path.join(os.path.dirname(PKG), "include"), "-o", out, os.path.join(HERE, "vf_probe.hip")] + extra
     subprocess.check_call(cmd)
 
@@ -83,7 +85,21 @@ def summarize(lib):
                 lp = min(loops, key=lambda x: x[1] - x[0]) if key == "miller_loop_2_l" else big
                 inner = sum(1 for _, l in ins[lp[0]:lp[1]] if l.startswith("scratch_"))
                 DYN[name] = sc + (t - 1) * inner
+        if name not in DYN and loops:
+            # the Miller loop inlined into the kernel (op_verify_l_kernel): its doubling iteration is the smallest loop
+            # holding ~61 product calls
+            ml = [lp for lp in loops if 50 <= sum(1 for _, l in ins[lp[0]:lp[1]] if "swappc" in l) <= 70]
+            if ml:
+                lp = min(ml, key=lambda x: x[1] - x[0])
+                inner = sum(1 for _, l in ins[lp[0]:lp[1]] if l.startswith("scratch_"))
+                DYN[name] = sc + 61 * inner
+                MILLER[0] = DYN[name]
         DYN.setdefault(name, sc)
+        if os.environ.get("VF_LOOPS"):
+            for a0, a1 in sorted(set(loops)):
+                sub = ins[a0:a1]
+                print("   loop in %s: %d ins, %d scratch, %d swappc" % (name[:40], a1 - a0,
+                      sum(1 for _, l in sub if l.startswith("scratch_")), sum(1 for _, l in sub if "swappc" in l)))
     res = codeobj.resource_table(lib)
     return out, res
 
@@ -98,5 +114,5 @@ if __name__ == "__main__":
     for r in res:
         print("kernel", r)
     print("dynamic scratch estimate per Verify: %d (miller %d, karabina %d, cyc_sqr_run %d)" % (
-        sum(DYN.values()), sum(v for k, v in DYN.items() if "miller_loop_2_l" in k),
+        sum(DYN.values()), sum(v for k, v in DYN.items() if "miller_loop_2_l" in k) or MILLER[0],
         sum(v for k, v in DYN.items() if "karabina_l" in k), sum(v for k, v in DYN.items() if "cyc_sqr_run" in k)))
