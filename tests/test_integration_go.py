@@ -121,6 +121,10 @@ def test_patch_series_applies_to_reference(tmp_path):
     assert "tbls.BatchVerifyAggregate(aggKeys, aggSigs, aggMsgs)" in lk and "func VerifyLocksSignatures(" in lk
     assert "tbls.BatchVerify(regs.pks, regs.msgs, regs.sigs)" in lk
     # the bulk lock check has a behavioural Go test against the serial VerifySignatures
+    # ... and a real caller: charon combine verifies every node directory's lock copy in one bulk call
+    cb = open(tmp_path / "cmd" / "combine" / "combine.go").read()
+    assert cb.count("cluster.VerifyLocksSignatures(locks)") == 1 and "lockSignatureErrors(dir, root)" in cb
+    assert "lock.VerifySignatures()" in cb  # the fallback for a directory the bulk pass could not read
     lt = open(tmp_path / "cluster" / "lock_bulk_test.go").read()
     assert "cluster.VerifyLocksSignatures(cases)" in lt and "lock.VerifySignatures()" in lt
     # DKG: no per-partial tbls.Verify / per-DV ThresholdAggregate left in the three loops; one
