@@ -940,10 +940,12 @@ def main():
                                                              d_st5.data_ptr(), sp)
                 assert rc == 0
 
+            impl.set_rlc_mode(RLC_WINDOWS)  # the windows regime of a stream with invalid partials, as C4 (i) is timed
             c5kstep()
             torch.cuda.synchronize()
             t5k = timed_loop(c5kstep, args.rlc_steps, dev, barrier, world)
             torch.cuda.synchronize()
+            impl.set_rlc_mode(RLC_AUTO)
             assert {i for i, x in enumerate(d_st5.cpu().tolist()) if x != 0} == bad5, "C5 bitmap mismatch (table)"
             del d_k5
         if world > 1:  # node-wide failure count == construction
