@@ -640,6 +640,14 @@ def main():
                                                      (TAGG_FPMUL["pairing"] + TAGG_FPMUL["unscale"]) * G)}}
         if tagg2:
             tagg_roofline["frac_two_streams"] = round(unit * MADS_PER_FPMUL * (tagg2 / world) / 1e12 / MAD_PEAK_T, 4)
+        ceil = attainable_products()
+        if ceil:  # the product routines' own rate on every SIMD (roofline.attainable)
+            a = ceil["attainable_g_products_per_s_one_wave"]
+            tagg_roofline["attainable"] = {"g_products_per_s": a,
+                                           "achieved_g_products_per_s": round(unit * (tagg / world) / 1e9, 2),
+                                           "frac": round(unit * (tagg / world) / 1e9 / a, 4),
+                                           "frac_two_streams": round(unit * (tagg2 / world) / 1e9 / a, 4)
+                                           if tagg2 else None, "source": ceil["source_file"]}
 
     # ---- the host-buffer calls charon's Go side makes (INTEGRATION.md "What charon reaches"): tbls.BatchVerify ->
     # hipbls_verify_batch, or hipbls_verify_batch_keys once app loaded the pubshare table; sigagg.NewFused ->
