@@ -108,13 +108,17 @@ func TestReloadWaitsForKeyedCalls(t *testing.T) {
 	want, err := h.BatchVerify(pks, msgs, sigs)
 	require.NoError(t, err)
 
-	var wg sync.WaitGroup
+	var (
+		wg      sync.WaitGroup
+		loadErr error
+	)
 	wg.Add(1)
 	go func() {
 		defer wg.Done()
-		for k := 0; k < 20; k++ {
-			require.NoError(t, h.LoadPubShares(pks))
-			require.NoError(t, h.LoadPubShares(other))
+		for k := 0; k < 20 && loadErr == nil; k++ {
+			if loadErr = h.LoadPubShares(pks); loadErr == nil {
+				loadErr = h.LoadPubShares(other)
+			}
 		}
 	}()
 	for k := 0; k < 20; k++ {
@@ -125,6 +129,7 @@ func TestReloadWaitsForKeyedCalls(t *testing.T) {
 		}
 	}
 	wg.Wait()
+	require.NoError(t, loadErr)
 
 	require.NoError(t, h.LoadPubShares(nil))
 	_, ok, release := lockTable(pks)
