@@ -356,8 +356,11 @@ BLS_HD BLS_INLINE void fp12_mul_line_l(const f12l<S>& F, const fp2& g0_in, const
 // miller_loop_2 (pairing.h) with f in LDS; f_out and T1_out as there.
 // Register-allocation hint: x's dwords pass through an empty asm statement in accumulation registers, so the
 // allocator keeps a value that waits across a doubling step in AGPRs rather than in scratch.
+// Round 6: 6 (T0 and the first pair's line coefficients parked after its doubling step, P0 at the loop top). With
+// the loop inlined into k_verify_fused (op_verify_l_kernel) the parked values stay in AGPRs instead of scratch:
+// same-box A/B C2 1.854M -> 1.865M/s (profiles/r06/c2_park_ab.json; 2 alone +0.6 %, 4 alone +0.4 %).
 #ifndef BLS_ML_PARK
-#define BLS_ML_PARK 0
+#define BLS_ML_PARK 6
 #endif
 template <class T>
 BLS_HD BLS_INLINE void park_agpr(T& x) {
