@@ -1,9 +1,10 @@
 """Generate charon_amd/csrc/fp_asm_gfx950.h: the gfx950 Montgomery product as one asm routine.
 
 SHIPPED (gen_mul): radix 2^32, 12 limbs, product scanning (Comba) with the Montgomery reduction
-interleaved per column.  Every limb product is one v_mad_u64_u32 into a 64-bit column accumulator
-plus one v_addc_co_u32 catching the carry into a third word: 288 mads + 12 v_mul_lo_u32, canonical
-output (final conditional subtraction of p).  Registers are pinned (a = v[0:11] in/out, b = v[12:23])
+interleaved per column.  Every limb product is one v_mad_u64_u32 into a 64-bit column accumulator,
+plus one v_addc_co_u32 catching the carry into a third word unless the column's bound proves the
+accumulator cannot overflow there (carry elision, _comba: 74 of the 288 carries), + 12 v_mul_lo_u32,
+canonical output (final conditional subtraction of p); 598 instructions (672 with every carry caught).  Registers are pinned (a = v[0:11] in/out, b = v[12:23])
 and only v24-v39, s16-s28 and vcc are clobbered, so values live across a product stay in registers.
 The final select uses v_cndmask_b32_e64 with an explicit VCC operand: on gfx950 the VOP2 (e32) form that
 reads VCC implicitly issues at ~19 cycles per instruction against ~4.4 for the e64 form and for v_bfi_b32
@@ -224,10 +225,98 @@ def schedule(ins, issue=4):
     return order, t
 
 
+# ---------------------------------------------------------------- carry elision (round 6)
+# A v_mad_u64_u32 needs its carry-out caught only when the 64-bit column accumulator can overflow.  Every product
+# operand is < 2^382 (canonical values and the lazy sums in [0, 2p) of field.h), so a product with an operand's top
+# limb is < 2^62, and p's limbs 3, 5 and 7-11 are well below 2^32.  Such terms go first in their column, right after
+# the carried-in value (< (carries + 1) 2^32), and skip the v_addc while the sum of their bounds stays below 2^64.
+# emulate(strict=True) raises when a mad drops a carry.
+OPERAND_BITS = 382
+ELIDE = True  # False: the round-5 streams (every carry caught)
+TOP_BOUND = (1 << (OPERAND_BITS - 352)) - 1  # an operand's top limb
+LIMB_MAX = 0xFFFFFFFF
+M64 = (1 << 64) - 1
+PL32 = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
+
+
+def _comba(w, pairs, M, out, acc, elide=True):
+    """Product scanning with the Montgomery reduction interleaved per column (radix 2^32, R = 2^384): appends
+    r = (sum of X*Y over pairs)/R, raw, to the stream w.  pairs = [(X, Y)] (limb index -> register); M(i) holds the
+    quotient digits; out(j) receives result limb j (from column j + 12; out(j) may alias a register dead by then).
+    Accumulator v[acc:acc+1], the carried value (hi, carries) in v[acc+2:acc+3]; p in s16-s27, -p^-1 mod 2^32 in s28.
+    elide=False: every mad catches its carry (the round-5 streams, term for term)."""
+    lo, hi, mv, cw = ("v%d" % (acc + k) for k in range(4))
+    accp, srcp = "v[%d:%d]" % (acc, acc + 1), "v[%d:%d]" % (acc + 2, acc + 3)
+    Sp = lambda j: "s%d" % (16 + j)
+    n_prev = 0
+    for i in range(2 * N32 - 1):
+        body = []
+        for j in range(max(0, i - N32 + 1), min(i, N32 - 1) + 1):
+            for X, Y in pairs:
+                bx = TOP_BOUND if j == N32 - 1 else LIMB_MAX
+                by = TOP_BOUND if i - j == N32 - 1 else LIMB_MAX
+                body.append((X(j), Y(i - j), bx * by))
+            if j < i:
+                body.append((M(j), Sp(i - j), LIMB_MAX * PL32[i - j]))
+        start = 0 if i == 0 else (n_prev + 1) << 32
+        if elide:
+            free, s = [], start
+            for k in sorted(range(len(body)), key=lambda k: body[k][2]):
+                if s + body[k][2] > M64:
+                    break
+                free.append(k)
+                s += body[k][2]
+            seq = [(body[k], False) for k in free] + [(body[k], True) for k in range(len(body)) if k not in free]
+        else:
+            seq = [(t, not (i == 0 and k == 0)) for k, t in enumerate(body)]
+            s = None
+        st = {"src": "0" if i == 0 else srcp, "init": False, "n": 0}
+
+        def mac(x, y, need):
+            w("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (accp, x, y, st["src"]))
+            st["src"] = accp
+            if not need:
+                return
+            if st["init"]:
+                w("v_addc_co_u32_e32 %s, vcc, 0, %s, vcc" % (cw, cw))
+            else:
+                w("v_addc_co_u32_e64 %s, vcc, 0, 0, vcc" % cw)
+                st["init"] = True
+            st["n"] += 1
+
+        for k, ((x, y, _), need) in enumerate(seq):
+            mac(x, y, need)
+            if not elide and i == 0 and k == 0:
+                w("v_mov_b32 %s, 0" % cw)
+                st["init"] = True
+        if i < N32:
+            w("v_mul_lo_u32 %s, %s, s28" % (M(i), lo))
+            b = LIMB_MAX * PL32[0]
+            need = not elide or any(nd for _, nd in seq) or s + b > M64
+            mac(M(i), Sp(0), need)
+        if i == 2 * N32 - 2:
+            if elide:
+                w("v_mov_b32 %s, %s" % (out(i - N32), lo))
+                w("v_mov_b32 %s, %s" % (out(N32 - 1), hi))
+            else:
+                w("v_mov_b32 %s, %s" % (out(i - N32), lo))
+                w("v_mov_b32 %s, %s" % (mv, hi))
+                w("v_mov_b32 %s, %s" % (out(N32 - 1), mv))
+            break
+        if not st["init"]:
+            w("v_mov_b32 %s, 0" % cw)  # no carry caught in this column: the carried value's high word is 0
+        if i >= N32:
+            w("v_mov_b32 %s, %s" % (out(i - N32), lo))
+        w("v_mov_b32 %s, %s" % (mv, hi))
+        n_prev = st["n"]
+
+
 # ---------------------------------------------------------------- old radix-2^32 routine (probe)
-def gen_mul(e64_select=True):
-    """The shipped routine (Comba, radix 2^32, mad + addc carry capture, canonical output, R = 2^384).
-    e64_select=False reproduces the round-1 stream (VOP2 v_cndmask_b32_e32) for the microbenchmark."""
+def gen_mul(e64_select=True, elide=None):
+    """The shipped routine (Comba, radix 2^32, R = 2^384, canonical output for operands < 2^382): mad + addc carry
+    capture except where the column bound makes the carry impossible (_comba).  e64_select=False, elide=False
+    reproduce the round-1 stream (VOP2 v_cndmask_b32_e32, every carry caught) for the microbenchmark."""
+    elide = ELIDE if elide is None else elide
     PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
     PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
     Aa = lambda j: "v%d" % j
@@ -239,44 +328,7 @@ def gen_mul(e64_select=True):
     for j in range(N32):
         w("s_mov_b32 %s, 0x%08x" % (Sp(j), PL[j]))
     w("s_mov_b32 s28, 0x%08x" % PINV32)
-    first = [True]
-    src2 = ["v[36:37]"]
-
-    def mac(x, y):
-        w("v_mad_u64_u32 v[36:37], vcc, %s, %s, %s" % (x, y, src2[0]))
-        src2[0] = "v[36:37]"
-        if first[0]:
-            w("v_addc_co_u32_e64 v39, vcc, 0, 0, vcc")
-            first[0] = False
-        else:
-            w("v_addc_co_u32_e32 v39, vcc, 0, v39, vcc")
-
-    def shift():
-        w("v_mov_b32 v38, v37")
-        src2[0] = "v[38:39]"
-        first[0] = True
-
-    w("v_mad_u64_u32 v[36:37], vcc, v0, v12, 0")
-    w("v_mov_b32 v39, 0")
-    first[0] = False
-    w("v_mul_lo_u32 v24, v36, s28")
-    mac("v24", "s16")
-    shift()
-    for i in range(1, N32):
-        for j in range(i):
-            mac(Aa(j), Bb(i - j))
-            mac(Mm(j), Sp(i - j))
-        mac(Aa(i), Bb(0))
-        w("v_mul_lo_u32 %s, v36, s28" % Mm(i))
-        mac(Mm(i), "s16")
-        shift()
-    for i in range(N32, 2 * N32 - 1):
-        for j in range(i - N32 + 1, N32):
-            mac(Aa(j), Bb(i - j))
-            mac(Mm(j), Sp(i - j))
-        w("v_mov_b32 %s, v36" % Aa(i - N32))
-        shift()
-    w("v_mov_b32 v11, v38")
+    _comba(w, [(Aa, Bb)], Mm, Aa, 36, elide)
     for j in range(N32):
         w("v_mov_b32 %s, %s" % (Mm(j), Sp(j)))
     w("v_sub_co_u32_e32 v12, vcc, v0, v24")
@@ -309,94 +361,14 @@ FP2_A0, FP2_A1, FP2_B0, FP2_B1, FP2_C1, FP2_C0, FP2_T = 0, 12, 24, 36, 52, 64, 7
 def _gen_sop(w, X, Y, Z, Wd, M):
     """Appends r = (X*Y + Z*Wd)/2^384 mod p, in [0, 2p), to the stream w; the quotient digits m_i live in
     M(i) and the result limb j overwrites M(j) (m_j is dead from column j + 12 on)."""
-    first = [True]
-    src2 = ["v[48:49]"]
-
-    def mac(x, y):
-        w("v_mad_u64_u32 v[48:49], vcc, %s, %s, %s" % (x, y, src2[0]))
-        src2[0] = "v[48:49]"
-        if first[0]:
-            w("v_addc_co_u32_e64 v51, vcc, 0, 0, vcc")
-            first[0] = False
-        else:
-            w("v_addc_co_u32_e32 v51, vcc, 0, v51, vcc")
-
-    def shift():
-        w("v_mov_b32 v50, v49")
-        src2[0] = "v[50:51]"
-        first[0] = True
-
-    Sp = lambda j: "s%d" % (16 + j)
-    w("v_mad_u64_u32 v[48:49], vcc, %s, %s, 0" % (X(0), Y(0)))
-    w("v_mov_b32 v51, 0")
-    first[0] = False
-    mac(Z(0), Wd(0))
-    w("v_mul_lo_u32 %s, v48, s28" % M(0))
-    mac(M(0), "s16")
-    shift()
-    for i in range(1, N32):
-        for j in range(i):
-            mac(X(j), Y(i - j))
-            mac(Z(j), Wd(i - j))
-            mac(M(j), Sp(i - j))
-        mac(X(i), Y(0))
-        mac(Z(i), Wd(0))
-        w("v_mul_lo_u32 %s, v48, s28" % M(i))
-        mac(M(i), "s16")
-        shift()
-    for i in range(N32, 2 * N32 - 1):
-        for j in range(i - N32 + 1, N32):
-            mac(X(j), Y(i - j))
-            mac(Z(j), Wd(i - j))
-            mac(M(j), Sp(i - j))
-        w("v_mov_b32 %s, v48" % M(i - N32))
-        shift()
-    w("v_mov_b32 %s, v50" % M(N32 - 1))
+    _comba(w, [(X, Y), (Z, Wd)], M, M, 48, ELIDE)
 
 
 def _gen_prod(w, X, Y, M, R=None):
     """Appends r = X*Y/2^384 mod p, in [0, 2p), to the stream w (gen_mul's column schedule on named registers):
     quotient digits in M(i), result limb j over M(j) or, with R = X, over X(j) (both are dead from column
     j + 12 on)."""
-    R = R or M
-    first = [True]
-    src2 = ["v[48:49]"]
-
-    def mac(x, y):
-        w("v_mad_u64_u32 v[48:49], vcc, %s, %s, %s" % (x, y, src2[0]))
-        src2[0] = "v[48:49]"
-        if first[0]:
-            w("v_addc_co_u32_e64 v51, vcc, 0, 0, vcc")
-            first[0] = False
-        else:
-            w("v_addc_co_u32_e32 v51, vcc, 0, v51, vcc")
-
-    def shift():
-        w("v_mov_b32 v50, v49")
-        src2[0] = "v[50:51]"
-        first[0] = True
-
-    Sp = lambda j: "s%d" % (16 + j)
-    w("v_mad_u64_u32 v[48:49], vcc, %s, %s, 0" % (X(0), Y(0)))
-    w("v_mov_b32 v51, 0")
-    w("v_mul_lo_u32 %s, v48, s28" % M(0))
-    mac(M(0), "s16")
-    shift()
-    for i in range(1, N32):
-        for j in range(i):
-            mac(X(j), Y(i - j))
-            mac(M(j), Sp(i - j))
-        mac(X(i), Y(0))
-        w("v_mul_lo_u32 %s, v48, s28" % M(i))
-        mac(M(i), "s16")
-        shift()
-    for i in range(N32, 2 * N32 - 1):
-        for j in range(i - N32 + 1, N32):
-            mac(X(j), Y(i - j))
-            mac(M(j), Sp(i - j))
-        w("v_mov_b32 %s, v48" % R(i - N32))
-        shift()
-    w("v_mov_b32 %s, v50" % R(N32 - 1))
+    _comba(w, [(X, Y)], M, R or M, 48, ELIDE)
 
 
 def _gen_sopn(w, pairs, M):
@@ -791,11 +763,17 @@ def emulate_positional(body, outs, ins):
 
 
 # ---------------------------------------------------------------- CPU interpreter
-def emulate(body, a, b, regs=None):
+class DroppedCarry(AssertionError):
+    pass
+
+
+def emulate(body, a, b, regs=None, strict=True):
     """Interprets the instruction subset used above (one lane); a, b: 12 x 32-bit limbs.
     Returns the 12 output limbs (v0..v11).  With regs (a dict VGPR number -> value, updated in place)
-    the register file starts from regs instead of a in v0.. and b in v12.."""
+    the register file starts from regs instead of a in v0.. and b in v12..  strict: a v_mad_u64_u32 whose
+    carry-out is set must be followed by the v_addc that catches it (carry elision, _comba), else DroppedCarry."""
     v, s = ({}, {}) if regs is None else (regs, {})
+    pending = [None]
     M32, M64 = 0xFFFFFFFF, (1 << 64) - 1
     if regs is None:
         for j in range(N32):
@@ -829,6 +807,10 @@ def emulate(body, a, b, regs=None):
     for ins in body:
         op, rest = ins.split(" ", 1)
         o = [t.strip() for t in rest.split(",")]
+        if pending[0] is not None:
+            if strict and not (op.startswith("v_addc_co_u32") and o[-1] == "vcc"):
+                raise DroppedCarry(pending[0])
+            pending[0] = None
         if op == "s_mov_b32":
             s[o[0]] = rd(o[1])
         elif op == "v_mov_b32":
@@ -837,6 +819,8 @@ def emulate(body, a, b, regs=None):
             r = (rd(o[2]) & M32) * (rd(o[3]) & M32) + rd(o[4])
             wr(o[0], r & M64)
             s[o[1]] = r >> 64
+            if r >> 64:
+                pending[0] = ins
         elif op == "v_mul_lo_u32":
             wr(o[0], rd(o[1]) * rd(o[2]))
         elif op.startswith("v_addc_co_u32"):
@@ -876,6 +860,8 @@ def emulate(body, a, b, regs=None):
             wr(o[0], ((rd(o[1]) << rd(o[2])) + rd(o[3])) & M64)
         else:
             raise ValueError(ins)
+    if strict and pending[0] is not None:
+        raise DroppedCarry(pending[0])
     return [v[j] for j in range(N32)]
 
 

@@ -10,7 +10,7 @@
 #   c2:<lib>:<name>       the C2 part of the bench alone (5 steps) with HIPBLS_LIB=<lib>; repeat the step to alternate
 #   pmc:<counters>:<name> one rocprofv3 --pmc pass over a short C2-only bench -> gpurun_out/<tag>_pmc_<name>/
 #   pmcset:<wl>           the five counter passes of scripts/gpu_pmc.sh for workload c2|c3|c4|lat -> gpurun_out/pmc6_<wl>/
-#   ceiling               charon_amd/tools/ceiling_probe (the product routines alone, every SIMD) -> <tag>_ceiling.txt
+#   ceiling[:<bin>:<name>] charon_amd/tools/ceiling_probe or <bin> (the product routines alone, every SIMD) -> <tag>_ceiling[_<name>].txt
 #   py:<file>             python -u <file> (a probe script)                -> gpurun_out/<tag>_<basename>.log
 #
 # TAG (environment, default "run") prefixes every output.
@@ -69,10 +69,12 @@ for step in "$@"; do
       WL=${step#pmcset:} bash scripts/gpu_pmc.sh > "$O/${T}_pmcset_${step#pmcset:}.log" 2>&1 \
         || { echo "pmc set failed"; tail -20 "$O/${T}_pmcset_${step#pmcset:}.log"; exit 1; }
       tail -1 "$O/${T}_pmcset_${step#pmcset:}.log" ;;
-    ceiling)
-      timeout -k 10 300 charon_amd/tools/ceiling_probe > "$O/${T}_ceiling.txt" 2>&1 \
-        || { echo "ceiling probe failed"; tail -20 "$O/${T}_ceiling.txt"; exit 1; }
-      cat "$O/${T}_ceiling.txt" ;;
+    ceiling|ceiling:*)
+      IFS=: read -r _ bin name <<< "$step"
+      bin=${bin:-charon_amd/tools/ceiling_probe}
+      f="$O/${T}_ceiling${name:+_$name}.txt"
+      timeout -k 10 300 "$R/$bin" > "$f" 2>&1 || { echo "ceiling probe failed"; tail -20 "$f"; exit 1; }
+      cat "$f" ;;
     py:*)
       f=${step#py:}
       timeout -k 10 600 python -u "$f" > "$O/${T}_$(basename "$f" .py).log" 2>&1 \

@@ -248,3 +248,87 @@ def test_fp2_sum_of_three_products_routine():
         c1 = _val([regs[g.FP2_C1 + j] for j in range(12)])
         assert c0 == (x0 * y0 - x1 * y1 + z0 * w0 - z1 * w1 + u0 * t0 - u1 * t1) * R_INV % g.P, t
         assert c1 == (x0 * y1 + x1 * y0 + z0 * w1 + z1 * w0 + u0 * t1 + u1 * t0) * R_INV % g.P, t
+
+
+# ---------------------------------------------------------------- carry elision (round 6)
+def _symbolic_max(body, bound, carried="v[38:39]"):
+    """Walks a product stream with every operand at its largest value: a mad that no v_addc follows must leave the
+    64-bit accumulator <= 2^64 - 1 (the column's carried value counts as (carries + 1) 2^32).  Independent of the
+    generator's own bookkeeping (_comba); returns the number of carry-free mads."""
+    free, acc, n_cur, n_prev = 0, 0, 0, 0
+    for k, ins in enumerate(body):
+        op, rest = ins.split(" ", 1)
+        o = [t.strip() for t in rest.split(",")]
+        if op != "v_mad_u64_u32":
+            continue
+        if o[4] == "0":
+            base = 0
+        elif o[4] == carried:
+            n_prev, n_cur = n_cur, 0
+            base = (n_prev + 1) << 32
+        else:
+            base = acc
+        val = base + bound(o[2]) * bound(o[3])
+        if body[k + 1].startswith("v_addc_co_u32") if k + 1 < len(body) else False:
+            n_cur += 1
+            acc = (1 << 64) - 1  # caught: only the accumulator's width is known from here on
+        else:
+            assert val <= (1 << 64) - 1, (k, ins, hex(val))
+            free += 1
+            acc = val
+    return free
+
+
+def test_product_carry_elision_is_sound():
+    """gen_mul's carry-free mads: with operands < 2^382 (top limb < 2^30), q digits < 2^32 and p's limbs exact, no
+    carry-free mad can overflow its accumulator; and the same for a two-product column schedule (the Fp2 routines)."""
+    pl = {"s%d" % (16 + j): (g.P >> (32 * j)) & 0xFFFFFFFF for j in range(12)}
+
+    def bound_for(tops):
+        return lambda r: pl[r] if r in pl else (g.TOP_BOUND if r in tops else 0xFFFFFFFF)
+
+    body = g.gen_mul()
+    free = _symbolic_max(body, bound_for({"v11", "v23"}))
+    assert free >= 70 and sum(x.startswith("v_addc") for x in body) == 288 - free + 0
+    w = []
+    V = lambda base: (lambda j: "v%d" % (base + j))
+    g._comba(w.append, [(V(100), V(112)), (V(124), V(136))], V(148), V(148), 48)
+    assert _symbolic_max(w, bound_for({"v111", "v123", "v135", "v147"}), carried="v[50:51]") >= 70
+
+
+def test_product_extreme_operands_keep_every_carry():
+    """Operands at the elision's limits (2^382 - 1, every lower limb all ones, the top limb at 2^30 - 1 or at 2p's) in
+    the strict interpreter: no mad drops a carry, and the products stay Montgomery products (canonical for the Fp
+    product, whose operands may be anything < 2^382)."""
+    top = (1 << 382) - 1
+    ext = [top, top - 1, (0x3FFFFFFF << 352), (1 << 352) - 1, 2 * g.P - 1, 2 * g.P, g.P - 1, 0, 1,
+           (0x340223D4 << 352) | ((1 << 352) - 1)]
+    rnd = random.Random(606)
+    mul = g.gen_mul()
+    for a in ext:
+        for b in ext + [rnd.randrange(1 << 382) for _ in range(4)]:
+            got = _val(g.emulate(mul, _limbs(a), _limbs(b)))
+            assert got == a * b * R_INV % g.P, (hex(a), hex(b))
+    f2m, ok = g.gen_fp2_mul(), [x for x in ext if x <= 2 * g.P]
+    for t in range(200):
+        a0, a1, b0 = (rnd.choice(ext) for _ in range(3))
+        b1 = rnd.choice(ok)  # the routine forms 2p - b1
+        regs = {}
+        for base, x in ((g.FP2_A0, a0), (g.FP2_A1, a1), (g.FP2_B0, b0), (g.FP2_B1, b1)):
+            regs.update({base + j: v for j, v in enumerate(_limbs(x))})
+        g.emulate(f2m, None, None, regs)
+        c0 = _val([regs[g.FP2_C0 + j] for j in range(12)])
+        c1 = _val([regs[g.FP2_C1 + j] for j in range(12)])
+        assert c0 % g.P == (a0 * b0 - a1 * b1) * R_INV % g.P and c1 % g.P == (a0 * b1 + a1 * b0) * R_INV % g.P
+
+
+def test_strict_interpreter_catches_a_dropped_carry():
+    """The checker is live: removing a carry-catching v_addc from gen_mul makes the interpreter raise on all-ones
+    operands."""
+    body = g.gen_mul()
+    ks = [i for i, x in enumerate(body) if x.startswith("v_addc_co_u32_e32")]
+    k = ks[len(ks) // 2]  # a mid-product column: all-ones operands set its carries
+    broken = body[:k] + body[k + 1:]
+    a = (1 << 382) - 1
+    with pytest.raises(g.DroppedCarry):
+        g.emulate(broken, _limbs(a), _limbs(a))
