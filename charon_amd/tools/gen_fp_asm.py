@@ -233,6 +233,7 @@ def schedule(ins, issue=4):
 # emulate(strict=True) raises when a mad drops a carry.
 OPERAND_BITS = 382
 ELIDE = True  # False: the round-5 streams (every carry caught)
+P_MOV64 = True  # False: p staged with twelve v_mov_b32
 TOP_BOUND = (1 << (OPERAND_BITS - 352)) - 1  # an operand's top limb
 LIMB_MAX = 0xFFFFFFFF
 M64 = (1 << 64) - 1
@@ -311,6 +312,20 @@ def _comba(w, pairs, M, out, acc, elide=True):
         n_prev = st["n"]
 
 
+def _load_p(w, R):
+    """p (s16-s27) into the VGPRs R(0..11): six v_mov_b64 from SGPR pairs (one issue slot per two limbs; every
+    instruction of a one-wave-per-SIMD stream costs the same slot, tools/isa_probe.hip), or twelve v_mov_b32 with
+    P_MOV64 = False."""
+    if not P_MOV64:
+        for j in range(N32):
+            w("v_mov_b32 %s, s%d" % (R(j), 16 + j))
+        return
+    for j in range(0, N32, 2):
+        lo = int(R(j)[1:])
+        assert lo % 2 == 0 and R(j + 1) == "v%d" % (lo + 1)
+        w("v_mov_b64 v[%d:%d], s[%d:%d]" % (lo, lo + 1, 16 + j, 17 + j))
+
+
 # ---------------------------------------------------------------- old radix-2^32 routine (probe)
 def gen_mul(e64_select=True, elide=None):
     """The shipped routine (Comba, radix 2^32, R = 2^384, canonical output for operands < 2^382): mad + addc carry
@@ -329,8 +344,7 @@ def gen_mul(e64_select=True, elide=None):
         w("s_mov_b32 %s, 0x%08x" % (Sp(j), PL[j]))
     w("s_mov_b32 s28, 0x%08x" % PINV32)
     _comba(w, [(Aa, Bb)], Mm, Aa, 36, elide)
-    for j in range(N32):
-        w("v_mov_b32 %s, %s" % (Mm(j), Sp(j)))
+    _load_p(w, Mm)
     w("v_sub_co_u32_e32 v12, vcc, v0, v24")
     for j in range(1, N32):
         w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (Bb(j), Aa(j), Mm(j)))
@@ -510,8 +524,7 @@ def gen_fp2_sqr():
         w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
     w("s_mov_b32 s28, 0x%08x" % PINV32)
     # d = (p - a1) + a0 into C1 (p staged in C0 first), s = a0 + a1 into C0, a1 <- 2 a1
-    for j in range(N32):
-        w("v_mov_b32 %s, s%d" % (C0(j), 16 + j))
+    _load_p(w, C0)
     w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (C1(0), C0(0), A1(0)))
     for j in range(1, N32):
         w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (C1(j), C0(j), A1(j)))
@@ -527,8 +540,7 @@ def gen_fp2_sqr():
     T = V(52)
     _gen_prod(w, C0, C1, T, R=C0)                      # c0 = s d (raw) over s; digits in v52..v63
     _gen_prod(w, A0, A1, C1)                           # c1 = a0 (2 a1) (raw); digits and result over d
-    for j in range(N32):
-        w("v_mov_b32 %s, s%d" % (A0(j), 16 + j))
+    _load_p(w, A0)
     for C in (C0, C1):                                 # canonical: keep c when c - p borrows
         w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), A0(0)))
         for j in range(1, N32):
@@ -558,8 +570,7 @@ def gen_fp2_mul():
     for j in range(1, N32):                            # b1 <- 2p - b1 in (0, 2p]
         w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (B1(j), C0(j), B1(j)))
     _gen_sop(w, A0, B0, A1, B1, C0)                    # c0 (raw) in v[64:75]
-    for j in range(N32):                               # p over the dead 2p - b1; a0, a1, b0 stay intact
-        w("v_mov_b32 %s, s%d" % (B1(j), 16 + j))
+    _load_p(w, B1)                                     # p over the dead 2p - b1; a0, a1, b0 stay intact
     for C in (C1, C0):                                 # canonical: keep c when c - p borrows
         w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), B1(0)))
         for j in range(1, N32):
@@ -613,8 +624,7 @@ def gen_fp2_mul_half():
     for j in range(N32):                               # Y = c1 ? b1 : b0 (over b1)
         w("v_bfi_b32 %s, %s, %s, %s" % (B1(j), HM, B1(j), B0(j)))
     _gen_sop(w, A0, B1, A1, T, C)                      # (a0 Y + a1 W)/R, raw (< 2p), over C
-    for j in range(N32):                               # p over the dead b0
-        w("v_mov_b32 %s, s%d" % (B0(j), 16 + j))
+    _load_p(w, B0)                                     # p over the dead b0
     _final_sub(w, C, B0, T, "v48")
     return out
 
@@ -630,8 +640,7 @@ def gen_fp2_sqr_half():
     for j in range(N32):
         w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
     w("s_mov_b32 s28, 0x%08x" % PINV32)
-    for j in range(N32):                               # p staged in X
-        w("v_mov_b32 %s, s%d" % (X(j), 16 + j))
+    _load_p(w, X)                                      # p staged in X
     w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (Y(0), X(0), A1(0)))
     for j in range(1, N32):                            # Y <- p - a1
         w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (Y(j), X(j), A1(j)))
@@ -648,8 +657,7 @@ def gen_fp2_sqr_half():
         w("v_bfi_b32 %s, %s, %s, %s" % (X(j), HM, A0(j), X(j)))
         w("v_bfi_b32 %s, %s, %s, %s" % (Y(j), HM, T(j), Y(j)))
     _gen_prod(w, X, Y, M, R=X)                         # X Y / R, raw (< 2p), over X
-    for j in range(N32):                               # p for the final subtraction
-        w("v_mov_b32 %s, s%d" % (T(j), 16 + j))
+    _load_p(w, T)                                      # p for the final subtraction
     _final_sub(w, X, T, M, "v48")
     return out
 
@@ -790,6 +798,9 @@ def emulate(body, a, b, regs=None, strict=True):
         if x.startswith("v["):
             lo = int(x[2:x.index(":")])
             return v[lo] | (v[lo + 1] << 32)
+        if x.startswith("s["):
+            lo = int(x[2:x.index(":")])
+            return s["s%d" % lo] | (s["s%d" % (lo + 1)] << 32)
         if x.startswith("s"):
             return s[x]
         return v[int(x[1:])]
@@ -813,7 +824,7 @@ def emulate(body, a, b, regs=None, strict=True):
             pending[0] = None
         if op == "s_mov_b32":
             s[o[0]] = rd(o[1])
-        elif op == "v_mov_b32":
+        elif op in ("v_mov_b32", "v_mov_b64"):
             wr(o[0], rd(o[1]))
         elif op == "v_mad_u64_u32":
             r = (rd(o[2]) & M32) * (rd(o[3]) & M32) + rd(o[4])
