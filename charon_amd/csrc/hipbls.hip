@@ -45,6 +45,20 @@
 #include "kernels.h"
 #include "ranges.h"
 
+// The RLC item and hash stages at two waves per SIMD (rlc_wide.hip: its own translation unit, C linkage).
+extern "C" {
+__global__ void k_rlc_items(uint64_t i0, uint64_t i1, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
+                            uint64_t n, uint64_t n_msgs, bls::rlc_seed seed, uint32_t* rpk, uint32_t* rsig,
+                            int32_t* status, const uint32_t* key_idx, uint64_t T, const int32_t* tcode,
+                            const uint32_t* tab);
+__global__ void k_rlc_hash(const uint8_t* msgs, const uint64_t* offs, uint64_t n_hash, const uint32_t* mlist, uint32_t* H,
+                           uint64_t hstride, const uint32_t* hslot);
+__global__ void k_rlcb_items(uint64_t n, const uint8_t* pks, const uint8_t* sigs, const uint32_t* msg_idx,
+                             uint64_t n_msgs, bls::rlc_seed seed, uint32_t* rpk, uint32_t* pts, uint32_t* sc,
+                             int32_t* status, const uint32_t* key_idx, uint64_t T, const int32_t* tcode,
+                             const uint32_t* tab, const uint32_t* g1pos, uint32_t* gpts, uint32_t* gsc);
+}
+
 // The eight-lane latency path (verify_lat.hip, its own translation unit: BLS_FP2_PAIR build in namespace bls_fp2p).
 namespace bls_fp2p {
 __global__ void k_verify_prep8(const uint8_t* pks, const uint8_t* msgs, const uint64_t* offs, const uint8_t* sigs,

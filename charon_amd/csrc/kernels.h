@@ -772,30 +772,8 @@ __global__ void __launch_bounds__(kBlock) k_recover_secret(const uint8_t* __rest
 // ---------------------------------------------------------------- RLC BatchVerify (rlc.h)
 // The four stages run per sub-batch (a contiguous, window-aligned item range) so that several
 // sub-batches' stages overlap on separate streams (launch_rlc).
-// Stage 1: one lane per item -> status (final or RLC_PENDING), [r_i] pk_i and [r_i] sig_i in SoA.
-// pks == nullptr: public keys come from the resident pubshare table (key_idx, T, tcode, tab).
-__global__ void __launch_bounds__(kBlock) k_rlc_items(uint64_t i0, uint64_t i1, const uint8_t* __restrict__ pks,
-                                                      const uint8_t* __restrict__ sigs,
-                                                      const uint32_t* __restrict__ msg_idx, uint64_t n,
-                                                      uint64_t n_msgs, rlc_seed seed, uint32_t* __restrict__ rpk,
-                                                      uint32_t* __restrict__ rsig, int32_t* __restrict__ status,
-                                                      const uint32_t* __restrict__ key_idx, uint64_t T,
-                                                      const int32_t* __restrict__ tcode,
-                                                      const uint32_t* __restrict__ tab) {
-  const uint64_t i = i0 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (i < i1) rlc_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk, rsig, status, key_idx, T, tcode, tab);
-}
-
-// Stage 2: one lane per message to hash -> H(m) in affine SoA (48 words) at its table column.  mlist lists the
-// messages to hash (the H(m)-cache misses); nullptr = messages 0 .. n_hash-1.
-__global__ void __launch_bounds__(kBlock) k_rlc_hash(const uint8_t* __restrict__ msgs, const uint64_t* __restrict__ offs,
-                                                     uint64_t n_hash, const uint32_t* __restrict__ mlist,
-                                                     uint32_t* __restrict__ H, uint64_t hstride,
-                                                     const uint32_t* __restrict__ hslot) {
-  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (j < n_hash) rlc_hash_lane(mlist ? (uint64_t)mlist[j] : j, msgs, offs, H, hstride, hslot);
-}
-
+// Stages 1 and 2 (k_rlc_items, k_rlc_hash) and the batch-wide check's stage 1 (k_rlcb_items) live in rlc_wide.hip:
+// their own translation unit, compiled for two waves per SIMD.
 // Stage 3: one lane per window of RLC_W items -> one multi-pairing check.  The items a failed window
 // leaves pending are appended to this sub-batch's fallback list (one atomic per failed window), so
 // stage 4 runs on a dense list instead of waking a wave for every scattered pending item.
@@ -936,22 +914,7 @@ __global__ void __launch_bounds__(kBlock) k_rlc_fallback_lg2(const uint32_t* __r
 }
 
 // ---------------------------------------------------------------- batch-wide RLC check (rlcb.h)
-__global__ void __launch_bounds__(kBlock) k_rlcb_items(uint64_t n, const uint8_t* __restrict__ pks,
-                                                       const uint8_t* __restrict__ sigs,
-                                                       const uint32_t* __restrict__ msg_idx, uint64_t n_msgs,
-                                                       rlc_seed seed, uint32_t* __restrict__ rpk,
-                                                       uint32_t* __restrict__ pts, uint32_t* __restrict__ sc,
-                                                       int32_t* __restrict__ status,
-                                                       const uint32_t* __restrict__ key_idx, uint64_t T,
-                                                       const int32_t* __restrict__ tcode,
-                                                       const uint32_t* __restrict__ tab,
-                                                       const uint32_t* __restrict__ g1pos, uint32_t* __restrict__ gpts,
-                                                       uint32_t* __restrict__ gsc) {
-  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (i < n)
-    rlcb_items_lane(i, pks, sigs, msg_idx, n, n_msgs, seed, rpk, pts, sc, status, key_idx, T, tcode, tab, g1pos, gpts,
-                    gsc);
-}
+// Stage 1 (k_rlcb_items): rlc_wide.hip.
 
 // ---------------------------------------------------------------- the G1 MSM per large message (g1msm.h)
 __global__ void __launch_bounds__(256) k_g1m_count(uint64_t n, const uint32_t* __restrict__ msg_idx, uint64_t n_msgs,

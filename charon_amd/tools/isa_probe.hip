@@ -52,25 +52,35 @@ __global__ void __launch_bounds__(64) k(uint64_t* cyc, int iters) {
                        "v_mov_b32 v4, v3\n\tv_mad_u64_u32 v[2:3], vcc, v8, v9, v[4:5]\n\t") ::: CL);
     if (K == 11)  // v_mov_b32 VGPR -> VGPR (baseline)
       asm volatile(X32("v_mov_b32 v2, v0\n\tv_mov_b32 v3, v1\n\tv_mov_b32 v6, v4\n\tv_mov_b32 v7, v5\n\t") ::: CL);
+    if (K == 12)  // SALU only
+      asm volatile(X32("s_mov_b32 s40, 0x1a0111ea\n\ts_mov_b32 s41, 0x397fe69a\n\ts_mov_b32 s42, 0x4b1ba7b6\n\t"
+                       "s_mov_b32 s43, 0x434bacd7\n\t") ::: CL);
+    if (K == 13)  // VALU and SALU alternating (64 + 64 per iteration): does a scalar move take a slot of its own?
+      asm volatile(X32("v_add_u32_e32 v2, v0, v2\n\ts_mov_b32 s40, 0x1a0111ea\n\tv_add_u32_e32 v3, v1, v3\n\t"
+                       "s_mov_b32 s41, 0x397fe69a\n\t") ::: CL);
+    if (K == 14)  // mads with s_mov between (the routine head: p into SGPRs next to the first column)
+      asm volatile(X32("v_mad_u64_u32 v[2:3], vcc, v0, v1, v[2:3]\n\ts_mov_b32 s40, 0x1a0111ea\n\t"
+                       "v_mad_u64_u32 v[6:7], vcc, v4, v5, v[6:7]\n\ts_mov_b32 s41, 0x397fe69a\n\t") ::: CL);
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 int main() {
-  const char* names[12] = {"v_mul_lo_u32 4 dests", "v_mul_lo_u32 dependent", "v_mad_u64_u32 as mul (pair)",
+  const char* names[15] = {"v_mul_lo_u32 4 dests", "v_mul_lo_u32 dependent", "v_mad_u64_u32 as mul (pair)",
                            "v_mov_b64 from SGPR pair", "v_mov_b32 from SGPR", "mad + addc (product column)",
                            "mad back to back (carry-free)", "v_bfi_b32", "v_sub_co/v_subb_co chain",
-                           "v_pk_mov_b32 from SGPR pair", "mad,addc,mov shift", "v_mov_b32 v->v"};
+                           "v_pk_mov_b32 from SGPR pair", "mad,addc,mov shift", "v_mov_b32 v->v", "s_mov_b32 (SALU only)",
+                           "v_add / s_mov alternating", "v_mad / s_mov alternating"};
   uint64_t* d;
   if (hipMalloc(&d, 4096 * 8) != hipSuccess) return 2;
   static uint64_t h[4096];
-  for (int kk = 0; kk < 12; ++kk)
+  for (int kk = 0; kk < 15; ++kk)
     for (int w = 1; w <= 2; w *= 2) {
       const int blocks = 1024 * w;
       for (int rep = 0; rep < 2; ++rep) {
         switch (kk) {
 #define L(K) case K: hipLaunchKernelGGL(k<K>, dim3(blocks), dim3(64), 0, 0, d, 50); break;
-          L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11)
+          L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14)
         }
         if (hipDeviceSynchronize() != hipSuccess) return 3;
       }

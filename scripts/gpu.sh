@@ -8,6 +8,7 @@
 #   prof                  the default bench under rocprofv3 --kernel-trace --stats -> gpurun_out/<tag>_prof/
 #   rlc:<lib>:<name>      the C4(i) + C5 part of the bench with HIPBLS_LIB=<lib> (A/B of compile-time variants)
 #   c2:<lib>:<name>       the C2 part of the bench alone (5 steps) with HIPBLS_LIB=<lib>; repeat the step to alternate
+#   c3:<lib>:<name>       the C3 part (sigagg, 6 timed calls) with a 4,096-item C2, HIPBLS_LIB=<lib>
 #   pmc:<counters>:<name> one rocprofv3 --pmc pass over a short C2-only bench -> gpurun_out/<tag>_pmc_<name>/
 #   pmcset:<wl>           the five counter passes of scripts/gpu_pmc.sh for workload c2|c3|c4|lat -> gpurun_out/pmc6_<wl>/
 #   ceiling[:<bin>:<name>] charon_amd/tools/ceiling_probe or <bin> (the product routines alone, every SIMD) -> <tag>_ceiling[_<name>].txt
@@ -23,6 +24,7 @@ cd "$R" || exit 1
 export TMPDIR=/tmp
 RLC_ARGS="--steps 2 --warmup 1 --tagg-groups 0 --latency-calls 0 --host-path 0 --keys 0 --cpu-sample 0 --rlc-steps 3 --rlc-variants i"
 C2_ONLY="--tagg-groups 0 --latency-calls 0 --host-path 0 --keys 0 --cpu-sample 0 --rlc-node-validators 0 --c5 0"
+C3_ONLY="--c2-items 4096 --steps 2 --warmup 1 --tagg-steps 6 --latency-calls 0 --host-path 0 --keys 0 --cpu-sample 0 --rlc-node-validators 0 --c5 0"
 C2_ARGS="--steps 3 --warmup 1 --tagg-groups 0 --latency-calls 0 --host-path 0 --keys 0 --cpu-sample 0 --rlc-node-validators 0 --c5 0"
 
 for step in "$@"; do
@@ -51,6 +53,13 @@ for step in "$@"; do
       HIPBLS_LIB="$R/$lib" timeout -k 10 600 python -u bench.py $RLC_ARGS > "$O/${T}_rlc_${name}.json" \
         2> "$O/${T}_rlc_${name}.err" || { echo "rlc bench failed"; tail -30 "$O/${T}_rlc_${name}.err"; exit 1; }
       python3 scripts/bench_summary.py "$O/${T}_rlc_${name}.json" ;;
+    c3:*)
+      IFS=: read -r _ lib name <<< "$step"
+      k=0
+      while [ -e "$O/${T}_c3_${name}_$k.json" ]; do k=$((k+1)); done
+      HIPBLS_LIB="$R/$lib" timeout -k 10 300 python -u bench.py $C3_ONLY > "$O/${T}_c3_${name}_$k.json" \
+        2> "$O/${T}_c3_${name}_$k.err" || { echo "c3 bench failed"; tail -30 "$O/${T}_c3_${name}_$k.err"; exit 1; }
+      python3 scripts/bench_summary.py "$O/${T}_c3_${name}_$k.json" ;;
     c2:*)
       IFS=: read -r _ lib name <<< "$step"
       k=0
