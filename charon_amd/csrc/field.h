@@ -52,6 +52,26 @@ extern thread_local uint64_t g_fp_sqr_count;
 #define BLS_COUNT_SQR() ((void)0)
 #endif
 
+// Test build (tests/test_operand_contract.py, host only): the device routines' operand contracts checked wherever the
+// host runs the same per-lane code.  The product routines take operands below 2^382 (their carry elision, tools/
+// gen_fp_asm.py _comba; every operand is canonical or a lazy sum below 2p), the Fp2 square and the modular add / sub
+// canonical ones.  The host's lazy add / sub then stay unreduced as on the device, and a violation is counted.
+#if defined(BLS_CONTRACT_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
+namespace bls {
+extern uint64_t g_contract_violations;
+extern const char* g_contract_first;
+extern uint64_t g_contract_lazy_operands;  // products that received an unreduced (lazy) operand: the check's coverage
+}  // namespace bls
+#define BLS_CONTRACT(cond, what)                                            \
+  do {                                                                      \
+    if (!(cond)) {                                                          \
+      if (!::bls::g_contract_violations++) ::bls::g_contract_first = (what); \
+    }                                                                       \
+  } while (0)
+#else
+#define BLS_CONTRACT(cond, what) ((void)0)
+#endif
+
 namespace bls {
 
 BLS_HD BLS_INLINE void fp_set_zero(fp& r) {
@@ -74,6 +94,32 @@ BLS_HD BLS_INLINE bool fp_eq(const fp& a, const fp& b) {
   for (int i = 0; i < 12; ++i) acc |= a.v[i] ^ b.v[i];
   return acc == 0;
 }
+
+#if defined(BLS_CONTRACT_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
+static constexpr uint32_t P2_LIMBS_CONTRACT[12] = {0xffff5556u, 0x73fdffffu, 0x62a7ffffu, 0x3d57fffdu, 0xed61ec48u, 0xce61a541u, 0xe70a257eu, 0xc8ee9709u, 0x869759aeu, 0x96374f6cu, 0x72ffcd34u, 0x340223d4u};
+// a < k p (k = 1, 2) by a borrow chain
+inline bool fp_below_kp(const fp& a, int k) {
+  int64_t br = 0;
+  for (int i = 0; i < 12; ++i) {
+    const uint64_t pk = k == 1 ? (uint64_t)P_LIMBS[i] : (uint64_t)P2_LIMBS_CONTRACT[i];
+    br += (int64_t)a.v[i] - (int64_t)pk;
+    br >>= 32;
+  }
+  return br < 0;
+}
+inline bool fp_canonical(const fp& a) { return fp_below_kp(a, 1); }
+inline bool fp_product_operand(const fp& a) { return a.v[11] <= 0x3FFFFFFFu && fp_below_kp(a, 2); }
+inline void fp_reduce_2p(fp& r, const fp& a) {  // a < 2p -> a mod p
+  r = a;
+  if (fp_canonical(a)) return;
+  int64_t br = 0;
+  for (int i = 0; i < 12; ++i) {
+    br += (int64_t)a.v[i] - (int64_t)P_LIMBS[i];
+    r.v[i] = (uint32_t)br;
+    br >>= 32;
+  }
+}
+#endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
 }  // namespace bls
@@ -106,6 +152,7 @@ BLS_HD BLS_INLINE void fp_sub(fp& r, const fp& a, const fp& b) {
 #else
 // r = a + b mod p
 BLS_HD BLS_INLINE void fp_add(fp& r, const fp& a, const fp& b) {
+  BLS_CONTRACT(fp_canonical(a) && fp_canonical(b), "fp_add: an operand is not canonical");
   uint32_t s[12];
   uint64_t c = 0;
 #pragma unroll
@@ -130,6 +177,7 @@ BLS_HD BLS_INLINE void fp_add(fp& r, const fp& a, const fp& b) {
 
 // r = a - b mod p
 BLS_HD BLS_INLINE void fp_sub(fp& r, const fp& a, const fp& b) {
+  BLS_CONTRACT(fp_canonical(a) && fp_canonical(b), "fp_sub: an operand is not canonical");
   uint32_t d[12];
   int64_t br = 0;
 #pragma unroll
@@ -179,13 +227,36 @@ BLS_HD BLS_INLINE void fp_neg(fp& r, const fp& a) {
   fp_set_zero(z);
   fp_sub(r, z, a);
 }
+#if defined(BLS_CONTRACT_CHECK)
+// the contract build: unreduced, as on the device (a + b, a + (p - b) for canonical a, b)
+BLS_HD BLS_INLINE void fp_add_lazy(fp& r, const fp& a, const fp& b) {
+  BLS_CONTRACT(fp_canonical(a) && fp_canonical(b), "fp_add_lazy: an operand is not canonical");
+  uint64_t c = 0;
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)a.v[i] + b.v[i];
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+BLS_HD BLS_INLINE void fp_sub_lazy(fp& r, const fp& a, const fp& b) {
+  BLS_CONTRACT(fp_canonical(a) && fp_canonical(b), "fp_sub_lazy: an operand is not canonical");
+  int64_t c = 0;
+  for (int i = 0; i < 12; ++i) {
+    c += (int64_t)a.v[i] + (int64_t)P_LIMBS[i] - (int64_t)b.v[i];
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+#else
 // host builds keep every value canonical
 BLS_HD BLS_INLINE void fp_add_lazy(fp& r, const fp& a, const fp& b) { fp_add(r, a, b); }
 BLS_HD BLS_INLINE void fp_sub_lazy(fp& r, const fp& a, const fp& b) { fp_sub(r, a, b); }
 #endif
+#endif
 
 // r = a / 2 mod p (Montgomery form is preserved: (aR)/2 = (a/2)R): a + p when a is odd, then one right shift.
 BLS_HD BLS_INLINE void fp_half(fp& r, const fp& a) {
+  BLS_CONTRACT(fp_canonical(a), "fp_half: operand not canonical");
   const uint32_t m = 0u - (a.v[0] & 1u);
   uint32_t t[12];
   uint64_t c = 0;
@@ -356,6 +427,12 @@ static inline void fp_mul_impl64(fp& r, const fp& a, const fp& b) {
 #endif
 BLS_HD BLS_NOINLINE fp fp_mul_v(fp a, fp b) {
   BLS_COUNT_MUL();
+#if defined(BLS_CONTRACT_CHECK)
+  BLS_CONTRACT(fp_product_operand(a) && fp_product_operand(b), "fp_mul: an operand is not below 2p and 2^382");
+  g_contract_lazy_operands += !fp_canonical(a) || !fp_canonical(b);
+  fp_reduce_2p(a, a);
+  fp_reduce_2p(b, b);
+#endif
   fp r;
 #if defined(BLS_HOST_FAST_MUL)
   fp_mul_impl64(r, a, b);
@@ -366,6 +443,10 @@ BLS_HD BLS_NOINLINE fp fp_mul_v(fp a, fp b) {
 }
 BLS_HD BLS_NOINLINE fp fp_sqr_v(fp a) {
   BLS_COUNT_SQR();
+#if defined(BLS_CONTRACT_CHECK)
+  BLS_CONTRACT(fp_product_operand(a), "fp_sqr: the operand is not below 2p and 2^382");
+  fp_reduce_2p(a, a);
+#endif
   fp r;
 #if defined(BLS_HOST_FAST_MUL)
   fp_mul_impl64(r, a, a);

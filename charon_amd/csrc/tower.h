@@ -206,8 +206,24 @@ BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
   fp_from_vec(r.c1, c1);
 }
 #else
-BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
+BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a_in, const fp2& b_in) {
   // Karatsuba: 3 Fp products; the two sums only feed the third product, so they stay unreduced (fp_add_lazy)
+#if defined(BLS_CONTRACT_CHECK)
+  // the device routine's operands: below 2^382 each, and 2p - b1 formed inside it (b1 <= 2p)
+  BLS_CONTRACT(fp_product_operand(a_in.c0) && fp_product_operand(a_in.c1) && fp_product_operand(b_in.c0) &&
+                   fp_product_operand(b_in.c1),
+               "fp2_mul: an operand is not below 2p and 2^382");
+  g_contract_lazy_operands += !fp_canonical(a_in.c0) || !fp_canonical(a_in.c1) || !fp_canonical(b_in.c0) ||
+                              !fp_canonical(b_in.c1);
+  fp2 a, b;
+  fp_reduce_2p(a.c0, a_in.c0);
+  fp_reduce_2p(a.c1, a_in.c1);
+  fp_reduce_2p(b.c0, b_in.c0);
+  fp_reduce_2p(b.c1, b_in.c1);
+#else
+  const fp2& a = a_in;
+  const fp2& b = b_in;
+#endif
   fp t0, t1, t2, s0, s1;
   fp_mul(t0, a.c0, b.c0);
   fp_mul(t1, a.c1, b.c1);
@@ -286,7 +302,11 @@ BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
   fp_from_vec(r.c1, c1);
 }
 #else
-BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) { fp2_sqr_c(r, a); }
+BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
+  // the device routine forms (a0 + a1), (a0 + p - a1) and 2 a1 inside it: canonical operands only
+  BLS_CONTRACT(fp_canonical(a.c0) && fp_canonical(a.c1), "fp2_sqr: an operand is not canonical");
+  fp2_sqr_c(r, a);
+}
 #endif
 // The cyclotomic squaring's Fp2 squarings use the three-product C form: inside the inlined exponentiation loop the
 // routine's 64 pinned registers cost more spills than it saves (op_probe: fp12_cyc_exp_xabs 5.86M -> 5.64M cycles).

@@ -69,13 +69,45 @@ def cpu_baseline_lib():
 
 
 _lib = None
+# HIPBLS_HOST_CONTRACT=1 (tests/test_operand_contract.py): lib() is the BLS_CONTRACT_CHECK build, which counts every
+# product / add / sub whose operands break the device routines' contracts (field.h BLS_CONTRACT); at exit the count
+# and the first violation go to HIPBLS_HOST_CONTRACT_OUT.
+CONTRACT = os.environ.get("HIPBLS_HOST_CONTRACT") == "1"
+CT_LIB = os.path.join(HERE, "native", "libhost_ops_contract.so")
+
+
+def _contract_lib():
+    deps = [SRC] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    if not os.path.exists(CT_LIB) or any(os.path.getmtime(d) > os.path.getmtime(CT_LIB) for d in deps):
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-DBLS_CONTRACT_CHECK", "-o",
+                               CT_LIB + ".tmp", SRC])
+        os.replace(CT_LIB + ".tmp", CT_LIB)
+    L = ctypes.CDLL(CT_LIB)
+    L.ht_contract_violations.restype = ctypes.c_uint64
+    L.ht_contract_first.restype = ctypes.c_char_p
+    L.ht_contract_lazy_operands.restype = ctypes.c_uint64
+    out = os.environ.get("HIPBLS_HOST_CONTRACT_OUT")
+    if out:
+        import atexit
+        import json
+
+        def dump():
+            first = L.ht_contract_first()
+            with open(out, "w") as f:
+                json.dump({"violations": L.ht_contract_violations(), "first": first.decode() if first else None,
+                           "lazy_operands": L.ht_contract_lazy_operands()}, f)
+        atexit.register(dump)
+    return L
 
 
 def lib():
     global _lib
     if _lib is None:
-        build()
-        _lib = ctypes.CDLL(LIB)
+        if CONTRACT:
+            _lib = _contract_lib()
+        else:
+            build()
+            _lib = ctypes.CDLL(LIB)
     return _lib
 
 

@@ -11,7 +11,18 @@ static uint32_t g_g1m_min = 64;     // G1 MSM threshold (ht_rlcb_set_g1_min; the
 namespace bls {
 thread_local uint64_t g_fp_mul_count = 0;
 thread_local uint64_t g_fp_sqr_count = 0;
+#if defined(BLS_CONTRACT_CHECK)
+uint64_t g_contract_violations = 0;
+const char* g_contract_first = nullptr;
+uint64_t g_contract_lazy_operands = 0;
+#endif
 }  // namespace bls
+#if defined(BLS_CONTRACT_CHECK)
+// operand-contract violations counted by the BLS_CONTRACT_CHECK build (field.h), and the first one's description
+extern "C" uint64_t ht_contract_violations(void) { return bls::g_contract_violations; }
+extern "C" const char* ht_contract_first(void) { return bls::g_contract_first; }
+extern "C" uint64_t ht_contract_lazy_operands(void) { return bls::g_contract_lazy_operands; }
+#endif
 
 using namespace bls;
 
@@ -637,6 +648,17 @@ extern "C" int ht_rlcb_verify(const uint8_t* pks, const uint8_t* sigs, const uin
 }
 
 // ---- binary-GCD inversion (field.h fp_inv) against the Fermat power, on plain-limb inputs ------------------
+// one fp_mul on raw little-endian limbs (no range check of its own: tests/test_operand_contract.py)
+extern "C" void ht_fp_mul_raw(const uint32_t* a12, const uint32_t* b12, uint32_t* out12) {
+  fp a, b, r;
+  for (int i = 0; i < 12; ++i) {
+    a.v[i] = a12[i];
+    b.v[i] = b12[i];
+  }
+  fp_mul(r, a, b);
+  for (int i = 0; i < 12; ++i) out12[i] = r.v[i];
+}
+
 extern "C" void ht_fp_inv(const uint32_t* x12, int gcd, uint32_t* out12) {
   fp x, r;
   for (int i = 0; i < 12; ++i) x.v[i] = x12[i];
