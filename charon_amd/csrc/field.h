@@ -366,12 +366,35 @@ __device__ __forceinline__ uint32_t fp2p_bfi(uint32_t m, uint32_t a, uint32_t b)
   return r;
 }
 #endif
+// The routines read p from s16-s27 and -p^-1 mod 2^32 from s28 (tools/gen_fp_asm.py P_SGPR): the callers hold
+// them there -- loaded from constant memory, uniform values the compiler keeps in those SGPRs across
+// calls -- as inputs of every call, so the thirteen scalar moves leave the routines (each a full issue slot at one
+// wave per SIMD, tools/isa_probe.hip).  The call's own address arithmetic then uses s[36:37].
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+static __constant__ uint32_t bls_p_sgpr[16] __attribute__((aligned(64))) = {0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau, 0xfffcfffdu, 0x00000000u, 0x00000000u, 0x00000000u};
+// readfirstlane at each call: the values are uniform, and it keeps them scalar where the optimizer merged copies of
+// them across divergent branches (a merged value is a VGPR, which an SGPR operand cannot take)
+__device__ __forceinline__ uint32_t bls_p_word(int k) { return __builtin_amdgcn_readfirstlane(bls_p_sgpr[k]); }
+__device__ __forceinline__ u32x8 bls_p_lo() {
+  u32x8 v;
+  v.s0 = bls_p_word(0); v.s1 = bls_p_word(1); v.s2 = bls_p_word(2); v.s3 = bls_p_word(3);
+  v.s4 = bls_p_word(4); v.s5 = bls_p_word(5); v.s6 = bls_p_word(6); v.s7 = bls_p_word(7);
+  return v;
+}
+__device__ __forceinline__ u32x4v bls_p_hi() {
+  u32x4v v;
+  v.s0 = bls_p_word(8); v.s1 = bls_p_word(9); v.s2 = bls_p_word(10); v.s3 = bls_p_word(11);
+  return v;
+}
+#define BLS_P_SGPR_IN "{s[16:23]}"(bls_p_lo()), "{s[24:27]}"(bls_p_hi()), "{s28}"(bls_p_word(12))
 #define BLS_ASM_CALL(fn)                                                                           \
-  "s_getpc_b64 s[16:17]\n\ts_add_u32 s16, s16, " fn "@rel32@lo+4\n\ts_addc_u32 s17, s17, " fn \
-  "@rel32@hi+12\n\ts_swappc_b64 s[30:31], s[16:17]\n\t"
+  "s_getpc_b64 s[36:37]\n\ts_add_u32 s36, s36, " fn "@rel32@lo+4\n\ts_addc_u32 s37, s37, " fn \
+  "@rel32@hi+12\n\ts_swappc_b64 s[30:31], s[36:37]\n\t"
+#define BLS_CALL_CLOBBERS "s30", "s31", "s36", "s37", "scc"
 __device__ __forceinline__ static u32x12 fp_mul_dev(u32x12 a, u32x12 b) {
-  asm volatile(BLS_ASM_CALL("bls_fp_mul_rt") : "+{v[0:11]}"(a), "+{v[12:23]}"(b) : : BLS_FP_MUL_ASM_CLOBBERS,
-               "s30", "s31", "scc");
+  asm volatile(BLS_ASM_CALL("bls_fp_mul_rt") : "+{v[0:11]}"(a), "+{v[12:23]}"(b) : BLS_P_SGPR_IN
+               : BLS_FP_MUL_ASM_CLOBBERS, BLS_CALL_CLOBBERS);
   return a;
 }
 BLS_HD BLS_INLINE u32x12 fp_to_vec(const fp& a) {

@@ -175,8 +175,8 @@ BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
   asm volatile(BLS_ASM_CALL("bls_fp2_mul_half_rt")
                : "+{v[0:11]}"(a0), "+{v[12:23]}"(a1), "+{v[24:35]}"(b0), "+{v[36:47]}"(b1), "={v[52:63]}"(c),
                  "+{v76}"(hm)
-               :
-               : BLS_FP2_MUL_HALF_ASM_CLOBBERS, "s30", "s31", "scc");
+               : BLS_P_SGPR_IN
+               : BLS_FP2_MUL_HALF_ASM_CLOBBERS, BLS_CALL_CLOBBERS);
   fp2p_join(r, c, h);
 }
 BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
@@ -185,8 +185,8 @@ BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
   const uint32_t h = hm;
   asm volatile(BLS_ASM_CALL("bls_fp2_sqr_half_rt")
                : "+{v[0:11]}"(a0), "+{v[12:23]}"(a1), "={v[24:35]}"(c), "+{v76}"(hm)
-               :
-               : BLS_FP2_SQR_HALF_ASM_CLOBBERS, "s30", "s31", "scc");
+               : BLS_P_SGPR_IN
+               : BLS_FP2_SQR_HALF_ASM_CLOBBERS, BLS_CALL_CLOBBERS);
   fp2p_join(r, c, h);
 }
 #elif defined(__HIP_DEVICE_COMPILE__)
@@ -200,8 +200,8 @@ BLS_HD BLS_INLINE void fp2_mul(fp2& r, const fp2& a, const fp2& b) {
   asm volatile(BLS_ASM_CALL("bls_fp2_mul_rt")
                : "+{v[0:11]}"(a0), "+{v[12:23]}"(a1), "+{v[24:35]}"(b0), "+{v[36:47]}"(b1), "={v[52:63]}"(c1),
                  "={v[64:75]}"(c0)
-               :
-               : BLS_FP2_MUL_ASM_CLOBBERS, "s30", "s31", "scc");
+               : BLS_P_SGPR_IN
+               : BLS_FP2_MUL_ASM_CLOBBERS, BLS_CALL_CLOBBERS);
   fp_from_vec(r.c0, c0);
   fp_from_vec(r.c1, c1);
 }
@@ -245,7 +245,7 @@ BLS_HD BLS_INLINE void fp2_mul2(fp2& r, const fp2& x, const fp2& y, const fp2& z
                : "+{v[0:11]}"(x0), "+{v[12:23]}"(x1), "+{v[24:35]}"(y0), "+{v[36:47]}"(y1), "+{v[88:99]}"(z0),
                  "+{v[100:111]}"(z1), "+{v[112:123]}"(w0), "+{v[124:135]}"(w1), "={v[52:63]}"(c1), "={v[64:75]}"(c0)
                :
-               : BLS_FP2_MUL2_ASM_CLOBBERS, "s30", "s31", "scc");
+               : BLS_FP2_MUL2_ASM_CLOBBERS, BLS_CALL_CLOBBERS);
   fp_from_vec(r.c0, c0);
   fp_from_vec(r.c1, c1);
 }
@@ -259,7 +259,7 @@ BLS_HD BLS_INLINE void fp2_mul3(fp2& r, const fp2& x, const fp2& y, const fp2& z
                  "+{v[100:111]}"(z1), "+{v[112:123]}"(w0), "+{v[124:135]}"(w1), "+{v[136:147]}"(u0),
                  "+{v[148:159]}"(u1), "+{v[160:171]}"(t0), "+{v[172:183]}"(t1), "={v[52:63]}"(c1), "={v[64:75]}"(c0)
                :
-               : BLS_FP2_MUL2_ASM_CLOBBERS, "s30", "s31", "scc");
+               : BLS_FP2_MUL2_ASM_CLOBBERS, BLS_CALL_CLOBBERS);
   fp_from_vec(r.c0, c0);
   fp_from_vec(r.c1, c1);
 }
@@ -296,8 +296,8 @@ BLS_HD BLS_INLINE void fp2_sqr(fp2& r, const fp2& a) {
   u32x12 a0 = fp_to_vec(a.c0), a1 = fp_to_vec(a.c1), c0, c1;
   asm volatile(BLS_ASM_CALL("bls_fp2_sqr_rt")
                : "+{v[0:11]}"(a0), "+{v[12:23]}"(a1), "={v[24:35]}"(c0), "={v[36:47]}"(c1)
-               :
-               : BLS_FP2_SQR_ASM_CLOBBERS, "s30", "s31", "scc");
+               : BLS_P_SGPR_IN
+               : BLS_FP2_SQR_ASM_CLOBBERS, BLS_CALL_CLOBBERS);
   fp_from_vec(r.c0, c0);
   fp_from_vec(r.c1, c1);
 }

@@ -234,6 +234,7 @@ def schedule(ins, issue=4):
 OPERAND_BITS = 382
 ELIDE = True  # False: the round-5 streams (every carry caught)
 P_MOV64 = True  # False: p staged with twelve v_mov_b32
+P_SGPR = True  # False: every routine loads p and -p^-1 into s16-s28 itself (thirteen s_mov_b32)
 TOP_BOUND = (1 << (OPERAND_BITS - 352)) - 1  # an operand's top limb
 LIMB_MAX = 0xFFFFFFFF
 M64 = (1 << 64) - 1
@@ -312,6 +313,18 @@ def _comba(w, pairs, M, out, acc, elide=True):
         n_prev = st["n"]
 
 
+def _p_sgprs(w):
+    """p into s16-s27 and -p^-1 mod 2^32 into s28, or nothing with P_SGPR: the callers then hold them there (field.h
+    BLS_P_SGPR_IN: loaded once from constant memory, inputs of every routine call, never clobbered), and the thirteen
+    scalar moves -- a full issue slot each at one wave per SIMD (tools/isa_probe.hip) -- leave every call."""
+    if P_SGPR:
+        return
+    PINV32 = (-pow(P, -1, 1 << 32)) % (1 << 32)
+    for j in range(N32):
+        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL32[j]))
+    w("s_mov_b32 s28, 0x%08x" % PINV32)
+
+
 def _load_p(w, R):
     """p (s16-s27) into the VGPRs R(0..11): six v_mov_b64 from SGPR pairs (one issue slot per two limbs; every
     instruction of a one-wave-per-SIMD stream costs the same slot, tools/isa_probe.hip), or twelve v_mov_b32 with
@@ -340,9 +353,7 @@ def gen_mul(e64_select=True, elide=None):
     Sp = lambda j: "s%d" % (16 + j)
     out = []
     w = out.append
-    for j in range(N32):
-        w("s_mov_b32 %s, 0x%08x" % (Sp(j), PL[j]))
-    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    _p_sgprs(w)
     _comba(w, [(Aa, Bb)], Mm, Aa, 36, elide)
     _load_p(w, Mm)
     w("v_sub_co_u32_e32 v12, vcc, v0, v24")
@@ -520,9 +531,7 @@ def gen_fp2_sqr():
     A0, A1, C0, C1 = V(FP2S_A0), V(FP2S_A1), V(FP2S_C0), V(FP2S_C1)
     out = []
     w = out.append
-    for j in range(N32):
-        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
-    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    _p_sgprs(w)
     # d = (p - a1) + a0 into C1 (p staged in C0 first), s = a0 + a1 into C0, a1 <- 2 a1
     _load_p(w, C0)
     w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (C1(0), C0(0), A1(0)))
@@ -558,9 +567,7 @@ def gen_fp2_mul():
     A0, A1, B0, B1, C1, C0 = (V(FP2_A0), V(FP2_A1), V(FP2_B0), V(FP2_B1), V(FP2_C1), V(FP2_C0))
     out = []
     w = out.append
-    for j in range(N32):
-        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
-    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    _p_sgprs(w)
     P2L = [((2 * P) >> (32 * i)) & 0xFFFFFFFF for i in range(N32)]
     T = V(FP2_T)
     _gen_sop(w, A0, B1, A1, B0, C1)                    # c1 (raw, < 2p) in v[52:63]
@@ -611,9 +618,7 @@ def gen_fp2_mul_half():
     HM = "v%d" % FP2H_MASK
     out = []
     w = out.append
-    for j in range(N32):
-        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
-    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    _p_sgprs(w)
     for j in range(N32):                               # 2p staged in C (one constant-bus operand per carry step)
         w("v_mov_b32 %s, 0x%08x" % (C(j), P2L[j]))
     w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), B1(0)))
@@ -637,9 +642,7 @@ def gen_fp2_sqr_half():
     HM = "v%d" % FP2H_MASK
     out = []
     w = out.append
-    for j in range(N32):
-        w("s_mov_b32 s%d, 0x%08x" % (16 + j, PL[j]))
-    w("s_mov_b32 s28, 0x%08x" % PINV32)
+    _p_sgprs(w)
     _load_p(w, X)                                      # p staged in X
     w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (Y(0), X(0), A1(0)))
     for j in range(1, N32):                            # Y <- p - a1
@@ -781,6 +784,9 @@ def emulate(body, a, b, regs=None, strict=True):
     the register file starts from regs instead of a in v0.. and b in v12..  strict: a v_mad_u64_u32 whose
     carry-out is set must be followed by the v_addc that catches it (carry elision, _comba), else DroppedCarry."""
     v, s = ({}, {}) if regs is None else (regs, {})
+    for j in range(N32):  # the callers' SGPRs (P_SGPR): p and -p^-1 mod 2^32
+        s["s%d" % (16 + j)] = PL32[j]
+    s["s28"] = (-pow(P, -1, 1 << 32)) % (1 << 32)
     pending = [None]
     M32, M64 = 0xFFFFFFFF, (1 << 64) - 1
     if regs is None:
@@ -928,17 +934,16 @@ def emit_header(path, bodies, extra=()):
             sep = "\\n\\t" if k + 1 < len(body) else ""
             lines.append('  "%s%s" \\' % (ins, sep))
         lines.append("")
-    clob = ", ".join('"v%d"' % r for r in range(24, 40)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
+    sg = "" if P_SGPR else ", " + ", ".join('"s%d"' % r for r in range(16, 29))  # s16-s28: inputs with P_SGPR
+    clob = ", ".join('"v%d"' % r for r in range(24, 40)) + ', "vcc"' + sg
     lines.append("#define BLS_FP_MUL_ASM_CLOBBERS %s" % clob)
-    clob2 = ", ".join('"v%d"' % r for r in list(range(48, 52)) + list(range(76, 88))) + ', "vcc", ' + \
-        ", ".join('"s%d"' % r for r in range(16, 29))
+    clob2 = ", ".join('"v%d"' % r for r in list(range(48, 52)) + list(range(76, 88))) + ', "vcc"' + sg
     lines.append("#define BLS_FP2_MUL_ASM_CLOBBERS %s" % clob2)
-    clob3 = ", ".join('"v%d"' % r for r in range(48, 64)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
+    clob3 = ", ".join('"v%d"' % r for r in range(48, 64)) + ', "vcc"' + sg
     lines.append("#define BLS_FP2_SQR_ASM_CLOBBERS %s" % clob3)
-    clob4 = ", ".join('"v%d"' % r for r in list(range(48, 52)) + list(range(64, 76))) + ', "vcc", ' + \
-        ", ".join('"s%d"' % r for r in range(16, 29))
+    clob4 = ", ".join('"v%d"' % r for r in list(range(48, 52)) + list(range(64, 76))) + ', "vcc"' + sg
     lines.append("#define BLS_FP2_MUL_HALF_ASM_CLOBBERS %s" % clob4)
-    clob5 = ", ".join('"v%d"' % r for r in range(36, 76)) + ', "vcc", ' + ", ".join('"s%d"' % r for r in range(16, 29))
+    clob5 = ", ".join('"v%d"' % r for r in range(36, 76)) + ', "vcc"' + sg
     lines.append("#define BLS_FP2_SQR_HALF_ASM_CLOBBERS %s" % clob5)
     for name, body in extra:
         lines.append("")
