@@ -85,8 +85,8 @@ def build(force=False, verbose=True, extra=(), out=LIB):
     measurements (loaded with HIPBLS_LIB=<path>); the product is the default in-tree build."""
     if not force and out == LIB and not stale(extra=extra):
         return LIB
-    # the four translation units compile in parallel (each a separate code object; the link combines them), then link
-    srcs = [os.path.join(CSRC, f) for f in ("hipbls.hip", "verify_lat.hip", "verify_hex.hip", "rlc_wide.hip")]
+    # the five translation units compile in parallel (each a separate code object; the link combines them), then link
+    srcs = [os.path.join(CSRC, f) for f in ("hipbls.hip", "verify_lat.hip", "verify_hex.hip", "rlc_wide.hip", "fav_wide.hip")]
     flags = _base_flags() + list(extra)
     # the build id (hipbls_build_id): digests of the sources and of the flags, checked before any GPU run
     flags += ['-DHIPBLS_SRC_SHA="%s"' % source_digest(), '-DHIPBLS_FLAGS_SHA="%s"' % flags_digest(extra)]

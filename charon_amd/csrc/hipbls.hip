@@ -78,9 +78,13 @@ __global__ void k_fav_prep8(const uint8_t* pks, uint64_t nkeys, const uint8_t* s
 namespace bls_hex {
 __global__ void k_verify_pair_lq16(const uint32_t* ws, uint64_t n, int32_t* status, uint32_t replicas, uint32_t* race,
                                    uint32_t epoch);
+
+}  // namespace bls_hex
+// FastAggregateVerify's check at two waves per SIMD (fav_wide.hip: verify_hex.hip again, namespace bls_hexw).
+namespace bls_hexw {
 __global__ void k_fav_pair_lq16(const uint32_t* pts, const int32_t* kcode, uint64_t nkeys, const uint64_t* goff,
                                 const uint32_t* ws, uint64_t G, int32_t* status);
-}  // namespace bls_hex
+}  // namespace bls_hexw
 namespace bls_fp2p {
 // LDS the S-factor workgroup reserves at launch and never touches: the chunk kernel's 36 KiB per workgroup (four per
 // CU), so a CU that hosts the S-factor wave takes at most three chunk waves and no SIMD runs two (a shared SIMD
@@ -339,6 +343,7 @@ struct KernelRef {
 #define KREF(k) {#k, reinterpret_cast<const void*>(&k)}
 #define KREF8(k) {#k, reinterpret_cast<const void*>(&bls_fp2p::k)}
 #define KREF16(k) {#k, reinterpret_cast<const void*>(&bls_hex::k)}
+#define KREF16W(k) {#k, reinterpret_cast<const void*>(&bls_hexw::k)}
 // Every kernel the library launches (tests/test_kernel_resources.py: the same set as both code objects hold, minus the
 // reserve kernels).
 const KernelRef kKernels[] = {
@@ -354,7 +359,7 @@ const KernelRef kKernels[] = {
     KREF(k_verify_fused), KREF(k_verify_keys), KREF(k_verify_pair_lg2), KREF(k_verify_pair_lq4),
     KREF(k_verify_pair_single), KREF(k_verify_prep), KREF(k_zero_sig_status), KREF8(k_g1m_miller8),
     KREF8(k_rlcb_final8), KREF8(k_rlcb_sfactor8), KREF8(k_verify_pair_lq8), KREF8(k_verify_prep8),
-    KREF16(k_verify_pair_lq16), KREF8(k_fav_prep8), KREF16(k_fav_pair_lq16),
+    KREF16(k_verify_pair_lq16), KREF8(k_fav_prep8), KREF16W(k_fav_pair_lq16),
 };
 #define RES(s) reinterpret_cast<const void*>(&k_scratch_reserve<s>)
 // 8 KiB to the per-lane budget (charon_amd/codeobj.py PRIVATE_SEGMENT_BUDGET, 13,104 B) in 256-byte steps: at most
@@ -367,6 +372,8 @@ const void* const kReserve[] = {
 #undef RES
 #undef KREF
 #undef KREF8
+#undef KREF16
+#undef KREF16W
 
 std::string kernel_names() {
   std::string s;
@@ -1606,7 +1613,7 @@ int launch_fav(Context& c, const uint8_t* d_pks, uint64_t nkeys, const uint64_t*
     });
     if (rc) return rc;
     rc = timed(c, "fav_lq16", s, [&] {
-      hipLaunchKernelGGL(bls_hex::k_fav_pair_lq16, dim3((unsigned)n_groups), dim3(kBlock), 0, s,
+      hipLaunchKernelGGL(bls_hexw::k_fav_pair_lq16, dim3((unsigned)n_groups), dim3(kBlock), 0, s,
                          (const uint32_t*)c.b_pts.p, (const int32_t*)c.b_pst.p, nkeys, d_goff,
                          (const uint32_t*)c.f_ws.p, n_groups, d_status);
     });

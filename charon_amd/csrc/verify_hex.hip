@@ -13,7 +13,11 @@
 // Everything here lives in namespace bls_hex (the kernel headers are included with `bls` renamed).
 #define BLS_FP2_PAIR 1
 #define BLS_HEX 1
+#ifdef BLS_HEX_FAV_WIDE  // fav_wide.hip: this file compiled again for FastAggregateVerify's check alone
+#define bls bls_hexw
+#else
 #define bls bls_hex
+#endif
 #include <hip/hip_runtime.h>
 
 #include "race.h"
@@ -24,6 +28,7 @@ namespace bls {
 
 constexpr int kHexBlock = 64;
 
+#ifndef BLS_HEX_FAV_WIDE
 // Stage 2 on sixteen lanes per item (k_verify_pair_lq8's body: the status from the decode codes in herumi's order,
 // then lq4_verify on lanes q = t & 3 with their twins and their second copies).  Replicas race as in verify_lat.hip
 // (race word race[3]).
@@ -59,6 +64,16 @@ __global__ void __launch_bounds__(kHexBlock) k_verify_pair_lq16(const uint32_t* 
   bls_race::finish();
 }
 
+#else
+// FastAggregateVerify's check at two waves per SIMD (BLS_FAV_WAVES, default two): a batch call that fills every SIMD
+// with two 256-register waves (the RLC item stage, rlc_wide.hip) otherwise starves this 512-register wave until that
+// stage ends -- a full SIMD frees only when both of its waves end together (C5's overlapped sync-committee check).
+#ifndef BLS_FAV_WAVES
+#define BLS_FAV_WAVES 2
+#endif
+#if BLS_FAV_WAVES > 1
+#define BLS_FAV_ATTR __attribute__((amdgpu_waves_per_eu(BLS_FAV_WAVES, BLS_FAV_WAVES)))
+#endif
 // FastAggregateVerify's check for a few groups (tbls/herumi.go:315-339), one workgroup per group g over the keys
 // [goff[g], goff[g + 1]) that verify_lat.hip k_fav_prep8 decoded: the 64 lanes sum them (strided mixed additions, then
 // an LDS tree, as kernels.h k_fav_batch), then lanes 0-15 run lq4_verify on the aggregate key in the sixteen-lane
@@ -66,7 +81,12 @@ __global__ void __launch_bounds__(kHexBlock) k_verify_pair_lq16(const uint32_t* 
 // lq4_verify's Miller loop, so the check runs whenever the signature decoded, with -g1 standing in for a key sum that
 // cannot be used), then a key's encoding error, then "verification failed" (also for an empty key list, an infinity
 // key or signature, a key sum at infinity).
-__global__ void __launch_bounds__(kHexBlock) k_fav_pair_lq16(const uint32_t* __restrict__ pts,
+#endif  // BLS_HEX_FAV_WIDE: k_verify_pair_lq16 here, k_fav_pair_lq16 in fav_wide.hip
+#ifdef BLS_HEX_FAV_WIDE
+#ifndef BLS_FAV_ATTR
+#define BLS_FAV_ATTR
+#endif
+__global__ void __launch_bounds__(kHexBlock) BLS_FAV_ATTR k_fav_pair_lq16(const uint32_t* __restrict__ pts,
                                                              const int32_t* __restrict__ kcode, uint64_t nkeys,
                                                              const uint64_t* __restrict__ goff,
                                                              const uint32_t* __restrict__ ws, uint64_t G,
@@ -146,4 +166,5 @@ __global__ void __launch_bounds__(kHexBlock) k_fav_pair_lq16(const uint32_t* __r
   if (tid == 0) status[g] = st;
 }
 
+#endif
 }  // namespace bls

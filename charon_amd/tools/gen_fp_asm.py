@@ -235,6 +235,7 @@ OPERAND_BITS = 382
 ELIDE = True  # False: the round-5 streams (every carry caught)
 P_MOV64 = True  # False: p staged with twelve v_mov_b32
 P_SGPR = True  # False: every routine loads p and -p^-1 into s16-s28 itself (thirteen s_mov_b32)
+ACC_IN_PLACE = True  # False: every result column's low word is moved out of v[acc:acc+1]
 TOP_BOUND = (1 << (OPERAND_BITS - 352)) - 1  # an operand's top limb
 LIMB_MAX = 0xFFFFFFFF
 M64 = (1 << 64) - 1
@@ -261,13 +262,29 @@ def _comba(w, pairs, M, out, acc, elide=True):
             if j < i:
                 body.append((M(j), Sp(i - j), LIMB_MAX * PL32[i - j]))
         start = 0 if i == 0 else (n_prev + 1) << 32
+        # Even result columns accumulate in place: the pair (out(i - 12), out(i - 11)) is the accumulator, so the
+        # column's low word is already result limb i - 12 (no move).  out(i - 11) is read by exactly one term of the
+        # column (its last use) -- that term goes first, before the first mad overwrites the register.
+        cacc = accp
+        alias = None
+        if elide and ACC_IN_PLACE and i >= N32 and i % 2 == 0:
+            lo_n, hi_n = int(out(i - N32)[1:]), int(out(i - N32 + 1)[1:])
+            if lo_n % 2 == 0 and hi_n == lo_n + 1:
+                ka = [k for k, t in enumerate(body) if out(i - N32 + 1) in (t[0], t[1])]
+                assert len(ka) == 1, (i, ka)
+                alias = ka[0]
+                cacc = "v[%d:%d]" % (lo_n, hi_n)
         if elide:
             free, s = [], start
-            for k in sorted(range(len(body)), key=lambda k: body[k][2]):
+            order = sorted(range(len(body)), key=lambda k: body[k][2])
+            if alias is not None:
+                order = [alias] + [k for k in order if k != alias]
+            for k in order:
                 if s + body[k][2] > M64:
                     break
                 free.append(k)
                 s += body[k][2]
+            assert alias is None or free[:1] == [alias], (i, "the in-place column's first term must be carry-free")
             seq = [(body[k], False) for k in free] + [(body[k], True) for k in range(len(body)) if k not in free]
         else:
             seq = [(t, not (i == 0 and k == 0)) for k, t in enumerate(body)]
@@ -275,8 +292,8 @@ def _comba(w, pairs, M, out, acc, elide=True):
         st = {"src": "0" if i == 0 else srcp, "init": False, "n": 0}
 
         def mac(x, y, need):
-            w("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (accp, x, y, st["src"]))
-            st["src"] = accp
+            w("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (cacc, x, y, st["src"]))
+            st["src"] = cacc
             if not need:
                 return
             if st["init"]:
@@ -297,7 +314,9 @@ def _comba(w, pairs, M, out, acc, elide=True):
             need = not elide or any(nd for _, nd in seq) or s + b > M64
             mac(M(i), Sp(0), need)
         if i == 2 * N32 - 2:
-            if elide:
+            if alias is not None:
+                pass  # limbs 10 and 11 are the accumulator
+            elif elide:
                 w("v_mov_b32 %s, %s" % (out(i - N32), lo))
                 w("v_mov_b32 %s, %s" % (out(N32 - 1), hi))
             else:
@@ -307,9 +326,12 @@ def _comba(w, pairs, M, out, acc, elide=True):
             break
         if not st["init"]:
             w("v_mov_b32 %s, 0" % cw)  # no carry caught in this column: the carried value's high word is 0
-        if i >= N32:
-            w("v_mov_b32 %s, %s" % (out(i - N32), lo))
-        w("v_mov_b32 %s, %s" % (mv, hi))
+        if alias is not None:
+            w("v_mov_b32 %s, %s" % (mv, out(i - N32 + 1)))
+        else:
+            if i >= N32:
+                w("v_mov_b32 %s, %s" % (out(i - N32), lo))
+            w("v_mov_b32 %s, %s" % (mv, hi))
         n_prev = st["n"]
 
 
