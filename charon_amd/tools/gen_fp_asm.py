@@ -576,9 +576,8 @@ def gen_fp2_sqr():
         w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), A0(0)))
         for j in range(1, N32):
             w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (T(j), C(j), A0(j)))
-        w("v_subb_co_u32_e64 %s, vcc, 0, 0, vcc" % A1(0))
         for j in range(N32):
-            w("v_bfi_b32 %s, %s, %s, %s" % (C(j), A1(0), C(j), T(j)))
+            w("v_cndmask_b32_e64 %s, %s, %s, vcc" % (C(j), T(j), C(j)))
     return out
 
 
@@ -604,9 +603,8 @@ def gen_fp2_mul():
         w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), B1(0)))
         for j in range(1, N32):
             w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (T(j), C(j), B1(j)))
-        w("v_subb_co_u32_e64 v48, vcc, 0, 0, vcc")
         for j in range(N32):
-            w("v_bfi_b32 %s, v48, %s, %s" % (C(j), C(j), T(j)))
+            w("v_cndmask_b32_e64 %s, %s, %s, vcc" % (C(j), T(j), C(j)))
     return out
 
 
@@ -621,14 +619,13 @@ def gen_fp2_mul():
 FP2H_MASK, FP2H_OUT, FP2HS_OUT = 76, 52, 24
 
 
-def _final_sub(w, C, PR, T, mask):
-    """C <- C - p when that does not borrow (C < 2p -> canonical); PR holds p, T is scratch, mask a VGPR."""
+def _final_sub(w, C, PR, T, mask=None):
+    """C <- C - p when that does not borrow (C < 2p -> canonical); PR holds p, T is scratch."""
     w("v_sub_co_u32_e32 %s, vcc, %s, %s" % (T(0), C(0), PR(0)))
     for j in range(1, N32):
         w("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (T(j), C(j), PR(j)))
-    w("v_subb_co_u32_e64 %s, vcc, 0, 0, vcc" % mask)
-    for j in range(N32):
-        w("v_bfi_b32 %s, %s, %s, %s" % (C(j), mask, C(j), T(j)))
+    for j in range(N32):  # the borrow selects straight from VCC (the e64 form: one slot, unlike the VOP2 one)
+        w("v_cndmask_b32_e64 %s, %s, %s, vcc" % (C(j), T(j), C(j)))
 
 
 def gen_fp2_mul_half():
@@ -704,9 +701,8 @@ def gen_add():
     w.append("v_sub_co_u32_e32 %12, vcc, %0, %49")
     for i in range(1, 12):
         w.append("v_subb_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (12 + i, i, 49 + i))
-    w.append("v_subb_co_u32_e64 %24, vcc, 0, 0, vcc")
-    for i in range(12):
-        w.append("v_bfi_b32 %%%d, %%24, %%%d, %%%d" % (i, i, 12 + i))
+    for i in range(12):  # keep s where s - p borrows (VCC), else s - p; %24 is left unused
+        w.append("v_cndmask_b32_e64 %%%d, %%%d, %%%d, vcc" % (i, 12 + i, i))
     return w
 
 
@@ -722,9 +718,8 @@ def gen_sub(neg=False):
         w.append("v_sub_co_u32_e32 %0, vcc, %25, %37")
         for i in range(1, 12):
             w.append("v_subb_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (i, 25 + i, 37 + i))
-    w.append("v_subb_co_u32_e64 %24, vcc, 0, 0, vcc")
-    for i in range(12):
-        w.append("v_and_b32_e32 %%%d, %%24, %%%d" % (12 + i, pb + i))
+    for i in range(12):  # p where a - b borrowed (VCC), else 0; %24 is left unused
+        w.append("v_cndmask_b32_e64 %%%d, 0, %%%d, vcc" % (12 + i, pb + i))
     w.append("v_add_co_u32_e32 %0, vcc, %0, %12")
     for i in range(1, 12):
         w.append("v_addc_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (i, i, 12 + i))
@@ -790,6 +785,8 @@ def emulate_positional(body, outs, ins):
             reg[d] = (m & rd(o[2])) | (~m & M32 & rd(o[3]))
         elif op == "v_and_b32_e32":
             reg[d] = rd(o[1]) & rd(o[2])
+        elif op == "v_cndmask_b32_e64":
+            reg[d] = rd(o[2]) if rd(o[3]) else rd(o[1])
         else:
             raise ValueError(ins_)
     return [reg[k] for k in outs]
